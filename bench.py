@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""bench.py — GiB/s of device-resident chunk unshuffle+reduce (f32 sum) on MI355X.
+
+Workload (BASELINE.json configs[1], "c2"): one step = one 64 MiB chunk of 16 Mi f32 values stored
+big-endian and byte-shuffled (element_size 4), reduced with `sum` by one launch of the fused
+unshuffle + byte-swap + f64-accumulated sum kernel.  Inputs are resident in HBM before timing; 8
+distinct chunks (512 MiB > the 256 MiB Infinity Cache) are rotated so every step streams from HBM.
+Ranks (one per GPU, torchrun) each process their own chunks: weak scaling, no data-path collective
+(the control-plane barrier / max-time reduction uses gloo).
+
+Also reported (extra.c4_batch): BASELINE configs[3] — a batch of 1024 independent 4 MiB shuffled f32
+chunks summed by one launch per step, the batch split across ranks (strong scaling of that batch).
+
+Roofline: bytes_alg per launch = n_elements * 4 B read (unshuffle / byte swap add no algorithmic
+bytes; the 16 B result is negligible) / average kernel duration from HIP events recorded on the
+launch stream around every step of the timed region; peak = 8.0 TB/s HBM3E (MI355X_MICROARCH.md).
+`traffic` comes from a rocprofv3 PMC pass (profiles/*_pmc.json) when one is committed.
+cpu_baseline: the oracle (CPU restatement of the reference's sequential path) on 1 host core.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (str(ROOT / "reductionist-rs_amd"), str(ROOT)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GIB = float(1 << 30)
+PEAK_GBS = 8000.0          # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md "Chip-level parameters")
+C2_ELEMS = 16 * 1024 * 1024
+C2_BYTES = C2_ELEMS * 4
+N_BUF = 8
+C4_CHUNKS = 1024
+C4_ELEMS = 1024 * 1024
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--c4-steps", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c4", action="store_true")
+    return ap.parse_args()
+
+
+def shuffled_be_f32(torch, vals):
+    """values (…, n) f32 on device -> big-endian bytes, byte-shuffled with element_size 4
+    (src/filters/shuffle.rs:124-135 encoder), laid out (…, 4*n) uint8 contiguous."""
+    b = vals.contiguous().view(torch.uint8).reshape(*vals.shape, 4).flip(-1)       # big-endian
+    return b.transpose(-1, -2).contiguous().reshape(*vals.shape[:-1], 4 * vals.shape[-1])
+
+
+def traffic_from_profiles(tag):
+    p = ROOT / "profiles" / f"{tag}_pmc.json"
+    if p.exists():
+        try:
+            return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def cpu_baseline(seconds):
+    """Oracle on the host: unshuffle + byte swap + sequential f32 fold of one 64 MiB chunk."""
+    import numpy as np
+    from oracle import py_oracle as oracle
+    from reductionist_amd import _abi
+    rng = np.random.default_rng(0x5EED0004)
+    vals = rng.random(C2_ELEMS, dtype=np.float32)
+    data = vals.astype(">f4").view(np.uint8).reshape(C2_ELEMS, 4).T.copy().tobytes()
+    creq = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
+    lib = oracle.lib()
+    src = C.create_string_buffer(data, len(data))
+    body = (C.c_uint8 * 64)()
+    counts = (C.c_int64 * 8)()
+    info = _abi.rdx_response_info()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        st = lib.oracle_execute(C.addressof(creq.c), src, len(data), body, 64, counts, 8, C.byref(info))
+        assert st == 0
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 1000:
+            break
+    return {"value": round(reps * C2_BYTES / el / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x one 64 MiB chunk (16 Mi f32, big-endian, shuffle es=4), sum, sequential "
+                      f"oracle/rdx_oracle.cpp g++ -O2 on 1 host core, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+
+    from reductionist_amd import Engine, _abi
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    eng = Engine([local_rank])
+    ws = eng.workspace(local_rank)
+    lib = _abi.lib()
+    stream = torch.cuda.current_stream()
+    sh = C.c_void_p(stream.cuda_stream)
+
+    # ---- C2: 8 distinct 64 MiB chunks resident in HBM --------------------------------------------------
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0004 + rank)
+    vals = torch.rand(N_BUF, C2_ELEMS, device="cuda", generator=g, dtype=torch.float32)
+    chunks = shuffled_be_f32(torch, vals)
+    exact = vals.double().sum(dim=1).cpu()
+    del vals
+    bodies = torch.zeros(N_BUF, dtype=torch.float32, device="cuda")
+    counts = torch.zeros(N_BUF, dtype=torch.int64, device="cuda")
+    status = torch.zeros(N_BUF, dtype=torch.int32, device="cuda")
+    creq = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
+    info = _abi.rdx_response_info()
+    fn = lib.rdx_execute_device
+    argv = [(ws.ws, creq.ref, C.c_void_p(chunks[i].data_ptr()), C2_BYTES, C.c_void_p(bodies[i:].data_ptr()),
+             C.c_void_p(counts[i:].data_ptr()), C.c_void_p(status[i:].data_ptr()), sh, C.byref(info))
+            for i in range(N_BUF)]
+
+    def step(i):
+        st = fn(*argv[i % N_BUF])
+        if st:
+            raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    # correctness of what we time: every buffer vs an f64 reference sum (f32 tolerance)
+    got = bodies.double().cpu()
+    assert int(status.abs().sum()) == 0 and bool((counts.cpu() == C2_ELEMS).all())
+    tol = (exact.abs() * 2.0 ** -23 + 1e-3)
+    assert bool(((got - exact).abs() <= tol).all()), (got, exact)
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step(i)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = max_over_ranks(t1 - t0)
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    kern_avg_s = statistics.fmean(kern_ms) / 1e3
+    kern_med_s = statistics.median(kern_ms) / 1e3
+    value = args.steps * C2_BYTES * world / elapsed / GIB
+    achieved = C2_BYTES / kern_avg_s / 1e9
+
+    # ---- C4 (extra): 1024 x 4 MiB chunks, one batched launch per step ----------------------------------
+    extra = {}
+    if not args.no_c4:
+        n_local = C4_CHUNKS // world + (1 if rank < C4_CHUNKS % world else 0)
+        g.manual_seed(0x5EED1000 + rank)
+        v4 = torch.rand(n_local, C4_ELEMS, device="cuda", generator=g, dtype=torch.float32)
+        ex4 = v4.double().sum(dim=1).cpu()
+        # native byte order, shuffle es=4
+        c4 = v4.view(torch.uint8).reshape(n_local, C4_ELEMS, 4).transpose(1, 2).contiguous().reshape(n_local, -1)
+        del v4
+        b4 = torch.zeros(n_local, dtype=torch.float32, device="cuda")
+        n4 = torch.zeros(n_local, dtype=torch.int64, device="cuda")
+        s4 = torch.zeros(n_local, dtype=torch.int32, device="cuda")
+        creq4 = _abi.CRequest("sum", "float32", filters=[{"id": "shuffle", "element_size": 4}])
+        ptrs = [c4[i].data_ptr() for i in range(n_local)]
+        for _ in range(2):
+            ws.execute_batch_device(creq4, ptrs, 4 * C4_ELEMS, b4.data_ptr(), n4.data_ptr(), s4.data_ptr(),
+                                    stream.cuda_stream)
+        torch.cuda.synchronize()
+        assert bool((n4.cpu() == C4_ELEMS).all()) and int(s4.abs().sum()) == 0
+        assert bool(((b4.double().cpu() - ex4).abs() <= ex4.abs() * 2.0 ** -23 + 1e-3).all())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.c4_steps):
+            ws.execute_batch_device(creq4, ptrs, 4 * C4_ELEMS, b4.data_ptr(), n4.data_ptr(), s4.data_ptr(),
+                                    stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        el4 = max_over_ranks(t1 - t0)
+        k4 = e0.elapsed_time(e1) / 1e3 / args.c4_steps
+        extra["c4_batch"] = {
+            "workload": "1024 x 4 MiB f32 chunks, shuffle es=4, native order, sum; batch split over ranks",
+            "value": round(args.c4_steps * C4_CHUNKS * 4 * C4_ELEMS / el4 / GIB, 2), "unit": "GiB/s",
+            "scaling": "strong", "steps": args.c4_steps, "ms_per_step": round(el4 / args.c4_steps * 1e3, 4),
+            "chunks_per_rank": n_local,
+            "roofline_frac": round(n_local * 4 * C4_ELEMS / k4 / 1e9 / PEAK_GBS, 4)}
+        del c4
+
+    line = {
+        "metric": "GiB/s device-resident chunk unshuffle+reduce (f32 sum), 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic U[0,1) f32, big-endian, byte-shuffled (es=4)",
+        "config": {"workload": "c2: sum over one 64 MiB f32 chunk per step per GPU (16 Mi elements), "
+                               "byte shuffle es=4 + non-native (big) byte order, 8 rotating HBM-resident chunks",
+                   "chunk_bytes": C2_BYTES, "elements": C2_ELEMS, "parallelism": f"independent chunks x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_GBS, 4), "traffic": traffic_from_profiles("c2"),
+                     "kernel": "k_all_contig<float, OP_SUM, FUSED>", "kernel_us_avg": round(kern_avg_s * 1e6, 3),
+                     "kernel_us_median": round(kern_med_s * 1e6, 3), "bytes_alg_per_launch": C2_BYTES},
+        "extra": extra,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        line["cpu_baseline"]["nproc"] = os.cpu_count()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ws.close()
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

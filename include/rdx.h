@@ -1,0 +1,202 @@
+/*
+ * rdx.h — C ABI of the MI355X chunk filter+reduce engine (reductionist-rs drop-in).
+ *
+ * This is the boundary a Reductionist host (Rust, through `extern "C"`) binds to replace the
+ * synchronous part of a request: `operation<T>()` in src/app.rs:163-183, i.e.
+ *   filter_pipeline()            src/filter_pipeline.rs:19-34 (byte unshuffle; decompression is NOT on
+ *                                the device, see RDX_E_UNSUPPORTED)
+ *   validate_raw_size()          src/app.rs:169-172 -> src/models.rs:214-239
+ *   T::execute(&RequestData,..)  src/operation.rs:53-96 -> src/operations.rs (Count/Max/Min/Select/Sum)
+ *   build_array + slicing        src/array.rs:18-208 (byte-order swap, hyperslab)
+ *   missing-data predicate       src/types/missing.rs:114-122, src/operations.rs:25-33
+ *
+ * Plain C: no torch / HIP types in any signature. Device streams are passed as `void*`
+ * (a hipStream_t); device buffers as plain pointers.  Every entry point returns an rdx_status and
+ * never aborts the process; the host shim maps the status onto ActiveStorageError
+ * (src/error.rs:30-130) — see rdx_status below and INTEGRATION.md.
+ */
+#ifndef RDX_H
+#define RDX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDX_ABI_VERSION 1u
+/* Maximum rank of a request shape (the reference accepts any rank via ndarray IxDyn; 32 matches
+ * numpy's NPY_MAXDIMS and is far above any chunk layout seen in practice). */
+#define RDX_MAX_NDIM 32u
+
+/* ---- status codes (mapped onto src/error.rs ActiveStorageError by the host shim) ------------- */
+typedef enum rdx_status {
+    RDX_OK = 0,
+    RDX_E_INVALID_ARGUMENT = 1,    /* NULL pointer / bad enum / ABI version mismatch (caller bug)            */
+    RDX_E_REQUEST_VALIDATION = 2,  /* models.rs:179-313 validators and validate_raw_size (HTTP 400)          */
+    RDX_E_FROM_BYTES = 3,          /* array.rs:18-27 length not a multiple of / misaligned for T (HTTP 500)  */
+    RDX_E_SHAPE_INVALID = 4,       /* array.rs:58-63 ndarray from_shape failure (HTTP 400)                  */
+    RDX_E_INCOMPATIBLE_MISSING = 5,/* dvalue.rs:43-83 / missing.rs:47-80 conversion failure (HTTP 400)      */
+    RDX_E_SHUFFLE_LENGTH = 6,      /* shuffle.rs:21 assert_eq!(len % element_size, 0) — reference panics    */
+    RDX_E_NAN_UNORDERED = 7,       /* operations.rs:181-183,355-357 NaN in min/max — reference panics with
+                                      "unexpected undefined order error for min"                            */
+    RDX_E_UNSUPPORTED = 8,         /* compression != none (decompression stays on the CPU) / rank > 32     */
+    RDX_E_DEVICE = 9,              /* HIP runtime error                                                      */
+    RDX_E_OUT_OF_MEMORY = 10,      /* device or pinned allocation failed                                     */
+    RDX_E_BUFFER_TOO_SMALL = 11,   /* caller-provided output buffer smaller than rdx_plan() reported        */
+    RDX_E_NO_DEVICE = 12           /* no usable gfx950 device                                                */
+} rdx_status;
+
+/* ---- request enums (src/models.rs) ------------------------------------------------------------ */
+typedef enum rdx_op { /* routes /v2/{count,max,min,select,sum}, src/app.rs:61-71 */
+    RDX_OP_COUNT = 0, RDX_OP_MAX = 1, RDX_OP_MIN = 2, RDX_OP_SELECT = 3, RDX_OP_SUM = 4
+} rdx_op;
+
+typedef enum rdx_dtype { /* DType, src/models.rs:14-27 */
+    RDX_DTYPE_INT32 = 0, RDX_DTYPE_INT64 = 1, RDX_DTYPE_UINT32 = 2,
+    RDX_DTYPE_UINT64 = 3, RDX_DTYPE_FLOAT32 = 4, RDX_DTYPE_FLOAT64 = 5
+} rdx_dtype;
+
+typedef enum rdx_byte_order { /* Option<ByteOrder>, src/types/byte_order.rs:19-24 */
+    RDX_BYTE_ORDER_UNSET = 0, RDX_BYTE_ORDER_LITTLE = 1, RDX_BYTE_ORDER_BIG = 2
+} rdx_byte_order;
+
+typedef enum rdx_order { /* Option<Order>, src/models.rs:47-52 */
+    RDX_ORDER_UNSET = 0, RDX_ORDER_C = 1, RDX_ORDER_F = 2
+} rdx_order;
+
+typedef enum rdx_axes_kind { /* ReductionAxes, src/models.rs:122-127 */
+    RDX_AXES_ALL = 0, RDX_AXES_ONE = 1, RDX_AXES_MULTI = 2
+} rdx_axes_kind;
+
+typedef enum rdx_filter_id { /* Filter, src/models.rs:111-117 */
+    RDX_FILTER_SHUFFLE = 1, RDX_FILTER_SHUFFLE_SIMD = 2
+} rdx_filter_id;
+
+typedef enum rdx_compression { /* Option<Compression>, src/models.rs:98-105 */
+    RDX_COMPRESSION_NONE = 0, RDX_COMPRESSION_GZIP = 1, RDX_COMPRESSION_ZLIB = 2, RDX_COMPRESSION_BLOSC2 = 3
+} rdx_compression;
+
+typedef enum rdx_missing_kind { /* Missing<T>, src/types/missing.rs:31-42 */
+    RDX_MISSING_NONE = 0, RDX_MISSING_VALUE = 1, RDX_MISSING_VALUES = 2,
+    RDX_MISSING_VALID_MIN = 3, RDX_MISSING_VALID_MAX = 4, RDX_MISSING_VALID_RANGE = 5
+} rdx_missing_kind;
+
+/* numpy-semantics slice [start, end, stride], src/models.rs:77-92 */
+typedef struct rdx_slice {
+    int64_t start;
+    int64_t end;
+    int64_t stride;
+} rdx_slice;
+
+typedef struct rdx_filter {
+    uint32_t id;           /* rdx_filter_id */
+    uint32_t reserved;
+    uint64_t element_size; /* NOT validated by the reference; 0 or len % es != 0 -> RDX_E_SHUFFLE_LENGTH */
+} rdx_filter;
+
+/* Missing-data descriptor with values ALREADY converted to the request dtype (native byte order)
+ * by the host, using the reference's TryFromDValue rules (src/types/dvalue.rs:43-83);
+ * rdx_missing_from_f64/i64/u64 below implement those rules for hosts that want them. */
+typedef struct rdx_missing {
+    uint32_t kind;         /* rdx_missing_kind */
+    uint32_t reserved;
+    uint64_t n_values;     /* VALUE/VALID_MIN/VALID_MAX: 1, VALID_RANGE: 2 (min,max), VALUES: list length */
+    const void *values;    /* n_values elements of the request dtype */
+} rdx_missing;
+
+/* One request = one chunk (src/models.rs:133-176 RequestData, minus the transport fields). */
+typedef struct rdx_request {
+    uint32_t abi_version;  /* RDX_ABI_VERSION */
+    uint32_t op;           /* rdx_op */
+    uint32_t dtype;        /* rdx_dtype */
+    uint32_t byte_order;   /* rdx_byte_order */
+    uint32_t order;        /* rdx_order */
+    uint32_t axes_kind;    /* rdx_axes_kind */
+    uint32_t ndim;         /* 0 => `shape` absent: 1-D of len/sizeof(T) elements (array.rs:40) */
+    uint32_t n_axes;       /* ONE: 1; MULTI: list length (may be 0 = numpy axis=()) */
+    const uint64_t *shape;         /* ndim entries or NULL */
+    const rdx_slice *selection;    /* ndim entries or NULL */
+    const uint64_t *axes;          /* n_axes entries or NULL */
+    uint32_t n_filters;
+    uint32_t compression;          /* rdx_compression; anything but NONE -> RDX_E_UNSUPPORTED */
+    const rdx_filter *filters;     /* n_filters entries, in REQUEST order (decoded in reverse) */
+    rdx_missing missing;
+    uint32_t has_size;             /* RequestData.size is Some(..): app.rs:169 skips validate_raw_size */
+    uint32_t reserved;
+    uint64_t size;
+} rdx_request;
+
+/* Everything a caller needs to size the response (src/models.rs:316-351 Response). */
+typedef struct rdx_response_info {
+    uint32_t dtype;        /* response dtype (count -> INT64) */
+    uint32_t ndim;         /* rank of the response shape */
+    uint64_t shape[RDX_MAX_NDIM];
+    uint64_t body_bytes;   /* bytes of the response body (native-endian values) */
+    uint64_t n_counts;     /* number of i64 counts */
+} rdx_response_info;
+
+/* ---- library / device management -------------------------------------------------------------- */
+uint32_t rdx_abi_version(void);
+const char *rdx_status_string(rdx_status status);
+/* Number of visible gfx950 devices (0 when none / no driver). Never initialises anything else. */
+int rdx_device_count(void);
+
+/* A context is a pool over one or more devices (one chunk per device at a time, round-robin),
+ * each with its own stream(s), pinned staging and workspace.  Thread-safe: rdx_execute may be
+ * called concurrently from any number of host threads (src/app.rs:147-152 runs requests on
+ * Tokio/Rayon worker threads).  devices == NULL / n_devices == 0 => device 0. */
+typedef struct rdx_context rdx_context;
+rdx_status rdx_context_create(const int *devices, int n_devices, rdx_context **out);
+void rdx_context_destroy(rdx_context *ctx);
+
+/* ---- host logic (no device needed) -------------------------------------------------------------- */
+/* models.rs:242-313 validate_request_data (+ missing validation, missing.rs:47-80, with typed values). */
+rdx_status rdx_validate_request(const rdx_request *req);
+/* Shape / dtype / sizes of the response for a chunk of chunk_len bytes; runs every check
+ * operation<T>() would run before touching the data (app.rs:163-183, array.rs:18-63). */
+rdx_status rdx_plan(const rdx_request *req, uint64_t chunk_len, rdx_response_info *info);
+/* TryFromDValue (dvalue.rs:43-83): JSON number -> dtype value bytes (out: 8 bytes). */
+rdx_status rdx_missing_from_i64(uint32_t dtype, int64_t v, void *out);
+rdx_status rdx_missing_from_u64(uint32_t dtype, uint64_t v, void *out);
+rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out);
+
+/* ---- execution ------------------------------------------------------------------------------------ */
+/* Host-resident chunk in, host-resident response out (the drop-in for operation<T>()).
+ * `chunk` is borrowed read-only; body/counts are caller-provided with capacities from rdx_plan.
+ * Blocks until the response is in host memory. */
+rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req,
+                       const void *chunk, uint64_t chunk_len,
+                       void *body, uint64_t body_capacity,
+                       int64_t *counts, uint64_t counts_capacity,
+                       rdx_response_info *info);
+
+/* Device-resident path: everything already in HBM, nothing copied, asynchronous on `stream`.
+ * A workspace holds the per-stream scratch (partials, arrival tickets, unshuffle buffers); use one
+ * workspace per concurrently used stream. `d_status` (device, one uint32 per chunk, may be NULL)
+ * receives 0 or an rdx_status raised inside the kernels (RDX_E_NAN_UNORDERED). */
+typedef struct rdx_workspace rdx_workspace;
+rdx_status rdx_workspace_create(rdx_context *ctx, int device, rdx_workspace **out);
+void rdx_workspace_destroy(rdx_workspace *ws);
+
+rdx_status rdx_execute_device(rdx_workspace *ws, const rdx_request *req,
+                              const void *d_chunk, uint64_t chunk_len,
+                              void *d_body, int64_t *d_counts, uint32_t *d_status,
+                              void *stream, rdx_response_info *info);
+
+/* Batch of n_chunks independent chunks sharing one request (same dtype/shape/filters/selection),
+ * e.g. many chunks of one variable: one launch for the whole batch.  h_chunk_ptrs is a HOST array
+ * of n_chunks DEVICE pointers; chunk i's response goes to d_bodies + i*body_bytes,
+ * d_counts + i*n_counts, d_status + i. */
+rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req,
+                                    uint64_t n_chunks, const void *const *h_chunk_ptrs,
+                                    uint64_t chunk_len,
+                                    void *d_bodies, int64_t *d_counts, uint32_t *d_status,
+                                    void *stream, rdx_response_info *info);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RDX_H */

@@ -1,0 +1,342 @@
+// Reductions over ALL axes (axis unset: src/operations.rs:139-148, :303-318, :457-473, :622-632).
+//
+//  k_all_contig  — the selection is one ascending contiguous run of the chunk (whole chunk, or any
+//                  hyperslab that canonicalises to one run).  HBM-bound streaming:
+//                    * every lane reads 16 B per byte-plane (fused unshuffle, 4 or 8 planes) or
+//                      4 x 16 B of plain data per tile: each wave instruction reads 1 KiB contiguous;
+//                    * the byte transpose of the unshuffle and the byte-order swap happen in
+//                      registers with v_perm_b32 (two stages of 4 perms per 4 elements) — no LDS
+//                      round trip is needed because each lane already holds every plane of its
+//                      elements;
+//                    * per-lane accumulation, a 64-lane butterfly, a 4-wave LDS combine, and one
+//                      partial per workgroup folded by the last-arriving workgroup (no 2nd launch).
+//  k_all_strided — any other hyperslab: per-element index decomposition with magic division.
+#include "rdx_device.hpp"
+#include "rdx_kernels.hpp"
+
+namespace rdx {
+namespace {
+
+__device__ __forceinline__ uint32_t perm(uint32_t a, uint32_t b, uint32_t sel) {
+    return __builtin_amdgcn_perm(a, b, sel);
+}
+
+// 4x4 byte transpose: d[k] holds byte k of elements 0..3 (one dword per byte-plane).  Output w[m] is
+// element m assembled little-endian (selA/selB = 0x05040100/0x07060302) or byte-reversed
+// (0x00010405/0x02030607, the non-native byte order of array.rs:147-154).
+__device__ __forceinline__ void transpose4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t selA,
+                                           uint32_t selB, uint32_t w[4]) {
+    const uint32_t t01lo = perm(d1, d0, 0x05010400u), t01hi = perm(d1, d0, 0x07030602u);
+    const uint32_t t23lo = perm(d3, d2, 0x05010400u), t23hi = perm(d3, d2, 0x07030602u);
+    w[0] = perm(t23lo, t01lo, selA);
+    w[1] = perm(t23lo, t01lo, selB);
+    w[2] = perm(t23hi, t01hi, selA);
+    w[3] = perm(t23hi, t01hi, selB);
+}
+
+__device__ __forceinline__ uint32_t comp(const uint4 &v, int j) {
+    return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+
+template <typename T, int OP, bool MISS>
+__device__ __forceinline__ void consume(Red<T, OP> &r, T x, const KAllContig &a, uint64_t e) {
+    auto rank = [&]() -> int64_t { return a.r0 + (int64_t)(e - a.off) * a.rs; };
+    if constexpr (MISS) {
+        if (!included(a.miss, x, a.filter_semantics)) return;
+    }
+    if constexpr (OP == OP_COUNT) r.cnt += 1;
+    else r.add(x, rank);
+}
+
+// One tile step for one lane: the 16-byte granules this lane owns in tile `t`.
+//   fused   : element granule [e, e+16) with e = t*4096 + lane*16, one 16 B load per plane
+//   plain   : 4 granules of 16 B at byte offsets t*16384 + m*4096 + lane*16
+template <typename T, bool FUSED>
+struct Tile {
+    static constexpr int kPlanes = FUSED ? (int)sizeof(T) : 4;
+    uint4 p[kPlanes];
+};
+
+template <typename T, bool FUSED>
+__device__ __forceinline__ uint64_t tile_elems() {
+    return FUSED ? (uint64_t)kBlock * 16 : (uint64_t)kBlock * 64 / sizeof(T);
+}
+
+template <typename T, bool FUSED>
+__device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *base, uint64_t plane, uint64_t va,
+                                          uint64_t vb, uint64_t t, bool &full) {
+    const uint64_t te = tile_elems<T, FUSED>();
+    const uint64_t t0 = va + t * te;
+    full = t0 + te <= vb;
+    if constexpr (FUSED) {
+        const uint64_t e = t0 + threadIdx.x * 16;
+        if (e + 16 <= vb) {
+#pragma unroll
+            for (int k = 0; k < (int)sizeof(T); ++k)
+                tl.p[k] = *reinterpret_cast<const uint4 *>(base + (uint64_t)k * plane + e);
+        }
+    } else {
+        const uint8_t *b = base + t0 * sizeof(T);
+        const uint64_t lim = (vb - t0) * sizeof(T);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
+            if (o + 16 <= lim) tl.p[m] = *reinterpret_cast<const uint4 *>(b + o);
+        }
+    }
+}
+
+template <typename T, int OP, bool FUSED, bool MISS>
+__device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED> &tl, const KAllContig &a, uint64_t va,
+                                             uint64_t vb, uint64_t t, uint32_t selA, uint32_t selB) {
+    using U = typename UIntOf<T>::type;
+    const uint64_t te = tile_elems<T, FUSED>();
+    const uint64_t t0 = va + t * te;
+    const bool bswap = a.src.bswap;
+    if constexpr (FUSED) {
+        const uint64_t e = t0 + threadIdx.x * 16;
+        if (e + 16 > vb) return;
+        if constexpr (OP == OP_COUNT && !MISS) {
+            r.cnt += 16;
+            return;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t lo[4];
+            if constexpr (sizeof(T) == 4) {
+                transpose4(comp(tl.p[0], j), comp(tl.p[1], j), comp(tl.p[2], j), comp(tl.p[3], j), selA, selB, lo);
+                if constexpr (OP == OP_SUM && std::is_same_v<T, float> && !MISS) {
+                    // pairwise f64 partial of 4 elements (ILP), then one dependent add
+                    const double s01 = (double)__builtin_bit_cast(float, lo[0]) + (double)__builtin_bit_cast(float, lo[1]);
+                    const double s23 = (double)__builtin_bit_cast(float, lo[2]) + (double)__builtin_bit_cast(float, lo[3]);
+                    r.s += s01 + s23;
+                    r.cnt += 4;
+                } else {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) consume<T, OP, MISS>(r, from_u<T>((U)lo[m]), a, e + j * 4 + m);
+                }
+            } else {
+                // 8-byte elements: low dwords from planes 0-3, high from 4-7 (swapped + reversed
+                // for the non-native byte order).
+                uint32_t hi[4];
+                const int A = bswap ? 4 : 0, B = bswap ? 0 : 4;
+                transpose4(comp(tl.p[A + 0], j), comp(tl.p[A + 1], j), comp(tl.p[A + 2], j), comp(tl.p[A + 3], j),
+                           selA, selB, lo);
+                transpose4(comp(tl.p[B + 0], j), comp(tl.p[B + 1], j), comp(tl.p[B + 2], j), comp(tl.p[B + 3], j),
+                           selA, selB, hi);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    consume<T, OP, MISS>(r, from_u<T>((U)(((uint64_t)hi[m] << 32) | lo[m])), a, e + j * 4 + m);
+            }
+        }
+    } else {
+        const uint64_t lim = (vb - t0) * sizeof(T);
+        constexpr int kPer = 16 / sizeof(T);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
+            if (o + 16 > lim) continue;
+            const uint64_t e = t0 + o / sizeof(T);
+            if constexpr (OP == OP_COUNT && !MISS) {
+                r.cnt += kPer;
+                continue;
+            }
+            if constexpr (sizeof(T) == 4) {
+                uint32_t w[4] = {tl.p[m].x, tl.p[m].y, tl.p[m].z, tl.p[m].w};
+                if constexpr (OP == OP_SUM && std::is_same_v<T, float> && !MISS) {
+                    float f[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) f[q] = __builtin_bit_cast(float, bswap ? bswap_u(w[q]) : w[q]);
+                    r.s += ((double)f[0] + (double)f[1]) + ((double)f[2] + (double)f[3]);
+                    r.cnt += 4;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t u = bswap ? bswap_u(w[q]) : w[q];
+                        consume<T, OP, MISS>(r, from_u<T>((U)u), a, e + q);
+                    }
+                }
+            } else {
+                uint64_t w[2] = {((uint64_t)tl.p[m].y << 32) | tl.p[m].x, ((uint64_t)tl.p[m].w << 32) | tl.p[m].z};
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const uint64_t u = bswap ? bswap_u(w[q]) : w[q];
+                    consume<T, OP, MISS>(r, from_u<T>((U)u), a, e + q);
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int OP, bool FUSED, bool MISS>
+__global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
+    const uint32_t bpc = a.blocks_per_chunk;
+    const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
+    const uint8_t *base = chunk_base(a.src, chunk);
+    const bool bswap = a.src.bswap;
+    const uint32_t selA = bswap ? 0x00010405u : 0x05040100u;
+    const uint32_t selB = bswap ? 0x02030607u : 0x07060302u;
+
+    Red<T, OP> r;
+    r.init();
+    const uint64_t lo = a.off, hi = a.off + a.n;
+    // 16-byte granules: G elements per granule
+    constexpr uint64_t G = FUSED ? 16 : 16 / sizeof(T);
+    const bool vec_ok = ((uintptr_t)base % 16 == 0) && (!FUSED || a.src.plane % 16 == 0);
+    uint64_t va = hi, vb = hi;
+    if (vec_ok) {
+        va = (lo + G - 1) / G * G;
+        vb = hi / G * G;
+        if (va >= vb) va = vb = hi;
+    }
+    // scalar head and tail (< G elements each), owned by workgroup 0 of the chunk
+    if (b == 0) {
+        for (uint64_t e = lo + threadIdx.x; e < va; e += kBlock)
+            consume<T, OP, MISS>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
+        for (uint64_t e = vb + threadIdx.x; e < hi; e += kBlock)
+            consume<T, OP, MISS>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
+    }
+    // vector body: tiles of tile_elems() split into contiguous per-workgroup ranges
+    const uint64_t te = tile_elems<T, FUSED>();
+    const uint64_t ntiles = (vb - va + te - 1) / te;
+    const uint64_t per = (ntiles + bpc - 1) / bpc;
+    const uint64_t t_begin = (uint64_t)b * per;
+    const uint64_t t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
+    uint64_t t = t_begin;
+    for (; t + 1 < t_end; t += 2) {  // two tiles in flight per lane
+        Tile<T, FUSED> x0, x1;
+        bool f0, f1;
+        load_tile<T, FUSED>(x0, base, a.src.plane, va, vb, t, f0);
+        load_tile<T, FUSED>(x1, base, a.src.plane, va, vb, t + 1, f1);
+        consume_tile<T, OP, FUSED, MISS>(r, x0, a, va, vb, t, selA, selB);
+        consume_tile<T, OP, FUSED, MISS>(r, x1, a, va, vb, t + 1, selA, selB);
+    }
+    if (t < t_end) {
+        Tile<T, FUSED> x0;
+        bool f0;
+        load_tile<T, FUSED>(x0, base, a.src.plane, va, vb, t, f0);
+        consume_tile<T, OP, FUSED, MISS>(r, x0, a, va, vb, t, selA, selB);
+    }
+    finalize_all<T, OP>(r, a.out, chunk, bpc, b);
+}
+
+// ---- strided views ---------------------------------------------------------------------------------
+template <typename T, int OP, bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
+    const uint32_t bpc = a.blocks_per_chunk;
+    const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
+    const uint8_t *base = chunk_base(a.src, chunk);
+    const bool bswap = a.src.bswap;
+    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    const KView &v = a.view;
+    Red<T, OP> r;
+    r.init();
+    const uint64_t per = ((v.n + bpc - 1) / bpc + kBlock - 1) / kBlock * kBlock;
+    const uint64_t g_begin = (uint64_t)b * per;
+    const uint64_t g_end = g_begin + per < v.n ? g_begin + per : v.n;
+    constexpr int kUnroll = 4;
+    for (uint64_t g0 = g_begin + threadIdx.x; g0 < g_end; g0 += kBlock * kUnroll) {
+        int64_t off[kUnroll], rk[kUnroll];
+        bool ok[kUnroll];
+        T x[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t g = g0 + (uint64_t)u * kBlock;
+            ok[u] = g < g_end;
+            uint32_t q = (uint32_t)g;
+            int64_t o = v.base_off, rr = v.r0;
+            for (int k = 0; k < v.ndim; ++k) {
+                const uint32_t qn = udiv(q, v.div[k].magic);
+                const uint32_t idx = q - qn * v.count[k];
+                o += (int64_t)idx * v.vstride[k];
+                if constexpr (Red<T, OP>::kRank) rr += (int64_t)idx * v.rstride[k];
+                q = qn;
+            }
+            off[u] = o;
+            rk[u] = rr;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+            if (ok[u]) x[u] = load_elem<T, FUSED>(base, a.src.plane, bswap, (uint64_t)off[u]);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            if (!ok[u]) continue;
+            if (miss && !included(a.miss, x[u], a.filter_semantics)) continue;
+            if constexpr (OP == OP_COUNT) r.cnt += 1;
+            else r.add(x[u], [&]() { return rk[u]; });
+        }
+    }
+    finalize_all<T, OP>(r, a.out, chunk, bpc, b);
+}
+
+template <typename T, int OP>
+hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
+    const dim3 grid(a.blocks_per_chunk * n_chunks), block(kBlock);
+    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    if (a.src.fused) {
+        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, true, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_all_contig<T, OP, true, false>), grid, block, 0, s, a);
+    } else {
+        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, false, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_all_contig<T, OP, false, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+template <typename T, int OP>
+hipError_t launch_strided_t(const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
+    const dim3 grid(a.blocks_per_chunk * n_chunks), block(kBlock);
+    if (a.src.fused) hipLaunchKernelGGL((k_all_strided<T, OP, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_all_strided<T, OP, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_contig_op(uint32_t op, const KAllContig &a, uint32_t n, hipStream_t s) {
+    switch (op) {
+        case OP_COUNT: return launch_contig_t<T, OP_COUNT>(a, n, s);
+        case OP_MAX: return launch_contig_t<T, OP_MAX>(a, n, s);
+        case OP_MIN: return launch_contig_t<T, OP_MIN>(a, n, s);
+        case OP_SUM: return launch_contig_t<T, OP_SUM>(a, n, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t launch_strided_op(uint32_t op, const KAllStrided &a, uint32_t n, hipStream_t s) {
+    switch (op) {
+        case OP_COUNT: return launch_strided_t<T, OP_COUNT>(a, n, s);
+        case OP_MAX: return launch_strided_t<T, OP_MAX>(a, n, s);
+        case OP_MIN: return launch_strided_t<T, OP_MIN>(a, n, s);
+        case OP_SUM: return launch_strided_t<T, OP_SUM>(a, n, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_all_contig(uint32_t dtype, uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
+    switch (dtype) {
+        case RDX_DTYPE_INT32: return launch_contig_op<int32_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_INT64: return launch_contig_op<int64_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_UINT32: return launch_contig_op<uint32_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_UINT64: return launch_contig_op<uint64_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_FLOAT32: return launch_contig_op<float>(op, a, n_chunks, s);
+        case RDX_DTYPE_FLOAT64: return launch_contig_op<double>(op, a, n_chunks, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_all_strided(uint32_t dtype, uint32_t op, const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
+    switch (dtype) {
+        case RDX_DTYPE_INT32: return launch_strided_op<int32_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_INT64: return launch_strided_op<int64_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_UINT32: return launch_strided_op<uint32_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_UINT64: return launch_strided_op<uint64_t>(op, a, n_chunks, s);
+        case RDX_DTYPE_FLOAT32: return launch_strided_op<float>(op, a, n_chunks, s);
+        case RDX_DTYPE_FLOAT64: return launch_strided_op<double>(op, a, n_chunks, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace rdx

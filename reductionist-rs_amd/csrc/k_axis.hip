@@ -1,0 +1,194 @@
+// Reductions over a subset of axes: count_array_multi_axis / max_ / min_ / sum_array_multi_axis
+// (src/operations.rs:51-100, 213-268, 361-416, 532-583).  Output o (C order over the kept dims)
+// folds every element of its reduced sub-array.  The values are order independent except the f32/f64
+// sum (tolerance) and the ±0 tie of float min/max, which is resolved by the rank of the
+// zero in the reference's fold order: F order over the reduced axes in request order (fold_axis
+// over the first axis, then over the partials along the next, operations.rs:229-258).
+//
+//  k_axis_rows — innermost memory dim is reduced: one wave per (output, slice); lanes stride the
+//                reduced elements (coalesced), butterfly reduce.
+//  k_axis_cols — innermost memory dim is kept: one lane per (output, slice); consecutive lanes
+//                read consecutive addresses, each walks its reduced elements.
+//  k_axis_combine — when the reduced range is split into slices, fold the slices in order.
+#include "rdx_device.hpp"
+#include "rdx_kernels.hpp"
+
+namespace rdx {
+namespace {
+
+template <typename T, int OP>
+__device__ __forceinline__ void write_result(const KOut &out, uint64_t o, const Red<T, OP> &r) {
+    if constexpr (OP == OP_COUNT) reinterpret_cast<int64_t *>(out.body)[o] = r.cnt;
+    else reinterpret_cast<T *>(out.body)[o] = r.value();
+    out.counts[o] = r.cnt;
+    if constexpr (Red<T, OP>::kRank) {
+        if (r.nan && out.status)
+            __hip_atomic_fetch_or(out.status, (uint32_t)RDX_E_NAN_UNORDERED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void write_partial(const KOut &out, uint64_t idx, const Red<T, OP> &r) {
+    uint64_t w[kPartialWords];
+    r.to_words(w);
+#pragma unroll
+    for (int i = 0; i < kPartialWords; ++i) out.partials[idx * kPartialWords + i] = w[i];
+}
+
+__device__ __forceinline__ int64_t kept_offset(const KView &kv, uint32_t t, int64_t &out_index) {
+    int64_t off = kv.base_off, oi = 0;
+    uint32_t q = t;
+    for (int k = 0; k < kv.ndim; ++k) {
+        const uint32_t qn = udiv(q, kv.div[k].magic);
+        const uint32_t idx = q - qn * kv.count[k];
+        off += (int64_t)idx * kv.vstride[k];
+        oi += (int64_t)idx * kv.rstride[k];
+        q = qn;
+    }
+    out_index = oi;
+    return off;
+}
+
+template <bool RANK>
+__device__ __forceinline__ int64_t red_offset(const KView &rv, uint32_t r, int64_t &rank) {
+    int64_t off = 0, rk = rv.r0;
+    uint32_t q = r;
+    for (int k = 0; k < rv.ndim; ++k) {
+        const uint32_t qn = udiv(q, rv.div[k].magic);
+        const uint32_t idx = q - qn * rv.count[k];
+        off += (int64_t)idx * rv.vstride[k];
+        if (RANK) rk += (int64_t)idx * rv.rstride[k];
+        q = qn;
+    }
+    rank = rk;
+    return off;
+}
+
+template <typename T, int OP, bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
+    constexpr bool RANK = Red<T, OP>::kRank;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t items = a.n_out * a.slices;
+    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    const bool bswap = a.src.bswap;
+    for (uint64_t it = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); it < items; it += nw) {
+        const uint64_t o = it / a.slices, s = it - o * a.slices;
+        int64_t oi;
+        const int64_t koff = kept_offset(a.kept, (uint32_t)o, oi);
+        const uint64_t r_lo = s * a.n_red / a.slices, r_hi = (s + 1) * a.n_red / a.slices;
+        Red<T, OP> r;
+        r.init();
+        for (uint64_t ri = r_lo + lane; ri < r_hi; ri += 64) {
+            int64_t rk;
+            const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)ri, rk);
+            const T x = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
+            if (miss && is_missing(a.miss, x)) continue;
+            if constexpr (OP == OP_COUNT) r.cnt += 1;
+            else r.add(x, [&]() { return rk; });
+        }
+        wave_reduce(r);
+        if (lane == 0) {
+            if (a.slices == 1) write_result(a.out, (uint64_t)oi, r);
+            else write_partial(a.out, (uint64_t)oi * a.slices + s, r);
+        }
+    }
+}
+
+template <typename T, int OP, bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
+    constexpr bool RANK = Red<T, OP>::kRank;
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t s = blockIdx.y;
+    if (t >= a.n_out) return;
+    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    const bool bswap = a.src.bswap;
+    int64_t oi;
+    const int64_t koff = kept_offset(a.kept, (uint32_t)t, oi);
+    const uint64_t r_lo = s * a.n_red / a.slices, r_hi = (s + 1) * a.n_red / a.slices;
+    Red<T, OP> r;
+    r.init();
+    constexpr int kU = 4;
+    for (uint64_t r0 = r_lo; r0 < r_hi; r0 += kU) {
+        T x[kU];
+        int64_t rk[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (r0 + u < r_hi) {
+                const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)(r0 + u), rk[u]);
+                x[u] = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (r0 + u >= r_hi) continue;
+            if (miss && is_missing(a.miss, x[u])) continue;
+            if constexpr (OP == OP_COUNT) r.cnt += 1;
+            else r.add(x[u], [&]() { return rk[u]; });
+        }
+    }
+    if (a.slices == 1) write_result(a.out, (uint64_t)oi, r);
+    else write_partial(a.out, (uint64_t)oi * a.slices + s, r);
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void k_axis_combine(const KAxis a) {
+    const uint64_t o = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (o >= a.n_out) return;
+    Red<T, OP> acc;
+    acc.init();
+    for (uint32_t s = 0; s < a.slices; ++s) {
+        Red<T, OP> p;
+        p.from_words(a.out.partials + (o * a.slices + s) * kPartialWords);
+        acc.merge(p);
+    }
+    write_result(a.out, o, acc);
+}
+
+template <typename T, int OP>
+hipError_t launch_axis_t(const KAxis &a, int cus, hipStream_t st) {
+    const dim3 block(kBlock);
+    if (a.mode == 0) {
+        const uint64_t items = a.n_out * a.slices;
+        uint64_t blocks = (items + kBlock / 64 - 1) / (kBlock / 64);
+        const uint64_t cap = (uint64_t)cus * 16;
+        if (blocks > cap) blocks = cap;
+        if (blocks == 0) blocks = 1;
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true>), dim3((uint32_t)blocks), block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_rows<T, OP, false>), dim3((uint32_t)blocks), block, 0, st, a);
+    } else {
+        const dim3 grid((uint32_t)((a.n_out + kBlock - 1) / kBlock), a.slices);
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_cols<T, OP, false>), grid, block, 0, st, a);
+    }
+    if (a.slices > 1)
+        hipLaunchKernelGGL((k_axis_combine<T, OP>), dim3((uint32_t)((a.n_out + kBlock - 1) / kBlock)), block, 0, st, a);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_axis_op(uint32_t op, const KAxis &a, int cus, hipStream_t s) {
+    switch (op) {
+        case OP_COUNT: return launch_axis_t<T, OP_COUNT>(a, cus, s);
+        case OP_MAX: return launch_axis_t<T, OP_MAX>(a, cus, s);
+        case OP_MIN: return launch_axis_t<T, OP_MIN>(a, cus, s);
+        case OP_SUM: return launch_axis_t<T, OP_SUM>(a, cus, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_axis(uint32_t dtype, uint32_t op, const KAxis &a, int cus, hipStream_t s) {
+    switch (dtype) {
+        case RDX_DTYPE_INT32: return launch_axis_op<int32_t>(op, a, cus, s);
+        case RDX_DTYPE_INT64: return launch_axis_op<int64_t>(op, a, cus, s);
+        case RDX_DTYPE_UINT32: return launch_axis_op<uint32_t>(op, a, cus, s);
+        case RDX_DTYPE_UINT64: return launch_axis_op<uint64_t>(op, a, cus, s);
+        case RDX_DTYPE_FLOAT32: return launch_axis_op<float>(op, a, cus, s);
+        case RDX_DTYPE_FLOAT64: return launch_axis_op<double>(op, a, cus, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace rdx

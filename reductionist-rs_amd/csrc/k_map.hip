@@ -1,0 +1,137 @@
+// Element-wise kernels and the generic unshuffle.
+//
+//  k_map       — Select (src/operations.rs:487-526: every selected element in C order, or F order
+//                when the unsliced array is not standard layout, plus the non-missing count with
+//                missing_filter semantics) and reductions over axis=() (operations.rs:58-67,
+//                188-210: value + 0/1 count per element).
+//  k_unshuffle — src/filters/shuffle.rs:20-85 for any element_size into a scratch buffer: a workgroup
+//                stages a tile of TI elements x es byte-planes in LDS (coalesced plane reads),
+//                then writes TI*es contiguous output bytes.  Used for filter chains and for
+//                element_size != sizeof(dtype); the common es == sizeof(dtype) case is fused into
+//                the reduction kernels instead.
+#include "rdx_device.hpp"
+#include "rdx_kernels.hpp"
+
+namespace rdx {
+namespace {
+
+template <typename T, bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
+    const KView &v = a.view;
+    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    const bool bswap = a.src.bswap;
+    int64_t cnt = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < v.n; g += stride) {
+        uint32_t q = (uint32_t)g;
+        int64_t off = v.base_off;
+        for (int k = 0; k < v.ndim; ++k) {
+            const uint32_t qn = udiv(q, v.div[k].magic);
+            off += (int64_t)(q - qn * v.count[k]) * v.vstride[k];
+            q = qn;
+        }
+        const T x = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
+        if (a.kind == 0) {
+            reinterpret_cast<T *>(a.out.body)[g] = x;
+            cnt += (!miss || included(a.miss, x, true)) ? 1 : 0;
+        } else {
+            const int64_t c = (miss && is_missing(a.miss, x)) ? 0 : 1;
+            if (a.kind == 1) reinterpret_cast<T *>(a.out.body)[g] = x;
+            else reinterpret_cast<int64_t *>(a.out.body)[g] = c;
+            a.out.counts[g] = c;
+        }
+    }
+    if (a.kind == 0) {
+        // integer count: order-free, one device atomic per workgroup
+        __shared__ int64_t part[kBlock / 64];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) cnt += (int64_t)shfl_xor_u64((uint64_t)cnt, m);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t t = 0;
+            for (int k = 0; k < kBlock / 64; ++k) t += part[k];
+            if (t) __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(a.out.counts), (unsigned long long)t,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// out[i*es + k] = in[k*N + i]
+__global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                      uint64_t n, uint32_t es, uint32_t ti) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    for (uint64_t i0 = (uint64_t)blockIdx.x * ti; i0 < n; i0 += (uint64_t)gridDim.x * ti) {
+        const uint32_t cnt = (uint32_t)((n - i0) < ti ? (n - i0) : ti);
+        for (uint32_t k = 0; k < es; ++k)
+            for (uint32_t i = threadIdx.x; i < cnt; i += kBlock) tile[i * es + k] = in[(uint64_t)k * n + i0 + i];
+        __syncthreads();
+        const uint64_t obase = i0 * es;
+        const uint32_t bytes = cnt * es;
+        if ((((uintptr_t)out + obase) & 3) == 0) {
+            const uint32_t words = bytes / 4;
+            for (uint32_t w = threadIdx.x; w < words; w += kBlock)
+                reinterpret_cast<uint32_t *>(out + obase)[w] = reinterpret_cast<const uint32_t *>(tile)[w];
+            for (uint32_t q = words * 4 + threadIdx.x; q < bytes; q += kBlock) out[obase + q] = tile[q];
+        } else {
+            for (uint32_t q = threadIdx.x; q < bytes; q += kBlock) out[obase + q] = tile[q];
+        }
+        __syncthreads();
+    }
+}
+
+// element sizes too large for an LDS tile: direct byte gather
+__global__ __launch_bounds__(kBlock) void k_unshuffle_big(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                          uint64_t n, uint64_t es) {
+    const uint64_t total = n * es;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i = j / es, k = j - i * es;
+        out[j] = in[k * n + i];
+    }
+}
+
+template <typename T>
+hipError_t launch_map_t(const KMap &a, int cus, hipStream_t s) {
+    uint64_t blocks = (a.view.n + kBlock - 1) / kBlock;
+    const uint64_t cap = (uint64_t)cus * 16;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    if (a.src.fused) hipLaunchKernelGGL((k_map<T, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_map<T, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_map(uint32_t dtype, const KMap &a, int cus, hipStream_t s) {
+    switch (dtype) {
+        case RDX_DTYPE_INT32: return launch_map_t<int32_t>(a, cus, s);
+        case RDX_DTYPE_INT64: return launch_map_t<int64_t>(a, cus, s);
+        case RDX_DTYPE_UINT32: return launch_map_t<uint32_t>(a, cus, s);
+        case RDX_DTYPE_UINT64: return launch_map_t<uint64_t>(a, cus, s);
+        case RDX_DTYPE_FLOAT32: return launch_map_t<float>(a, cus, s);
+        case RDX_DTYPE_FLOAT64: return launch_map_t<double>(a, cus, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_unshuffle(const uint8_t *in, uint8_t *out, uint64_t len, uint64_t es, int cus, hipStream_t s) {
+    const uint64_t n = len / es;
+    if (n == 0) return hipSuccess;
+    if (es > 16384) {
+        uint64_t blocks = (len + kBlock - 1) / kBlock;
+        if (blocks > (uint64_t)cus * 16) blocks = (uint64_t)cus * 16;
+        hipLaunchKernelGGL(k_unshuffle_big, dim3((uint32_t)blocks), dim3(kBlock), 0, s, in, out, n, es);
+        return hipGetLastError();
+    }
+    uint32_t ti = (uint32_t)(16384 / es);
+    if (ti > 4096) ti = 4096;
+    if (ti == 0) ti = 1;
+    uint64_t blocks = (n + ti - 1) / ti;
+    if (blocks > (uint64_t)cus * 8) blocks = (uint64_t)cus * 8;
+    const size_t lds = (size_t)ti * es;
+    hipLaunchKernelGGL(k_unshuffle, dim3((uint32_t)blocks), dim3(kBlock), lds, s, in, out, n, (uint32_t)es, ti);
+    return hipGetLastError();
+}
+
+}  // namespace rdx

@@ -1,0 +1,329 @@
+// Device building blocks shared by the gfx950 kernels: element fetch (plain / fused byte-unshuffle,
+// optional byte-order swap), the missing-data predicate, the reduction state of each operation and
+// the deterministic cross-workgroup finalisation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <limits>
+#include <type_traits>
+
+#include "../../include/rdx.h"
+#include "rdx_kdesc.h"
+
+namespace rdx {
+
+template <typename T> struct UIntOf;
+template <> struct UIntOf<int32_t> { using type = uint32_t; };
+template <> struct UIntOf<uint32_t> { using type = uint32_t; };
+template <> struct UIntOf<float> { using type = uint32_t; };
+template <> struct UIntOf<int64_t> { using type = uint64_t; };
+template <> struct UIntOf<uint64_t> { using type = uint64_t; };
+template <> struct UIntOf<double> { using type = uint64_t; };
+
+template <typename T>
+__device__ __forceinline__ T from_u(typename UIntOf<T>::type u) { return __builtin_bit_cast(T, u); }
+template <typename T>
+__device__ __forceinline__ typename UIntOf<T>::type to_u(T v) { return __builtin_bit_cast(typename UIntOf<T>::type, v); }
+
+template <typename T>
+__device__ __forceinline__ T from_bits64(uint64_t b) {
+    using U = typename UIntOf<T>::type;
+    return from_u<T>((U)b);
+}
+
+__device__ __forceinline__ uint32_t bswap_u(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint64_t bswap_u(uint64_t x) { return __builtin_bswap64(x); }
+
+// Magic-number division of a 32-bit index (rdx_plan.cpp make_div).
+__device__ __forceinline__ uint32_t udiv(uint32_t n, uint64_t magic) {
+    return magic ? (uint32_t)__umul64hi((uint64_t)n, magic) : n;
+}
+
+__device__ __forceinline__ const uint8_t *chunk_base(const KSrc &s, uint32_t chunk) {
+    return s.ptrs ? s.ptrs[chunk] : s.base;
+}
+
+// One element by index e.  FUSED: byte k of element e is base[k*plane + e] (the inverse of
+// src/filters/shuffle.rs:32-83 evaluated on the fly); bswap: array.rs:147-154.
+template <typename T, bool FUSED>
+__device__ __forceinline__ T load_elem(const uint8_t *base, uint64_t plane, bool bswap, uint64_t e) {
+    using U = typename UIntOf<T>::type;
+    U u;
+    if constexpr (FUSED) {
+        u = 0;
+#pragma unroll
+        for (int k = 0; k < (int)sizeof(T); ++k) u |= (U)base[(uint64_t)k * plane + e] << (8 * k);
+    } else {
+        u = reinterpret_cast<const U *>(base)[e];
+    }
+    if (bswap) u = bswap_u(u);
+    return from_u<T>(u);
+}
+
+// ---- missing-data predicate ---------------------------------------------------------------------
+// Missing::is_missing (src/types/missing.rs:114-122).
+template <typename T>
+__device__ __forceinline__ bool is_missing(const KMissing &m, T x) {
+    switch (m.kind) {
+        case RDX_MISSING_VALUE: return x == from_bits64<T>(m.v0);
+        case RDX_MISSING_VALUES: {
+            if (m.n & 0x80000000u) {  // sorted device list: binary search (Vec::contains semantics)
+                uint32_t lo = 0, hi = m.n & 0x7fffffffu;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (from_bits64<T>(m.list[mid]) < x) lo = mid + 1;
+                    else hi = mid;
+                }
+                return lo < (m.n & 0x7fffffffu) && from_bits64<T>(m.list[lo]) == x;
+            }
+            bool hit = false;
+            for (uint32_t i = 0; i < m.n; ++i) hit |= x == from_bits64<T>(m.inl[i]);
+            return hit;
+        }
+        case RDX_MISSING_VALID_MIN: return x < from_bits64<T>(m.v0);
+        case RDX_MISSING_VALID_MAX: return x > from_bits64<T>(m.v0);
+        case RDX_MISSING_VALID_RANGE: return x < from_bits64<T>(m.v0) || x > from_bits64<T>(m.v1);
+        default: return false;
+    }
+}
+
+// Included in the operation?  fold semantics: !is_missing (operations.rs:227-241 etc.);
+// filter semantics: missing_filter (operations.rs:25-33, used by Count(All) and Select's count),
+// which differs only for NaN under valid_min/valid_max/valid_range (NaN >= min is false).
+template <typename T>
+__device__ __forceinline__ bool included(const KMissing &m, T x, bool filter_semantics) {
+    bool inc = !is_missing(m, x);
+    if constexpr (std::is_floating_point_v<T>) {
+        if (filter_semantics && m.kind >= RDX_MISSING_VALID_MIN) inc = inc && (x == x);
+    }
+    return inc;
+}
+
+// ---- reduction state ------------------------------------------------------------------------------
+// SUM:   integers wrap (release profile) — accumulated in u64 and truncated to T;
+//        f32 accumulated in f64 and rounded once; f64 Neumaier-compensated (operations.rs:622-632
+//        sums sequentially in T: results agree exactly for exactly-summable data and within the
+//        tolerance stated in DESIGN.md otherwise).
+// MAX/MIN: identity T::min_value()/max_value() (f32::MIN, not -inf), NaN -> RDX_E_NAN_UNORDERED,
+//        ±0 ties resolved by the fold-order rank of the zeros (max_by keeps the LAST equal element,
+//        min_by the FIRST; operations.rs:229-241,459-469).
+template <typename T, int OP>
+struct Red {
+    static constexpr bool kFloat = std::is_floating_point_v<T>;
+    static constexpr bool kRank = kFloat && (OP == OP_MAX || OP == OP_MIN);
+    double s, c;
+    uint64_t si;
+    T v;
+    int64_t cnt;
+    int64_t zp, zn;
+    uint32_t nan;
+
+    __device__ __forceinline__ void init() {
+        s = 0.0;
+        c = 0.0;
+        si = 0;
+        v = OP == OP_MAX ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
+        cnt = 0;
+        zp = zn = OP == OP_MAX ? -1 : INT64_MAX;
+        nan = 0;
+    }
+
+    __device__ __forceinline__ static void neumaier(double &s_, double &c_, double x) {
+        const double t = s_ + x;
+        if (fabs(s_) >= fabs(x)) c_ += (s_ - t) + x;
+        else c_ += (x - t) + s_;
+        s_ = t;
+    }
+
+    // value only (count handled by caller for batched adds)
+    template <class RankFn>
+    __device__ __forceinline__ void add_value(T x, RankFn &&rank) {
+        if constexpr (OP == OP_SUM) {
+            if constexpr (kFloat) {
+                if constexpr (sizeof(T) == 4) s += (double)x;
+                else neumaier(s, c, (double)x);
+            } else {
+                si += (uint64_t)x;
+            }
+        } else if constexpr (OP == OP_MAX || OP == OP_MIN) {
+            if constexpr (kFloat) {
+                nan |= (x != x);
+                if (x == T(0)) {
+                    const int64_t r = rank();
+                    if (__builtin_signbit(x)) zn = OP == OP_MAX ? max(zn, r) : min(zn, r);
+                    else zp = OP == OP_MAX ? max(zp, r) : min(zp, r);
+                }
+            }
+            if constexpr (OP == OP_MAX) v = x > v ? x : v;
+            else v = x < v ? x : v;
+        }
+    }
+
+    template <class RankFn>
+    __device__ __forceinline__ void add(T x, RankFn &&rank) {
+        add_value(x, rank);
+        cnt += 1;
+    }
+
+    __device__ __forceinline__ void merge(const Red &o) {
+        if constexpr (OP == OP_SUM) {
+            if constexpr (kFloat) {
+                if constexpr (sizeof(T) == 4) {
+                    s += o.s;
+                } else {
+                    neumaier(s, c, o.s);
+                    c += o.c;
+                }
+            } else {
+                si += o.si;
+            }
+        } else if constexpr (OP == OP_MAX) {
+            v = o.v > v ? o.v : v;
+        } else if constexpr (OP == OP_MIN) {
+            v = o.v < v ? o.v : v;
+        }
+        if constexpr (kRank) {
+            zp = OP == OP_MAX ? max(zp, o.zp) : min(zp, o.zp);
+            zn = OP == OP_MAX ? max(zn, o.zn) : min(zn, o.zn);
+            nan |= o.nan;
+        }
+        cnt += o.cnt;
+    }
+
+    __device__ __forceinline__ T value() const {
+        if constexpr (OP == OP_SUM) {
+            if constexpr (kFloat) {
+                if constexpr (sizeof(T) == 4) return (T)s;
+                else return __builtin_isfinite(s) ? s + c : s;
+            } else {
+                return (T)si;
+            }
+        } else {
+            T r = v;
+            if constexpr (kRank) {
+                if (r == T(0)) {
+                    const bool neg = OP == OP_MAX ? (zn > zp) : (zn < zp);
+                    r = neg ? -T(0) : T(0);
+                }
+            }
+            return r;
+        }
+    }
+
+    __device__ __forceinline__ void to_words(uint64_t w[kPartialWords]) const {
+        w[0] = OP == OP_SUM ? (kFloat ? __builtin_bit_cast(uint64_t, s) : si) : (uint64_t)to_u<T>(v);
+        w[1] = __builtin_bit_cast(uint64_t, c);
+        w[2] = (uint64_t)cnt;
+        w[3] = (uint64_t)zp;
+        w[4] = (uint64_t)zn;
+        w[5] = nan;
+    }
+    __device__ __forceinline__ void from_words(const uint64_t w[kPartialWords]) {
+        init();
+        if constexpr (OP == OP_SUM) {
+            if constexpr (kFloat) s = __builtin_bit_cast(double, w[0]);
+            else si = w[0];
+        } else {
+            v = from_bits64<T>(w[0]);
+        }
+        c = __builtin_bit_cast(double, w[1]);
+        cnt = (int64_t)w[2];
+        zp = (int64_t)w[3];
+        zn = (int64_t)w[4];
+        nan = (uint32_t)w[5];
+    }
+};
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)x, m, 64);
+    const int hi = __shfl_xor((int)(uint32_t)(x >> 32), m, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Deterministic butterfly over the 64 lanes; every lane ends with the wave total.
+template <typename T, int OP>
+__device__ __forceinline__ void wave_reduce(Red<T, OP> &r) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t w[kPartialWords], o[kPartialWords];
+        r.to_words(w);
+#pragma unroll
+        for (int i = 0; i < kPartialWords; ++i) o[i] = shfl_xor_u64(w[i], m);
+        Red<T, OP> other;
+        other.from_words(o);
+        r.merge(other);
+    }
+}
+
+// Workgroup total in thread 0 (waves merged in wave order).
+template <typename T, int OP>
+__device__ __forceinline__ void block_reduce(Red<T, OP> &r) {
+    __shared__ uint64_t lds[kBlock / 64][kPartialWords];
+    wave_reduce(r);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        uint64_t w[kPartialWords];
+        r.to_words(w);
+#pragma unroll
+        for (int i = 0; i < kPartialWords; ++i) lds[wave][i] = w[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBlock / 64; ++k) {
+            Red<T, OP> o;
+            o.from_words(lds[k]);
+            r.merge(o);
+        }
+    }
+    __syncthreads();
+}
+
+// Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
+// partials in workgroup order and write the response (one launch, no second kernel).
+// Hand-off form (MI355X_MICROARCH.md "Valid forms", row 1): one lane stores the partial with
+// agent-scope (sc1) stores, drains them (s_waitcnt vmcnt(0)), then adds to the chunk's ticket;
+// the workgroup whose add returns bpc-1 reads every partial with sc1 loads after a barrier.
+template <typename T, int OP>
+__device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
+    __shared__ uint32_t s_last;
+    block_reduce(r);
+    if (threadIdx.x == 0) {
+        uint64_t w[kPartialWords];
+        r.to_words(w);
+        uint64_t *P = out.partials + ((uint64_t)chunk * bpc + b) * kPartialWords;
+#pragma unroll
+        for (int i = 0; i < kPartialWords; ++i) __hip_atomic_store(P + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = __hip_atomic_fetch_add(out.tickets + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == bpc - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    Red<T, OP> acc;
+    acc.init();
+    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kPartialWords;
+    for (uint32_t j = threadIdx.x; j < bpc; j += kBlock) {
+        uint64_t w[kPartialWords];
+#pragma unroll
+        for (int i = 0; i < kPartialWords; ++i)
+            w[i] = __hip_atomic_load(P + (uint64_t)j * kPartialWords + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        Red<T, OP> o;
+        o.from_words(w);
+        acc.merge(o);
+    }
+    block_reduce(acc);
+    if (threadIdx.x == 0) {
+        if constexpr (OP == OP_COUNT) {
+            reinterpret_cast<int64_t *>(out.body + chunk * out.body_stride)[0] = acc.cnt;
+        } else {
+            reinterpret_cast<T *>(out.body + chunk * out.body_stride)[0] = acc.value();
+        }
+        out.counts[chunk * out.counts_stride] = acc.cnt;
+        if (out.status) out.status[chunk] = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
+        __hip_atomic_store(out.tickets + chunk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+}  // namespace rdx

@@ -1,0 +1,120 @@
+// Plain-data descriptors handed from the host planner (rdx_plan.cpp) to the gfx950 kernels
+// (rdx_kernels.hip).  Everything here is trivially copyable and passed BY VALUE as kernel
+// arguments (< 4 KiB), so a launch needs no descriptor upload.
+#pragma once
+#include <stdint.h>
+
+namespace rdx {
+
+constexpr int kMaxKDims = 16;        // dims left after canonicalisation (unit dims dropped, merged)
+constexpr int kInlineMissing = 16;   // missing_values lists up to this length travel in the args
+constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+constexpr int kPartialWords = 6;     // u64 words per partial record
+
+enum OpCode : uint32_t { OP_COUNT = 0, OP_MAX = 1, OP_MIN = 2, OP_SELECT = 3, OP_SUM = 4 };
+
+// u32 index division by a runtime constant: q = umulhi64(n, magic) for n < 2^32, d < 2^32.
+struct Div {
+    uint64_t magic;  // ceil(2^64 / d); 0 encodes d == 1
+    uint32_t d;
+    uint32_t pad;
+};
+
+// Where the element values come from.  `fused` != 0: the chunk is byte-shuffled with
+// element_size == sizeof(T) and element e's byte k lives at base[k * plane + e]
+// (src/filters/shuffle.rs:32-83 inverted on the fly).  `bswap`: reverse the byte order of every
+// element (src/array.rs:147-177, byte_order == NON_NATIVE).
+struct KSrc {
+    const uint8_t *base;                // single chunk (or NULL when ptrs is used)
+    const uint8_t *const *ptrs;         // batch: device array of chunk base pointers
+    uint64_t plane;                     // bytes per byte-plane (= chunk elements) when fused
+    uint32_t fused;
+    uint32_t bswap;
+};
+
+// Missing-data predicate (src/types/missing.rs:114-122).  Values are raw T bits.
+struct KMissing {
+    uint32_t kind;   // rdx_missing_kind
+    uint32_t n;      // MISSING_VALUES length
+    uint64_t v0, v1; // VALUE / VALID_MIN / VALID_MAX: v0; VALID_RANGE: v0=min, v1=max
+    uint64_t inl[kInlineMissing];   // VALUES, n <= kInlineMissing (linear scan, reference order)
+    const uint64_t *list;           // VALUES, n > kInlineMissing: sorted, -0.0 folded to +0.0 (binary search)
+};
+
+// Per-chunk outputs and the cross-workgroup reduction state.
+struct KOut {
+    uint8_t *body;            // response body (T or i64 values)
+    int64_t *counts;          // response counts
+    uint32_t *status;         // per-chunk status word (RDX_E_NAN_UNORDERED), may be NULL
+    uint64_t body_stride;     // bytes between consecutive chunks' bodies (batch)
+    uint64_t counts_stride;   // elements between consecutive chunks' counts (batch)
+    uint64_t *partials;       // [chunk][block] x kPartialWords
+    uint32_t *tickets;        // [chunk] arrival counters, self-resetting
+};
+
+// Reduction over ALL axes of a view whose elements form one ascending contiguous run
+// [off, off + n) of the chunk (after flipping negative strides).  rank(e) = r0 + (e - off) * rs
+// orders ±0 ties the way ndarray's fold visits them.
+struct KAllContig {
+    KSrc src;
+    KMissing miss;
+    KOut out;
+    uint64_t off, n;
+    int64_t r0, rs;
+    uint32_t filter_semantics;  // Count(All) uses missing_filter (operations.rs:25-33)
+    uint32_t blocks_per_chunk;
+};
+
+// A strided view: dims innermost-first.  offset(e) = base_off + sum idx_k * vstride_k,
+// rank(e) = r0 + sum idx_k * rstride_k.
+struct KView {
+    int32_t ndim;
+    int32_t pad;
+    int64_t base_off;
+    int64_t r0;
+    uint64_t n;                       // number of elements (< 2^32)
+    uint32_t count[kMaxKDims];
+    Div div[kMaxKDims];
+    int64_t vstride[kMaxKDims];
+    int64_t rstride[kMaxKDims];
+};
+
+struct KAllStrided {
+    KSrc src;
+    KMissing miss;
+    KOut out;
+    KView view;
+    uint32_t filter_semantics;
+    uint32_t blocks_per_chunk;
+};
+
+// Reduction over a subset of axes.  Output o (C order over kept dims) reduces the elements
+// base_off + okept(o) + sum over reduced dims.  Work is split into `slices` slices of the reduced
+// index range; slices > 1 write partials [o][slice] combined by k_axis_combine.
+struct KAxis {
+    KSrc src;
+    KMissing miss;
+    KOut out;
+    KView kept;      // kept dims innermost-first in the lane/thread enumeration order;
+                     // rstride here = output C-order stride of that dim
+    KView red;       // reduced dims innermost-first; rstride = tie rank stride
+    uint64_t n_out;
+    uint64_t n_red;
+    uint32_t slices;
+    uint32_t mode;   // 0 = rows (a wave per output), 1 = cols (a thread per output)
+};
+
+// Element-wise map in output order: Select (operations.rs:487-526) and axis=[]
+// (operations.rs:188-210, :58-67).  out index g -> element offset via `view` (dims
+// innermost-first in OUTPUT order).
+struct KMap {
+    KSrc src;
+    KMissing miss;
+    KOut out;
+    KView view;
+    uint32_t kind;    // 0 = select (values + non-missing count), 1 = zero-axes values+0/1 counts,
+                      // 2 = zero-axes counts only (Count op: body = counts)
+    uint32_t pad;
+};
+
+}  // namespace rdx

@@ -1,0 +1,530 @@
+// C ABI implementation (include/rdx.h): device pool, per-stream workspaces, host-resident and
+// device-resident execution.  No CPU fallback exists: without a gfx950 device every execute entry
+// point fails with RDX_E_NO_DEVICE / RDX_E_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rdx.h"
+#include "rdx_kernels.hpp"
+#include "rdx_plan.hpp"
+
+using namespace rdx;
+
+namespace {
+
+rdx_status map_err(hipError_t e) {
+    if (e == hipSuccess) return RDX_OK;
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return RDX_E_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return RDX_E_NO_DEVICE;
+    return RDX_E_DEVICE;
+}
+
+#define RDX_HIP(call)                                      \
+    do {                                                   \
+        hipError_t _e = (call);                            \
+        if (_e != hipSuccess) return map_err(_e);          \
+    } while (0)
+
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+};
+
+}  // namespace
+
+struct rdx_workspace {
+    int device = 0;
+    int cus = 256;
+    hipStream_t own_stream = nullptr;  // host path
+    DevBuf<uint64_t> partials;
+    DevBuf<uint32_t> tickets;
+    DevBuf<uint8_t> scratch[2];
+    DevBuf<uint64_t> miss_list;
+    DevBuf<const uint8_t *> ptrs;
+    // pinned staging for small uploads (missing list, batch pointer tables)
+    uint8_t *pinned = nullptr;
+    size_t pinned_cap = 0;
+    hipEvent_t upload_done = nullptr;
+    bool upload_pending = false;
+    std::vector<uint8_t> last_list, last_ptrs;
+    // host-path device buffers
+    DevBuf<uint8_t> chunk;
+    DevBuf<uint8_t> body;
+    DevBuf<int64_t> counts;
+    DevBuf<uint32_t> status;
+    hipStream_t bound_stream = nullptr;
+};
+
+struct rdx_context {
+    std::vector<int> devices;
+    std::vector<int> cus;
+    std::mutex mu;
+    std::vector<std::vector<rdx_workspace *>> free_ws;  // per device index
+    std::vector<rdx_workspace *> all_ws;
+    std::atomic<uint64_t> rr{0};
+};
+
+namespace {
+
+template <class T>
+rdx_status ensure(rdx_workspace *ws, DevBuf<T> &b, size_t n, hipStream_t s, bool zero = false) {
+    if (b.cap >= n && b.p) return RDX_OK;
+    if (b.p) {
+        RDX_HIP(hipStreamSynchronize(s));  // in-flight work may still read the old buffer
+        RDX_HIP(hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t want = std::max<size_t>(n, 1);
+    want = std::max(want, (size_t)(b.cap * 2));
+    void *p = nullptr;
+    RDX_HIP(hipMalloc(&p, want * sizeof(T)));
+    b.p = static_cast<T *>(p);
+    b.cap = want;
+    if (zero) RDX_HIP(hipMemset(b.p, 0, want * sizeof(T)));
+    (void)ws;
+    return RDX_OK;
+}
+
+// Stream-ordered upload of a small host array through the workspace's pinned staging buffer;
+// identical consecutive uploads are skipped (e.g. a batch re-using the same chunk set).
+rdx_status upload(rdx_workspace *ws, void *dst, const void *src, size_t bytes, std::vector<uint8_t> &cache,
+                  hipStream_t s) {
+    if (cache.size() == bytes && std::memcmp(cache.data(), src, bytes) == 0) return RDX_OK;
+    if (ws->upload_pending) {
+        RDX_HIP(hipEventSynchronize(ws->upload_done));
+        ws->upload_pending = false;
+    }
+    if (ws->pinned_cap < bytes) {
+        if (ws->pinned) RDX_HIP(hipHostFree(ws->pinned));
+        ws->pinned = nullptr;
+        ws->pinned_cap = 0;
+        RDX_HIP(hipHostMalloc((void **)&ws->pinned, bytes, hipHostMallocDefault));
+        ws->pinned_cap = bytes;
+    }
+    std::memcpy(ws->pinned, src, bytes);
+    RDX_HIP(hipMemcpyAsync(dst, ws->pinned, bytes, hipMemcpyHostToDevice, s));
+    RDX_HIP(hipEventRecord(ws->upload_done, s));
+    ws->upload_pending = true;
+    cache.assign(static_cast<const uint8_t *>(src), static_cast<const uint8_t *>(src) + bytes);
+    return RDX_OK;
+}
+
+uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
+    const uint64_t target = (uint64_t)cus * (uint64_t)env_int("RDX_BLOCKS_PER_CU", 8);
+    uint64_t bpc = (target + n_chunks - 1) / n_chunks;
+    const uint64_t min_tiles = (uint64_t)env_int("RDX_MIN_TILES_PER_BLOCK", 2);
+    uint64_t cap = (tiles + min_tiles - 1) / min_tiles;
+    if (bpc > cap) bpc = cap;
+    if (bpc < 1) bpc = 1;
+    if (bpc > 65536) bpc = 65536;
+    return (uint32_t)bpc;
+}
+
+// Everything after planning for n_chunks chunks that share the plan (device pointers only).
+rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, const uint8_t *const *h_ptrs,
+                      uint64_t n_chunks, uint64_t len, uint8_t *d_body, int64_t *d_counts, uint32_t *d_status,
+                      hipStream_t s) {
+    rdx_status st;
+    const uint64_t body_bytes = p.info.body_bytes, n_counts = p.info.n_counts;
+    const bool batchable = (p.mode == Mode::AllContig || p.mode == Mode::AllStrided) && p.unfused_es.empty();
+    if (n_chunks > 1 && !batchable) {
+        for (uint64_t i = 0; i < n_chunks; ++i) {
+            if ((st = run_device(ws, p, h_ptrs[i], nullptr, 1, len, d_body ? d_body + i * body_bytes : nullptr,
+                                 d_counts ? d_counts + i * n_counts : nullptr, d_status ? d_status + i : nullptr, s)))
+                return st;
+        }
+        return RDX_OK;
+    }
+    if (n_chunks == 1 && h_ptrs) d_chunk = h_ptrs[0];
+
+    // 1. filter chain (all but a fused final decode) into scratch
+    const uint8_t *src = d_chunk;
+    for (size_t i = 0; i < p.unfused_es.size(); ++i) {
+        DevBuf<uint8_t> &dst = ws->scratch[i & 1];
+        if ((st = ensure(ws, dst, len, s))) return st;
+        RDX_HIP(launch_unshuffle(src, dst.p, len, p.unfused_es[i], ws->cus, s));
+        src = dst.p;
+    }
+
+    // 2. missing list
+    KMissing miss = p.miss;
+    if (!p.miss_list.empty()) {
+        if ((st = ensure(ws, ws->miss_list, p.miss_list.size(), s))) return st;
+        if ((st = upload(ws, ws->miss_list.p, p.miss_list.data(), p.miss_list.size() * 8, ws->last_list, s))) return st;
+        miss.list = ws->miss_list.p;
+    }
+
+    KSrc ksrc{};
+    ksrc.base = src;
+    ksrc.plane = len / p.esz;
+    ksrc.fused = p.fused;
+    ksrc.bswap = p.bswap;
+    if (n_chunks > 1) {
+        if ((st = ensure(ws, ws->ptrs, n_chunks, s))) return st;
+        if ((st = upload(ws, (void *)ws->ptrs.p, h_ptrs, n_chunks * sizeof(void *), ws->last_ptrs, s))) return st;
+        ksrc.ptrs = ws->ptrs.p;
+        ksrc.base = nullptr;
+    }
+    KOut out{};
+    out.body = d_body;
+    out.counts = d_counts;
+    out.status = d_status;
+    out.body_stride = body_bytes;
+    out.counts_stride = n_counts;
+
+    switch (p.mode) {
+        case Mode::AllContig: {
+            KAllContig a = p.all_contig;
+            const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
+            a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus);
+            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
+            if ((st = ensure(ws, ws->tickets, n_chunks, s, true))) return st;
+            out.partials = ws->partials.p;
+            out.tickets = ws->tickets.p;
+            a.src = ksrc;
+            a.miss = miss;
+            a.out = out;
+            RDX_HIP(launch_all_contig(p.dtype, p.op, a, (uint32_t)n_chunks, s));
+            return RDX_OK;
+        }
+        case Mode::AllStrided: {
+            KAllStrided a = p.all_strided;
+            a.blocks_per_chunk = pick_bpc((a.view.n + 1023) / 1024, n_chunks, ws->cus);
+            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
+            if ((st = ensure(ws, ws->tickets, n_chunks, s, true))) return st;
+            out.partials = ws->partials.p;
+            out.tickets = ws->tickets.p;
+            a.src = ksrc;
+            a.miss = miss;
+            a.out = out;
+            RDX_HIP(launch_all_strided(p.dtype, p.op, a, (uint32_t)n_chunks, s));
+            return RDX_OK;
+        }
+        case Mode::Axis: {
+            KAxis a = p.axis;
+            if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
+            if (a.n_out == 0) return RDX_OK;
+            uint64_t slices = 1;
+            if (a.mode == 0) {
+                const uint64_t target = (uint64_t)ws->cus * 64;
+                if (a.n_out < target) slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (a.n_red + 1023) / 1024);
+            } else {
+                const uint64_t target = (uint64_t)ws->cus * 256;
+                if (a.n_out < target) slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (a.n_red + 63) / 64);
+            }
+            slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, 65535));
+            a.slices = (uint32_t)slices;
+            if (slices > 1) {
+                if ((st = ensure(ws, ws->partials, a.n_out * slices * kPartialWords, s))) return st;
+                out.partials = ws->partials.p;
+            }
+            a.src = ksrc;
+            a.miss = miss;
+            a.out = out;
+            RDX_HIP(launch_axis(p.dtype, p.op, a, ws->cus, s));
+            return RDX_OK;
+        }
+        case Mode::Map: {
+            KMap a = p.map;
+            if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
+            if (a.kind == 0) RDX_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t), s));
+            if (a.view.n == 0) return RDX_OK;
+            a.src = ksrc;
+            a.miss = miss;
+            a.out = out;
+            RDX_HIP(launch_map(p.dtype, a, ws->cus, s));
+            return RDX_OK;
+        }
+    }
+    return RDX_E_INVALID_ARGUMENT;
+}
+
+rdx_status create_workspace(int device, rdx_workspace **out) {
+    RDX_HIP(hipSetDevice(device));
+    auto *ws = new (std::nothrow) rdx_workspace();
+    if (!ws) return RDX_E_OUT_OF_MEMORY;
+    ws->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ws->cus = prop.multiProcessorCount;
+    hipError_t e = hipStreamCreateWithFlags(&ws->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ws->upload_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        delete ws;
+        return map_err(e);
+    }
+    *out = ws;
+    return RDX_OK;
+}
+
+void destroy_workspace(rdx_workspace *ws) {
+    if (!ws) return;
+    (void)hipSetDevice(ws->device);
+    if (ws->own_stream) (void)hipStreamSynchronize(ws->own_stream);
+    if (ws->upload_pending) (void)hipEventSynchronize(ws->upload_done);
+    auto fr = [](void *p) { if (p) (void)hipFree(p); };
+    fr(ws->partials.p);
+    fr(ws->tickets.p);
+    fr(ws->scratch[0].p);
+    fr(ws->scratch[1].p);
+    fr(ws->miss_list.p);
+    fr((void *)ws->ptrs.p);
+    fr(ws->chunk.p);
+    fr(ws->body.p);
+    fr(ws->counts.p);
+    fr(ws->status.p);
+    if (ws->pinned) (void)hipHostFree(ws->pinned);
+    if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
+    if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
+    delete ws;
+}
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+}  // namespace
+
+// ====================================== C ABI ========================================================
+extern "C" {
+
+uint32_t rdx_abi_version(void) { return RDX_ABI_VERSION; }
+
+const char *rdx_status_string(rdx_status s) {
+    switch (s) {
+        case RDX_OK: return "ok";
+        case RDX_E_INVALID_ARGUMENT: return "invalid argument";
+        case RDX_E_REQUEST_VALIDATION: return "request data is not valid";
+        case RDX_E_FROM_BYTES: return "failed to convert from bytes";
+        case RDX_E_SHAPE_INVALID: return "failed to create array from shape";
+        case RDX_E_INCOMPATIBLE_MISSING: return "Incompatible value for missing";
+        case RDX_E_SHUFFLE_LENGTH: return "data length is not a multiple of the shuffle element size";
+        case RDX_E_NAN_UNORDERED: return "unexpected undefined order error for min";
+        case RDX_E_UNSUPPORTED: return "unsupported by the device engine";
+        case RDX_E_DEVICE: return "device error";
+        case RDX_E_OUT_OF_MEMORY: return "out of memory";
+        case RDX_E_BUFFER_TOO_SMALL: return "output buffer too small";
+        case RDX_E_NO_DEVICE: return "no gfx950 device";
+    }
+    return "unknown status";
+}
+
+int rdx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int c = 0;
+    for (int d = 0; d < n; ++d) c += is_gfx950(d) ? 1 : 0;
+    return c;
+}
+
+rdx_status rdx_context_create(const int *devices, int n_devices, rdx_context **out) {
+    if (!out) return RDX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return RDX_E_NO_DEVICE;
+    auto *ctx = new (std::nothrow) rdx_context();
+    if (!ctx) return RDX_E_OUT_OF_MEMORY;
+    if (!devices || n_devices <= 0) ctx->devices.push_back(0);
+    else ctx->devices.assign(devices, devices + n_devices);
+    for (int d : ctx->devices) {
+        if (d < 0 || d >= n || !is_gfx950(d)) {
+            delete ctx;
+            return RDX_E_NO_DEVICE;
+        }
+    }
+    ctx->free_ws.resize(ctx->devices.size());
+    *out = ctx;
+    return RDX_OK;
+}
+
+void rdx_context_destroy(rdx_context *ctx) {
+    if (!ctx) return;
+    for (rdx_workspace *ws : ctx->all_ws) destroy_workspace(ws);
+    delete ctx;
+}
+
+rdx_status rdx_validate_request(const rdx_request *req) {
+    if (!req) return RDX_E_INVALID_ARGUMENT;
+    return validate_request(*req);
+}
+
+rdx_status rdx_plan(const rdx_request *req, uint64_t chunk_len, rdx_response_info *info) {
+    if (!req || !info) return RDX_E_INVALID_ARGUMENT;
+    ExecPlan p;
+    const rdx_status st = make_plan(*req, chunk_len, p);
+    if (st) return st;
+    *info = p.info;
+    return RDX_OK;
+}
+
+// src/types/dvalue.rs:43-83 TryFromDValue, for a JSON integer that fits i64.
+rdx_status rdx_missing_from_i64(uint32_t dtype, int64_t v, void *out) {
+    if (!out) return RDX_E_INVALID_ARGUMENT;
+    switch (dtype) {
+        case RDX_DTYPE_INT32: {
+            if (v < INT32_MIN || v > INT32_MAX) return RDX_E_INCOMPATIBLE_MISSING;
+            const int32_t x = (int32_t)v; std::memcpy(out, &x, 4); return RDX_OK;
+        }
+        case RDX_DTYPE_INT64: std::memcpy(out, &v, 8); return RDX_OK;
+        case RDX_DTYPE_UINT32: {
+            if (v < 0 || v > (int64_t)UINT32_MAX) return RDX_E_INCOMPATIBLE_MISSING;
+            const uint32_t x = (uint32_t)v; std::memcpy(out, &x, 4); return RDX_OK;
+        }
+        case RDX_DTYPE_UINT64: {
+            if (v < 0) return RDX_E_INCOMPATIBLE_MISSING;
+            const uint64_t x = (uint64_t)v; std::memcpy(out, &x, 8); return RDX_OK;
+        }
+        case RDX_DTYPE_FLOAT32: {
+            const float x = (float)(double)v;
+            if (!std::isfinite(x)) return RDX_E_INCOMPATIBLE_MISSING;
+            std::memcpy(out, &x, 4); return RDX_OK;
+        }
+        case RDX_DTYPE_FLOAT64: { const double x = (double)v; std::memcpy(out, &x, 8); return RDX_OK; }
+    }
+    return RDX_E_INVALID_ARGUMENT;
+}
+
+// ... for a JSON integer above i64::MAX (serde_json PosInt that as_i64() rejects).
+rdx_status rdx_missing_from_u64(uint32_t dtype, uint64_t v, void *out) {
+    if (!out) return RDX_E_INVALID_ARGUMENT;
+    if (v <= (uint64_t)INT64_MAX) return rdx_missing_from_i64(dtype, (int64_t)v, out);
+    switch (dtype) {
+        case RDX_DTYPE_INT32: case RDX_DTYPE_INT64: case RDX_DTYPE_UINT32: return RDX_E_INCOMPATIBLE_MISSING;
+        case RDX_DTYPE_UINT64: std::memcpy(out, &v, 8); return RDX_OK;
+        case RDX_DTYPE_FLOAT32: {
+            const float x = (float)(double)v;
+            if (!std::isfinite(x)) return RDX_E_INCOMPATIBLE_MISSING;
+            std::memcpy(out, &x, 4); return RDX_OK;
+        }
+        case RDX_DTYPE_FLOAT64: { const double x = (double)v; std::memcpy(out, &x, 8); return RDX_OK; }
+    }
+    return RDX_E_INVALID_ARGUMENT;
+}
+
+// ... for a JSON float (as_i64/as_u64 are None: integers are incompatible).
+rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out) {
+    if (!out) return RDX_E_INVALID_ARGUMENT;
+    switch (dtype) {
+        case RDX_DTYPE_INT32: case RDX_DTYPE_INT64: case RDX_DTYPE_UINT32: case RDX_DTYPE_UINT64:
+            return RDX_E_INCOMPATIBLE_MISSING;
+        case RDX_DTYPE_FLOAT32: {
+            const float x = (float)v;
+            if (!std::isfinite(x)) return RDX_E_INCOMPATIBLE_MISSING;
+            std::memcpy(out, &x, 4); return RDX_OK;
+        }
+        case RDX_DTYPE_FLOAT64: std::memcpy(out, &v, 8); return RDX_OK;
+    }
+    return RDX_E_INVALID_ARGUMENT;
+}
+
+rdx_status rdx_workspace_create(rdx_context *ctx, int device, rdx_workspace **out) {
+    if (!ctx || !out) return RDX_E_INVALID_ARGUMENT;
+    return create_workspace(device, out);
+}
+
+void rdx_workspace_destroy(rdx_workspace *ws) { destroy_workspace(ws); }
+
+rdx_status rdx_execute_device(rdx_workspace *ws, const rdx_request *req, const void *d_chunk, uint64_t chunk_len,
+                              void *d_body, int64_t *d_counts, uint32_t *d_status, void *stream,
+                              rdx_response_info *info) {
+    if (!ws || !req) return RDX_E_INVALID_ARGUMENT;
+    ExecPlan p;
+    rdx_status st = make_plan(*req, chunk_len, p);
+    if (st) return st;
+    if (info) *info = p.info;
+    if ((!d_chunk && chunk_len) || (!d_body && p.info.body_bytes) || (!d_counts && p.info.n_counts))
+        return RDX_E_INVALID_ARGUMENT;
+    RDX_HIP(hipSetDevice(ws->device));
+    return run_device(ws, p, static_cast<const uint8_t *>(d_chunk), nullptr, 1, chunk_len,
+                      static_cast<uint8_t *>(d_body), d_counts, d_status, static_cast<hipStream_t>(stream));
+}
+
+rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req, uint64_t n_chunks,
+                                    const void *const *h_chunk_ptrs, uint64_t chunk_len, void *d_bodies,
+                                    int64_t *d_counts, uint32_t *d_status, void *stream, rdx_response_info *info) {
+    if (!ws || !req || (n_chunks && !h_chunk_ptrs)) return RDX_E_INVALID_ARGUMENT;
+    ExecPlan p;
+    rdx_status st = make_plan(*req, chunk_len, p);
+    if (st) return st;
+    if (info) *info = p.info;
+    if (n_chunks == 0) return RDX_OK;
+    if ((!d_bodies && p.info.body_bytes) || (!d_counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
+    RDX_HIP(hipSetDevice(ws->device));
+    return run_device(ws, p, nullptr, reinterpret_cast<const uint8_t *const *>(h_chunk_ptrs), n_chunks, chunk_len,
+                      static_cast<uint8_t *>(d_bodies), d_counts, d_status, static_cast<hipStream_t>(stream));
+}
+
+rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len, void *body,
+                       uint64_t body_capacity, int64_t *counts, uint64_t counts_capacity, rdx_response_info *info) {
+    if (!ctx || !req || !info || (!chunk && chunk_len)) return RDX_E_INVALID_ARGUMENT;
+    ExecPlan p;
+    rdx_status st = make_plan(*req, chunk_len, p);
+    if (st) return st;
+    *info = p.info;
+    if (body_capacity < p.info.body_bytes || counts_capacity < p.info.n_counts) return RDX_E_BUFFER_TOO_SMALL;
+    if ((!body && p.info.body_bytes) || (!counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
+
+    // take a workspace (round-robin device, then any free workspace of it)
+    rdx_workspace *ws = nullptr;
+    size_t di = 0;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        di = (size_t)(ctx->rr++ % ctx->devices.size());
+        if (!ctx->free_ws[di].empty()) {
+            ws = ctx->free_ws[di].back();
+            ctx->free_ws[di].pop_back();
+        }
+    }
+    if (!ws) {
+        if ((st = create_workspace(ctx->devices[di], &ws))) return st;
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->all_ws.push_back(ws);
+    }
+    auto run = [&]() -> rdx_status {
+        RDX_HIP(hipSetDevice(ws->device));
+        hipStream_t s = ws->own_stream;
+        rdx_status r;
+        if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
+        if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
+        if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
+        if ((r = ensure(ws, ws->status, 1, s))) return r;
+        if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
+        RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
+        if ((r = run_device(ws, p, ws->chunk.p, nullptr, 1, chunk_len, ws->body.p, ws->counts.p, ws->status.p, s)))
+            return r;
+        uint32_t status = 0;
+        if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
+        if (p.info.n_counts)
+            RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipStreamSynchronize(s));
+        if (status) return (rdx_status)status;
+        return RDX_OK;
+    };
+    st = run();
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->free_ws[di].push_back(ws);
+    }
+    return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+"""Thin owner of an rdx_context / rdx_workspace (include/rdx.h).  No CPU fallback."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+from . import _abi
+from .errors import check
+
+
+class Engine:
+    """Device pool (rdx_context).  One per process; thread-safe like the C ABI."""
+
+    def __init__(self, devices: Sequence[int] | None = None):
+        self.lib = _abi.lib()
+        ctx = C.c_void_p()
+        if devices:
+            arr = (C.c_int * len(devices))(*devices)
+            check(self.lib.rdx_context_create(arr, len(devices), C.byref(ctx)))
+        else:
+            check(self.lib.rdx_context_create(None, 0, C.byref(ctx)))
+        self.ctx = ctx
+
+    def close(self):
+        if self.ctx:
+            self.lib.rdx_context_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def plan(self, creq: _abi.CRequest, chunk_len: int) -> _abi.rdx_response_info:
+        info = _abi.rdx_response_info()
+        check(self.lib.rdx_plan(creq.ref, chunk_len, C.byref(info)))
+        return info
+
+    def execute_raw(self, creq: _abi.CRequest, data: bytes):
+        """Host chunk in, (status, info, body, counts) out — no exception on kernel-side status."""
+        info = self.plan(creq, len(data))
+        body = (C.c_uint8 * max(1, info.body_bytes))()
+        counts = (C.c_int64 * max(1, info.n_counts))()
+        src = C.c_char_p(bytes(data)) if len(data) else None
+        st = self.lib.rdx_execute(self.ctx, creq.ref, src, len(data), body, info.body_bytes, counts,
+                                  info.n_counts, C.byref(info))
+        return st, info, bytes(body)[: info.body_bytes], [int(c) for c in counts[: info.n_counts]]
+
+    def execute(self, creq: _abi.CRequest, data: bytes):
+        st, info, body, counts = self.execute_raw(creq, data)
+        check(st)
+        return info, body, counts
+
+    def workspace(self, device: int = 0) -> "Workspace":
+        return Workspace(self, device)
+
+
+class Workspace:
+    """Per-stream scratch for the device-resident entry points (pointers are plain ints)."""
+
+    def __init__(self, engine: Engine, device: int = 0):
+        self.engine = engine
+        self.lib = engine.lib
+        ws = C.c_void_p()
+        check(self.lib.rdx_workspace_create(engine.ctx, device, C.byref(ws)))
+        self.ws = ws
+
+    def close(self):
+        if self.ws:
+            self.lib.rdx_workspace_destroy(self.ws)
+            self.ws = None
+
+    def execute_device(self, creq, d_chunk: int, chunk_len: int, d_body: int, d_counts: int,
+                       d_status: int | None, stream: int | None) -> _abi.rdx_response_info:
+        info = _abi.rdx_response_info()
+        check(self.lib.rdx_execute_device(self.ws, creq.ref, C.c_void_p(d_chunk), chunk_len, C.c_void_p(d_body),
+                                          C.c_void_p(d_counts), C.c_void_p(d_status or 0),
+                                          C.c_void_p(stream or 0), C.byref(info)))
+        return info
+
+    def execute_batch_device(self, creq, d_chunks: Sequence[int], chunk_len: int, d_bodies: int, d_counts: int,
+                             d_status: int | None, stream: int | None) -> _abi.rdx_response_info:
+        info = _abi.rdx_response_info()
+        ptrs = (C.c_void_p * len(d_chunks))(*d_chunks)
+        check(self.lib.rdx_execute_batch_device(self.ws, creq.ref, len(d_chunks), ptrs, chunk_len,
+                                                C.c_void_p(d_bodies), C.c_void_p(d_counts),
+                                                C.c_void_p(d_status or 0), C.c_void_p(stream or 0),
+                                                C.byref(info)))
+        return info

@@ -1,0 +1,159 @@
+"""Shared test helpers: KAT -> request marshalling and a random request generator used for the
+differential (engine vs oracle) tests."""
+from __future__ import annotations
+
+import json
+import math
+from pathlib import Path
+
+import numpy as np
+
+from reductionist_amd import _abi
+
+GOLDEN = Path(__file__).resolve().parent / "golden" / "kats.json"
+
+STATUS = {"ok": _abi.OK, "E_REQUEST_VALIDATION": _abi.E_REQUEST_VALIDATION, "E_FROM_BYTES": _abi.E_FROM_BYTES,
+          "E_SHAPE_INVALID": _abi.E_SHAPE_INVALID, "E_INCOMPATIBLE_MISSING": _abi.E_INCOMPATIBLE_MISSING,
+          "E_SHUFFLE_LENGTH": _abi.E_SHUFFLE_LENGTH, "E_NAN_UNORDERED": _abi.E_NAN_UNORDERED,
+          "E_UNSUPPORTED": _abi.E_UNSUPPORTED}
+
+NP = {"int32": np.int32, "int64": np.int64, "uint32": np.uint32, "uint64": np.uint64, "float32": np.float32,
+      "float64": np.float64}
+
+
+def load_kats(kind=None):
+    kats = json.loads(GOLDEN.read_text())
+    return [k for k in kats if kind is None or k["kind"] == kind]
+
+
+def make_request(op: str, req: dict, convert) -> _abi.CRequest:
+    """Build the C request; `convert(dtype, value) -> (status, bytes)` turns JSON missing values into T."""
+    dtype = req["dtype"]
+    kind, values, n = None, b"", 0
+    if req.get("missing"):
+        (kind, raw), = req["missing"].items()
+        vals = raw if kind in ("missing_values", "valid_range") else [raw]
+        packed = []
+        for v in vals:
+            st, bts = convert(dtype, v)
+            if st != 0:
+                raise ValueError(f"incompatible missing {v} for {dtype}")
+            packed.append(bts)
+        values, n = b"".join(packed), len(vals)
+    return _abi.CRequest(op, dtype, shape=req.get("shape"), selection=req.get("selection"), axis=req.get("axis"),
+                         order=req.get("order"), byte_order=req.get("byte_order"), filters=req.get("filters"),
+                         compression=req.get("compression"), missing_kind=kind, missing_values=values,
+                         n_missing=n, size=req.get("size"))
+
+
+def product_convert(dtype, v):
+    from reductionist_amd.models import dvalue_to_bytes
+    from reductionist_amd.errors import IncompatibleMissing
+    try:
+        return 0, dvalue_to_bytes(v, dtype)
+    except IncompatibleMissing:
+        return _abi.E_INCOMPATIBLE_MISSING, b""
+
+
+def check_kat_result(kat, st, info, body, counts):
+    exp = kat["expect"]
+    assert st == STATUS[exp["status"]], (kat["name"], st, exp)
+    if exp["status"] != "ok":
+        return
+    assert body.hex() == exp["body"], (kat["name"], body.hex(), exp["body"])
+    assert _abi.DTYPE_NAMES[info.dtype] == exp["dtype"], kat["name"]
+    assert info.shape_list() == exp["shape"], (kat["name"], info.shape_list())
+    assert counts == exp["count"], (kat["name"], counts, exp["count"])
+
+
+# ---- random requests -----------------------------------------------------------------------------------
+DTYPES = list(NP)
+OPS = ["count", "max", "min", "select", "sum"]
+
+
+def _values(rng, dtype, n, allow_nan=False):
+    if dtype.startswith("float"):
+        v = rng.integers(-6, 7, n).astype(NP[dtype])
+        neg = rng.random(n) < 0.5
+        v[(v == 0) & neg] = -0.0                    # exercise the ±0 tie rule
+        if rng.random() < 0.3:
+            v[rng.random(n) < 0.05] = np.inf if rng.random() < 0.5 else -np.inf
+        if allow_nan and rng.random() < 0.3:
+            v[rng.random(n) < 0.05] = np.nan
+        return v
+    info = np.iinfo(NP[dtype])
+    v = rng.integers(max(info.min, -6), 7, n).astype(NP[dtype])
+    if rng.random() < 0.3:  # wrap-around sums
+        m = rng.random(n) < 0.2
+        v[m] = info.max if rng.random() < 0.5 else info.min
+    return v
+
+
+def random_case(rng, dtype=None, op=None, max_dim=6, max_ndim=4, allow_nan=False):
+    """Return (op, request dict, raw chunk bytes)."""
+    dtype = dtype or DTYPES[rng.integers(len(DTYPES))]
+    op = op or OPS[rng.integers(len(OPS))]
+    esz = np.dtype(NP[dtype]).itemsize
+    req = {"dtype": dtype}
+    use_shape = rng.random() < 0.85
+    if use_shape:
+        ndim = int(rng.integers(1, max_ndim + 1))
+        shape = [int(s) for s in rng.integers(1, max_dim + 1, ndim)]
+        req["shape"] = shape
+        if rng.random() < 0.5:
+            req["order"] = "F" if rng.random() < 0.5 else "C"
+        if rng.random() < 0.6:
+            sel = []
+            for L in shape:
+                stride = int(rng.integers(1, 4)) * (1 if rng.random() < 0.7 else -1)
+                sel.append([int(rng.integers(-L - 2, L + 3)), int(rng.integers(-L - 2, L + 3)), stride])
+            req["selection"] = sel
+        r = rng.random()
+        if r < 0.35:
+            req["axis"] = int(rng.integers(0, ndim))
+        elif r < 0.7:
+            k = int(rng.integers(0, ndim + 1))
+            req["axis"] = sorted(int(a) for a in rng.choice(ndim, k, replace=False))
+        n = int(np.prod(shape))
+    else:
+        n = int(rng.integers(0, 40))
+    vals = _values(rng, dtype, n, allow_nan)
+    if rng.random() < 0.4:
+        req["byte_order"] = "big" if rng.random() < 0.6 else "little"
+    raw = vals.astype(vals.dtype.newbyteorder(">" if req.get("byte_order") == "big" else "<")).tobytes()
+    if rng.random() < 0.3 and n:
+        kinds = ["missing_value", "missing_values", "valid_min", "valid_max", "valid_range"]
+        kind = kinds[rng.integers(len(kinds))]
+        finite = vals[np.isfinite(vals)] if dtype.startswith("float") else vals
+        pick = lambda: (float(finite[rng.integers(len(finite))]) if dtype.startswith("float")
+                        else int(finite[rng.integers(len(finite))])) if len(finite) else 1
+        if kind == "missing_values":
+            req["missing"] = {kind: [pick() for _ in range(int(rng.integers(1, 4)))]}
+        elif kind == "valid_range":
+            a, b = sorted([pick(), pick()])
+            if a == b:
+                b = a + 1 if not dtype.startswith("float") else a + 0.5
+            req["missing"] = {kind: [a, b]}
+        else:
+            req["missing"] = {kind: pick()}
+    if rng.random() < 0.4 and len(raw):
+        # shuffle filters: es == sizeof(T) (fused path) or another divisor (scratch path), maybe a chain
+        cands = [e for e in (1, 2, 3, 4, 8, 16) if len(raw) % e == 0]
+        fl = [esz] if rng.random() < 0.6 else [int(cands[rng.integers(len(cands))])]
+        if rng.random() < 0.3:
+            fl.append(int(cands[rng.integers(len(cands))]))
+        req["filters"] = [{"id": "shuffle" if rng.random() < 0.5 else "shuffle_simd", "element_size": e} for e in fl]
+    return op, req, raw
+
+
+def encode_filters(raw: bytes, filters, shuffle) -> bytes:
+    """Apply the shuffle ENCODERS so that the pipeline's reverse-order decode restores `raw`."""
+    out = raw
+    for f in filters or []:
+        out = shuffle(out, f["element_size"])
+    return out
+
+
+def ulp(x: float, dtype) -> float:
+    x = abs(float(x))
+    return float(np.spacing(NP[dtype](x))) if math.isfinite(x) else 0.0
