@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """bench.py — GiB/s of device-resident chunk unshuffle+reduce (f32 sum) on MI355X.
 
-Workload (BASELINE.json configs[1], "c2"): one step = one 64 MiB chunk of 16 Mi f32 values stored
-big-endian and byte-shuffled (element_size 4), reduced with `sum` by one launch of the fused
-unshuffle + byte-swap + f64-accumulated sum kernel.  Inputs are resident in HBM before timing; 8
-distinct chunks (512 MiB > the 256 MiB Infinity Cache) are rotated so every step streams from HBM.
+Workload (BASELINE.json configs[1], "c2"): 64 MiB chunks of 16 Mi f32 values stored big-endian and
+byte-shuffled (element_size 4), each reduced with `sum` (its own result + count).  8 distinct chunks
+(512 MiB > the 256 MiB Infinity Cache) are resident in HBM before timing; one step = one launch of the
+fused unshuffle + byte-swap + f64-accumulated sum kernel over those 8 independent chunks through the
+engine's batch entry point (rdx_execute_batch_device), so every step streams 512 MiB from HBM and the
+per-launch ramp/finalisation (~6 us, profiles/) is paid once per 8 chunks.  extra.c2_single_chunk
+reports the same chunks at one chunk per launch (rdx_execute_device).
 Ranks (one per GPU, torchrun) each process their own chunks: weak scaling, no data-path collective
 (the control-plane barrier / max-time reduction uses gloo).
 
@@ -21,7 +24,6 @@ import argparse
 import ctypes as C
 import json
 import os
-import statistics
 import sys
 import time
 from pathlib import Path
@@ -49,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--primary-only", action="store_true", help="only the headline batched C2 loop (profiling)")
     return ap.parse_args()
 
 
@@ -139,45 +142,72 @@ def main():
     status = torch.zeros(N_BUF, dtype=torch.int32, device="cuda")
     creq = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
     info = _abi.rdx_response_info()
-    fn = lib.rdx_execute_device
-    argv = [(ws.ws, creq.ref, C.c_void_p(chunks[i].data_ptr()), C2_BYTES, C.c_void_p(bodies[i:].data_ptr()),
-             C.c_void_p(counts[i:].data_ptr()), C.c_void_p(status[i:].data_ptr()), sh, C.byref(info))
-            for i in range(N_BUF)]
+    ptrs = (C.c_void_p * N_BUF)(*[chunks[i].data_ptr() for i in range(N_BUF)])
+    batch_args = (ws.ws, creq.ref, N_BUF, ptrs, C2_BYTES, C.c_void_p(bodies.data_ptr()),
+                  C.c_void_p(counts.data_ptr()), C.c_void_p(status.data_ptr()), sh, C.byref(info))
+    single_args = [(ws.ws, creq.ref, C.c_void_p(chunks[i].data_ptr()), C2_BYTES, C.c_void_p(bodies[i:].data_ptr()),
+                    C.c_void_p(counts[i:].data_ptr()), C.c_void_p(status[i:].data_ptr()), sh, C.byref(info))
+                   for i in range(N_BUF)]
 
-    def step(i):
-        st = fn(*argv[i % N_BUF])
+    def check_results():
+        torch.cuda.synchronize()
+        got = bodies.double().cpu()
+        assert int(status.abs().sum()) == 0 and bool((counts.cpu() == C2_ELEMS).all())
+        tol = exact.abs() * 2.0 ** -23 + 1e-3
+        assert bool(((got - exact).abs() <= tol).all()), (got, exact)
+        bodies.zero_()
+        counts.zero_()
+
+    def batch_step(i):
+        st = lib.rdx_execute_batch_device(*batch_args)
+        if st:
+            raise RuntimeError(f"rdx_execute_batch_device failed: {_abi.status_string(st)}")
+
+    def single_step(i):
+        st = lib.rdx_execute_device(*single_args[i % N_BUF])
         if st:
             raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    # correctness of what we time: every buffer vs an f64 reference sum (f32 tolerance)
-    got = bodies.double().cpu()
-    assert int(status.abs().sum()) == 0 and bool((counts.cpu() == C2_ELEMS).all())
-    tol = (exact.abs() * 2.0 ** -23 + 1e-3)
-    assert bool(((got - exact).abs() <= tol).all()), (got, exact)
+    def timed(step, n):
+        """n back-to-back launches on one stream, bracketed by barrier + synchronize; HIP events on the
+        launch stream around the same region give the average launch duration (gaps included)."""
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(n):
+            step(i)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        return max_over_ranks(t1 - t0), ev0.elapsed_time(ev1) / 1e3 / n
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
-        step(i)
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = max_over_ranks(t1 - t0)
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    kern_avg_s = statistics.fmean(kern_ms) / 1e3
-    kern_med_s = statistics.median(kern_ms) / 1e3
-    value = args.steps * C2_BYTES * world / elapsed / GIB
-    achieved = C2_BYTES / kern_avg_s / 1e9
+    for i in range(args.warmup):
+        batch_step(i)
+    check_results()                       # what we time is correct: every chunk vs an f64 sum
+    elapsed, kern_avg_s = timed(batch_step, args.steps)
+    check_results()
+    step_bytes = N_BUF * C2_BYTES
+    value = args.steps * step_bytes * world / elapsed / GIB
+    achieved = step_bytes / kern_avg_s / 1e9
+
+    extra = {}
+    if args.primary_only:
+        args.no_c4 = args.no_cpu_baseline = True
+    else:
+        for i in range(args.warmup):
+            single_step(i)
+        check_results()
+        el1, k1 = timed(single_step, args.steps)
+        extra["c2_single_chunk"] = {
+        "workload": "the same 64 MiB chunks, one chunk per launch (rdx_execute_device)",
+        "value": round(args.steps * C2_BYTES * world / el1 / GIB, 2), "unit": "GiB/s",
+        "ms_per_step": round(el1 / args.steps * 1e3, 5), "kernel_us_avg": round(k1 * 1e6, 3),
+        "roofline_frac": round(C2_BYTES / k1 / 1e9 / PEAK_GBS, 4)}
 
     # ---- C4 (extra): 1024 x 4 MiB chunks, one batched launch per step ----------------------------------
-    extra = {}
     if not args.no_c4:
         n_local = C4_CHUNKS // world + (1 if rank < C4_CHUNKS % world else 0)
         g.manual_seed(0x5EED1000 + rank)
@@ -224,13 +254,16 @@ def main():
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic U[0,1) f32, big-endian, byte-shuffled (es=4)",
-        "config": {"workload": "c2: sum over one 64 MiB f32 chunk per step per GPU (16 Mi elements), "
-                               "byte shuffle es=4 + non-native (big) byte order, 8 rotating HBM-resident chunks",
-                   "chunk_bytes": C2_BYTES, "elements": C2_ELEMS, "parallelism": f"independent chunks x{world}"},
+        "config": {"workload": "c2: f32 sum over 64 MiB chunks (16 Mi elements each), byte shuffle es=4 + "
+                               "non-native (big) byte order; one step = one launch over 8 independent "
+                               "HBM-resident chunks (512 MiB) per GPU, one result per chunk",
+                   "chunk_bytes": C2_BYTES, "chunks_per_step": N_BUF, "elements_per_chunk": C2_ELEMS,
+                   "parallelism": f"independent chunks x{world} GPUs"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_GBS, 4), "traffic": traffic_from_profiles("c2"),
-                     "kernel": "k_all_contig<float, OP_SUM, FUSED>", "kernel_us_avg": round(kern_avg_s * 1e6, 3),
-                     "kernel_us_median": round(kern_med_s * 1e6, 3), "bytes_alg_per_launch": C2_BYTES},
+                     "kernel": "k_all_contig<float, OP_SUM, FUSED=1, MISS=0>",
+                     "kernel_us_avg": round(kern_avg_s * 1e6, 3), "bytes_alg_per_launch": step_bytes,
+                     "timing": "HIP events on the launch stream around the K back-to-back launches / K"},
         "extra": extra,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -62,18 +62,16 @@ __device__ __forceinline__ uint64_t tile_elems() {
     return FUSED ? (uint64_t)kBlock * 16 : (uint64_t)kBlock * 64 / sizeof(T);
 }
 
-template <typename T, bool FUSED>
-__device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *base, uint64_t plane, uint64_t va,
-                                          uint64_t vb, uint64_t t, bool &full) {
-    const uint64_t te = tile_elems<T, FUSED>();
-    const uint64_t t0 = va + t * te;
-    full = t0 + te <= vb;
+// FULL: every lane's granules are inside [va, vb) -> unconditional loads, so all UNR tiles' loads
+// issue back to back; the single partial tile of a range goes through the checked variant.
+template <typename T, bool FUSED, bool FULL>
+__device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *base, uint64_t plane, uint64_t t0,
+                                          uint64_t vb) {
     if constexpr (FUSED) {
         const uint64_t e = t0 + threadIdx.x * 16;
-        if (e + 16 <= vb) {
+        if (FULL || e + 16 <= vb) {
 #pragma unroll
-            for (int k = 0; k < (int)sizeof(T); ++k)
-                tl.p[k] = *reinterpret_cast<const uint4 *>(base + (uint64_t)k * plane + e);
+            for (int k = 0; k < (int)sizeof(T); ++k) tl.p[k] = gld<uint4>(base + (uint64_t)k * plane + e);
         }
     } else {
         const uint8_t *b = base + t0 * sizeof(T);
@@ -81,21 +79,19 @@ __device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *bas
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
-            if (o + 16 <= lim) tl.p[m] = *reinterpret_cast<const uint4 *>(b + o);
+            if (FULL || o + 16 <= lim) tl.p[m] = gld<uint4>(b + o);
         }
     }
 }
 
-template <typename T, int OP, bool FUSED, bool MISS>
-__device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED> &tl, const KAllContig &a, uint64_t va,
-                                             uint64_t vb, uint64_t t, uint32_t selA, uint32_t selB) {
+template <typename T, int OP, bool FUSED, bool MISS, bool FULL>
+__device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED> &tl, const KAllContig &a, uint64_t t0,
+                                             uint64_t vb, uint32_t selA, uint32_t selB) {
     using U = typename UIntOf<T>::type;
-    const uint64_t te = tile_elems<T, FUSED>();
-    const uint64_t t0 = va + t * te;
     const bool bswap = a.src.bswap;
     if constexpr (FUSED) {
         const uint64_t e = t0 + threadIdx.x * 16;
-        if (e + 16 > vb) return;
+        if (!FULL && e + 16 > vb) return;
         if constexpr (OP == OP_COUNT && !MISS) {
             r.cnt += 16;
             return;
@@ -135,7 +131,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
-            if (o + 16 > lim) continue;
+            if (!FULL && o + 16 > lim) continue;
             const uint64_t e = t0 + o / sizeof(T);
             if constexpr (OP == OP_COUNT && !MISS) {
                 r.cnt += kPer;
@@ -168,7 +164,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
     }
 }
 
-template <typename T, int OP, bool FUSED, bool MISS>
+template <typename T, int OP, bool FUSED, bool MISS, int UNR>
 __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
@@ -196,26 +192,30 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
         for (uint64_t e = vb + threadIdx.x; e < hi; e += kBlock)
             consume<T, OP, MISS>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
     }
-    // vector body: tiles of tile_elems() split into contiguous per-workgroup ranges
+    // vector body: full tiles split into contiguous per-workgroup ranges, UNR tiles in flight per
+    // lane; the one partial tile (if any) goes to workgroup 0 with the scalar head/tail.
     const uint64_t te = tile_elems<T, FUSED>();
-    const uint64_t ntiles = (vb - va + te - 1) / te;
-    const uint64_t per = (ntiles + bpc - 1) / bpc;
+    const uint64_t nfull = (vb - va) / te;
+    const uint64_t per = (nfull + bpc - 1) / bpc;
     const uint64_t t_begin = (uint64_t)b * per;
-    const uint64_t t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
+    const uint64_t t_end = t_begin + per < nfull ? t_begin + per : nfull;
     uint64_t t = t_begin;
-    for (; t + 1 < t_end; t += 2) {  // two tiles in flight per lane
-        Tile<T, FUSED> x0, x1;
-        bool f0, f1;
-        load_tile<T, FUSED>(x0, base, a.src.plane, va, vb, t, f0);
-        load_tile<T, FUSED>(x1, base, a.src.plane, va, vb, t + 1, f1);
-        consume_tile<T, OP, FUSED, MISS>(r, x0, a, va, vb, t, selA, selB);
-        consume_tile<T, OP, FUSED, MISS>(r, x1, a, va, vb, t + 1, selA, selB);
+    for (; t + UNR <= t_end; t += UNR) {
+        Tile<T, FUSED> x[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, va + (t + u) * te, vb);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MISS, true>(r, x[u], a, va + (t + u) * te, vb, selA, selB);
     }
-    if (t < t_end) {
+    for (; t < t_end; ++t) {
         Tile<T, FUSED> x0;
-        bool f0;
-        load_tile<T, FUSED>(x0, base, a.src.plane, va, vb, t, f0);
-        consume_tile<T, OP, FUSED, MISS>(r, x0, a, va, vb, t, selA, selB);
+        load_tile<T, FUSED, true>(x0, base, a.src.plane, va + t * te, vb);
+        consume_tile<T, OP, FUSED, MISS, true>(r, x0, a, va + t * te, vb, selA, selB);
+    }
+    if (b == 0 && va + nfull * te < vb) {
+        Tile<T, FUSED> x0;
+        load_tile<T, FUSED, false>(x0, base, a.src.plane, va + nfull * te, vb);
+        consume_tile<T, OP, FUSED, MISS, false>(r, x0, a, va + nfull * te, vb, selA, selB);
     }
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
@@ -269,17 +269,24 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
 
-template <typename T, int OP>
-hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
-    const dim3 grid(a.blocks_per_chunk * n_chunks), block(kBlock);
+template <typename T, int OP, int UNR>
+void launch_contig_u(const KAllContig &a, dim3 grid, hipStream_t s) {
+    const dim3 block(kBlock);
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
     if (a.src.fused) {
-        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, true, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_all_contig<T, OP, true, false>), grid, block, 0, s, a);
+        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, true, true, UNR>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_all_contig<T, OP, true, false, UNR>), grid, block, 0, s, a);
     } else {
-        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, false, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_all_contig<T, OP, false, false>), grid, block, 0, s, a);
+        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, false, true, UNR>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_all_contig<T, OP, false, false, UNR>), grid, block, 0, s, a);
     }
+}
+
+template <typename T, int OP>
+hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
+    const dim3 grid(a.blocks_per_chunk * n_chunks);
+    if (a.unroll >= 4) launch_contig_u<T, OP, 4>(a, grid, s);
+    else launch_contig_u<T, OP, 2>(a, grid, s);
     return hipGetLastError();
 }
 

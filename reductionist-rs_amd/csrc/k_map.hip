@@ -32,13 +32,13 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
         }
         const T x = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
         if (a.kind == 0) {
-            reinterpret_cast<T *>(a.out.body)[g] = x;
+            gst<T>(reinterpret_cast<T *>(a.out.body) + g, x);
             cnt += (!miss || included(a.miss, x, true)) ? 1 : 0;
         } else {
             const int64_t c = (miss && is_missing(a.miss, x)) ? 0 : 1;
-            if (a.kind == 1) reinterpret_cast<T *>(a.out.body)[g] = x;
-            else reinterpret_cast<int64_t *>(a.out.body)[g] = c;
-            a.out.counts[g] = c;
+            if (a.kind == 1) gst<T>(reinterpret_cast<T *>(a.out.body) + g, x);
+            else gst<int64_t>(reinterpret_cast<int64_t *>(a.out.body) + g, c);
+            gst<int64_t>(a.out.counts + g, c);
         }
     }
     if (a.kind == 0) {
@@ -64,14 +64,14 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *__restrict_
     for (uint64_t i0 = (uint64_t)blockIdx.x * ti; i0 < n; i0 += (uint64_t)gridDim.x * ti) {
         const uint32_t cnt = (uint32_t)((n - i0) < ti ? (n - i0) : ti);
         for (uint32_t k = 0; k < es; ++k)
-            for (uint32_t i = threadIdx.x; i < cnt; i += kBlock) tile[i * es + k] = in[(uint64_t)k * n + i0 + i];
+            for (uint32_t i = threadIdx.x; i < cnt; i += kBlock) tile[i * es + k] = gld<uint8_t>(in + (uint64_t)k * n + i0 + i);
         __syncthreads();
         const uint64_t obase = i0 * es;
         const uint32_t bytes = cnt * es;
         if ((((uintptr_t)out + obase) & 3) == 0) {
             const uint32_t words = bytes / 4;
             for (uint32_t w = threadIdx.x; w < words; w += kBlock)
-                reinterpret_cast<uint32_t *>(out + obase)[w] = reinterpret_cast<const uint32_t *>(tile)[w];
+                gst<uint32_t>(reinterpret_cast<uint32_t *>(out + obase) + w, reinterpret_cast<const uint32_t *>(tile)[w]);
             for (uint32_t q = words * 4 + threadIdx.x; q < bytes; q += kBlock) out[obase + q] = tile[q];
         } else {
             for (uint32_t q = threadIdx.x; q < bytes; q += kBlock) out[obase + q] = tile[q];
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle_big(const uint8_t *__restr
     const uint64_t total = n * es;
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j += (uint64_t)gridDim.x * kBlock) {
         const uint64_t i = j / es, k = j - i * es;
-        out[j] = in[k * n + i];
+        gst<uint8_t>(out + j, gld<uint8_t>(in + k * n + i));
     }
 }
 

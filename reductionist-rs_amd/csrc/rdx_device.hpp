@@ -33,6 +33,27 @@ __device__ __forceinline__ T from_bits64(uint64_t b) {
     return from_u<T>((U)b);
 }
 
+// Loads through the GLOBAL address space (global_load_*): generic pointers compile to flat_load_*,
+// which the compiler can only drain with vmcnt(0)+lgkmcnt(0) and which serialise the stream.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ V gld(const void *p) {
+    if constexpr (std::is_same_v<V, uint4>) {  // HIP_vector_type has no address-space copy ctor
+        typedef const __attribute__((address_space(1))) u32x4_t GV;
+        const u32x4_t v = *(GV *)(p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        typedef const __attribute__((address_space(1))) V GV;
+        return *(GV *)(p);
+    }
+}
+
+template <typename V>
+__device__ __forceinline__ void gst(void *p, V v) {
+    typedef __attribute__((address_space(1))) V GV;
+    *(GV *)(p) = v;
+}
+
 __device__ __forceinline__ uint32_t bswap_u(uint32_t x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ uint64_t bswap_u(uint64_t x) { return __builtin_bswap64(x); }
 
@@ -42,7 +63,7 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, uint64_t magic) {
 }
 
 __device__ __forceinline__ const uint8_t *chunk_base(const KSrc &s, uint32_t chunk) {
-    return s.ptrs ? s.ptrs[chunk] : s.base;
+    return s.ptrs ? gld<const uint8_t *>(s.ptrs + chunk) : s.base;
 }
 
 // One element by index e.  FUSED: byte k of element e is base[k*plane + e] (the inverse of
@@ -54,9 +75,9 @@ __device__ __forceinline__ T load_elem(const uint8_t *base, uint64_t plane, bool
     if constexpr (FUSED) {
         u = 0;
 #pragma unroll
-        for (int k = 0; k < (int)sizeof(T); ++k) u |= (U)base[(uint64_t)k * plane + e] << (8 * k);
+        for (int k = 0; k < (int)sizeof(T); ++k) u |= (U)gld<uint8_t>(base + (uint64_t)k * plane + e) << (8 * k);
     } else {
-        u = reinterpret_cast<const U *>(base)[e];
+        u = gld<U>(reinterpret_cast<const U *>(base) + e);
     }
     if (bswap) u = bswap_u(u);
     return from_u<T>(u);
@@ -283,8 +304,11 @@ __device__ __forceinline__ void block_reduce(Red<T, OP> &r) {
 // Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
 // partials in workgroup order and write the response (one launch, no second kernel).
 // Hand-off form (MI355X_MICROARCH.md "Valid forms", row 1): one lane stores the partial with
-// agent-scope (sc1) stores, drains them (s_waitcnt vmcnt(0)), then adds to the chunk's ticket;
-// the workgroup whose add returns bpc-1 reads every partial with sc1 loads after a barrier.
+// agent-scope (sc1) stores, drains them (s_waitcnt vmcnt(0)), then adds to an arrival counter;
+// the workgroup whose add completes the count reads every partial with sc1 loads after a barrier.
+// The counter is sharded 8 ways by workgroup index (b % 8 groups share an XCD under round-robin
+// dispatch) so that arrivals do not serialise on one word (~11 ns per atomic, "fanin" row); the
+// last arrival of each shard adds to the top counter.  All counters self-reset for the next launch.
 template <typename T, int OP>
 __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
     __shared__ uint32_t s_last;
@@ -296,8 +320,18 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
 #pragma unroll
         for (int i = 0; i < kPartialWords; ++i) __hip_atomic_store(P + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t prev = __hip_atomic_fetch_add(out.tickets + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == bpc - 1;
+        uint32_t *tk = out.tickets + (uint64_t)chunk * kTicketWords;
+        const uint32_t nsh = bpc < kTicketShards ? bpc : kTicketShards;
+        const uint32_t sh = b % kTicketShards;
+        const uint32_t members = (bpc - sh + kTicketShards - 1) / kTicketShards;
+        bool last = false;
+        const uint32_t p1 = __hip_atomic_fetch_add(tk + (1 + sh) * kTicketStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p1 == members - 1) {
+            __hip_atomic_store(tk + (1 + sh) * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t p2 = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = p2 == nsh - 1;
+        }
+        s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
@@ -322,7 +356,7 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
         }
         out.counts[chunk * out.counts_stride] = acc.cnt;
         if (out.status) out.status[chunk] = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
-        __hip_atomic_store(out.tickets + chunk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

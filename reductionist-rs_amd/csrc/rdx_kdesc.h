@@ -10,6 +10,9 @@ constexpr int kMaxKDims = 16;        // dims left after canonicalisation (unit d
 constexpr int kInlineMissing = 16;   // missing_values lists up to this length travel in the args
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kPartialWords = 6;     // u64 words per partial record
+constexpr uint32_t kTicketShards = 8; // arrival counter shards per chunk
+constexpr uint32_t kTicketStride = 64; // u32 words between counters: one 256 B line each
+constexpr uint32_t kTicketWords = (1 + kTicketShards) * kTicketStride;
 
 enum OpCode : uint32_t { OP_COUNT = 0, OP_MAX = 1, OP_MIN = 2, OP_SELECT = 3, OP_SUM = 4 };
 
@@ -49,7 +52,7 @@ struct KOut {
     uint64_t body_stride;     // bytes between consecutive chunks' bodies (batch)
     uint64_t counts_stride;   // elements between consecutive chunks' counts (batch)
     uint64_t *partials;       // [chunk][block] x kPartialWords
-    uint32_t *tickets;        // [chunk] arrival counters, self-resetting
+    uint32_t *tickets;        // [chunk][kTicketWords] arrival counters, self-resetting
 };
 
 // Reduction over ALL axes of a view whose elements form one ascending contiguous run
@@ -63,6 +66,8 @@ struct KAllContig {
     int64_t r0, rs;
     uint32_t filter_semantics;  // Count(All) uses missing_filter (operations.rs:25-33)
     uint32_t blocks_per_chunk;
+    uint32_t unroll;            // tiles in flight per lane (2 or 4)
+    uint32_t pad;
 };
 
 // A strided view: dims innermost-first.  offset(e) = base_off + sum idx_k * vstride_k,

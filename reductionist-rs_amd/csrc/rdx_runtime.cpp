@@ -126,13 +126,15 @@ rdx_status upload(rdx_workspace *ws, void *dst, const void *src, size_t bytes, s
 }
 
 uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
-    const uint64_t target = (uint64_t)cus * (uint64_t)env_int("RDX_BLOCKS_PER_CU", 8);
+    const uint64_t target = (uint64_t)cus * (uint64_t)env_int("RDX_BLOCKS_PER_CU", 2);
     uint64_t bpc = (target + n_chunks - 1) / n_chunks;
     const uint64_t min_tiles = (uint64_t)env_int("RDX_MIN_TILES_PER_BLOCK", 2);
     uint64_t cap = (tiles + min_tiles - 1) / min_tiles;
     if (bpc > cap) bpc = cap;
     if (bpc < 1) bpc = 1;
     if (bpc > 65536) bpc = 65536;
+    const int force = env_int("RDX_FORCE_BPC", 0);  // tuning only
+    if (force > 0) bpc = (uint64_t)force;
     return (uint32_t)bpc;
 }
 
@@ -193,8 +195,9 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             KAllContig a = p.all_contig;
             const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus);
+            a.unroll = (uint32_t)env_int("RDX_UNROLL", 2) >= 4 ? 4u : 2u;
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
-            if ((st = ensure(ws, ws->tickets, n_chunks, s, true))) return st;
+            if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
             out.tickets = ws->tickets.p;
             a.src = ksrc;
@@ -207,7 +210,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             KAllStrided a = p.all_strided;
             a.blocks_per_chunk = pick_bpc((a.view.n + 1023) / 1024, n_chunks, ws->cus);
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
-            if ((st = ensure(ws, ws->tickets, n_chunks, s, true))) return st;
+            if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
             out.tickets = ws->tickets.p;
             a.src = ksrc;

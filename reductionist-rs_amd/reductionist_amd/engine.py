@@ -39,7 +39,10 @@ class Engine:
 
     def execute_raw(self, creq: _abi.CRequest, data: bytes):
         """Host chunk in, (status, info, body, counts) out — no exception on kernel-side status."""
-        info = self.plan(creq, len(data))
+        info = _abi.rdx_response_info()
+        st = self.lib.rdx_plan(creq.ref, len(data), C.byref(info))
+        if st != _abi.OK:
+            return st, info, b"", []
         body = (C.c_uint8 * max(1, info.body_bytes))()
         counts = (C.c_int64 * max(1, info.n_counts))()
         src = C.c_char_p(bytes(data)) if len(data) else None
