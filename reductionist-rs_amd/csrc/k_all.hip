@@ -221,8 +221,14 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
 }
 
 // ---- strided views ---------------------------------------------------------------------------------
-template <typename T, int OP, bool FUSED>
+// VW > 1: the innermost canonical dim is contiguous (stride 1), its count and every other stride are
+// multiples of VW and the origin is VW-aligned, so each lane loads VW consecutive elements with one
+// 16-byte global_load.  U vectors per lane are in flight at once; the host sizes the grid so a
+// lane normally needs a single round trip.
+template <typename T, int OP, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
+    using U = typename UIntOf<T>::type;
+    constexpr int kU = VW > 1 ? 4 : 8;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
     const uint8_t *base = chunk_base(a.src, chunk);
@@ -231,19 +237,19 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
     const KView &v = a.view;
     Red<T, OP> r;
     r.init();
-    const uint64_t per = ((v.n + bpc - 1) / bpc + kBlock - 1) / kBlock * kBlock;
+    const uint64_t nv = v.n / VW;
+    const uint64_t per = ((nv + bpc - 1) / bpc + kBlock - 1) / kBlock * kBlock;
     const uint64_t g_begin = (uint64_t)b * per;
-    const uint64_t g_end = g_begin + per < v.n ? g_begin + per : v.n;
-    constexpr int kUnroll = 4;
-    for (uint64_t g0 = g_begin + threadIdx.x; g0 < g_end; g0 += kBlock * kUnroll) {
-        int64_t off[kUnroll], rk[kUnroll];
-        bool ok[kUnroll];
-        T x[kUnroll];
+    const uint64_t g_end = g_begin + per < nv ? g_begin + per : nv;
+    for (uint64_t g0 = g_begin + threadIdx.x; g0 < g_end; g0 += (uint64_t)kBlock * kU) {
+        int64_t off[kU], rk[kU];
+        bool ok[kU];
+        T x[kU][VW];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             const uint64_t g = g0 + (uint64_t)u * kBlock;
             ok[u] = g < g_end;
-            uint32_t q = (uint32_t)g;
+            uint32_t q = (uint32_t)(g * VW);
             int64_t o = v.base_off, rr = v.r0;
             for (int k = 0; k < v.ndim; ++k) {
                 const uint32_t qn = udiv(q, v.div[k].magic);
@@ -256,14 +262,27 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
             rk[u] = rr;
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-            if (ok[u]) x[u] = load_elem<T, FUSED>(base, a.src.plane, bswap, (uint64_t)off[u]);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             if (!ok[u]) continue;
-            if (miss && !included(a.miss, x[u], a.filter_semantics)) continue;
-            if constexpr (OP == OP_COUNT) r.cnt += 1;
-            else r.add(x[u], [&]() { return rk[u]; });
+            if constexpr (VW == 1) {
+                x[u][0] = load_elem<T, FUSED>(base, a.src.plane, bswap, (uint64_t)off[u]);
+            } else {
+                const uint4 w = gld<uint4>(base + (uint64_t)off[u] * sizeof(T));
+                U e[VW];
+                __builtin_memcpy(e, &w, 16);
+#pragma unroll
+                for (int j = 0; j < VW; ++j) x[u][j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (!ok[u]) continue;
+#pragma unroll
+            for (int j = 0; j < VW; ++j) {
+                if (miss && !included(a.miss, x[u][j], a.filter_semantics)) continue;
+                if constexpr (OP == OP_COUNT) r.cnt += 1;
+                else r.add(x[u][j], [&]() { return rk[u] + (int64_t)j * v.rstride[0]; });
+            }
         }
     }
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
@@ -285,16 +304,17 @@ void launch_contig_u(const KAllContig &a, dim3 grid, hipStream_t s) {
 template <typename T, int OP>
 hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
     const dim3 grid(a.blocks_per_chunk * n_chunks);
-    if (a.unroll >= 4) launch_contig_u<T, OP, 4>(a, grid, s);
-    else launch_contig_u<T, OP, 2>(a, grid, s);
+    launch_contig_u<T, OP, 2>(a, grid, s);  // 4 tiles in flight measured no faster (tools/sweep2.py)
     return hipGetLastError();
 }
 
 template <typename T, int OP>
 hipError_t launch_strided_t(const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
     const dim3 grid(a.blocks_per_chunk * n_chunks), block(kBlock);
-    if (a.src.fused) hipLaunchKernelGGL((k_all_strided<T, OP, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_all_strided<T, OP, false>), grid, block, 0, s, a);
+    constexpr int VW = 16 / sizeof(T);
+    if (a.src.fused) hipLaunchKernelGGL((k_all_strided<T, OP, true, 1>), grid, block, 0, s, a);
+    else if (a.vec > 1) hipLaunchKernelGGL((k_all_strided<T, OP, false, VW>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_all_strided<T, OP, false, 1>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 

@@ -15,45 +15,90 @@
 namespace rdx {
 namespace {
 
-template <typename T, bool FUSED>
+// VW > 1: contiguous, VW-aligned inner runs in BOTH the input view and the output (output order is
+// the traversal order), so each lane moves VW elements with one 16-byte load and one 16-byte store.
+template <typename T, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
+    using U = typename UIntOf<T>::type;
+    constexpr int kU = 4;
     const KView &v = a.view;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
     const bool bswap = a.src.bswap;
     int64_t cnt = 0;
+    const uint64_t nv = v.n / VW;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < v.n; g += stride) {
-        uint32_t q = (uint32_t)g;
-        int64_t off = v.base_off;
-        for (int k = 0; k < v.ndim; ++k) {
-            const uint32_t qn = udiv(q, v.div[k].magic);
-            off += (int64_t)(q - qn * v.count[k]) * v.vstride[k];
-            q = qn;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g0 < nv; g0 += stride * kU) {
+        int64_t off[kU];
+        bool ok[kU];
+        T x[kU][VW];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t g = g0 + (uint64_t)u * stride;
+            ok[u] = g < nv;
+            uint32_t q = (uint32_t)(g * VW);
+            int64_t o = v.base_off;
+            for (int k = 0; k < v.ndim; ++k) {
+                const uint32_t qn = udiv(q, v.div[k].magic);
+                o += (int64_t)(q - qn * v.count[k]) * v.vstride[k];
+                q = qn;
+            }
+            off[u] = o;
         }
-        const T x = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
-        if (a.kind == 0) {
-            gst<T>(reinterpret_cast<T *>(a.out.body) + g, x);
-            cnt += (!miss || included(a.miss, x, true)) ? 1 : 0;
-        } else {
-            const int64_t c = (miss && is_missing(a.miss, x)) ? 0 : 1;
-            if (a.kind == 1) gst<T>(reinterpret_cast<T *>(a.out.body) + g, x);
-            else gst<int64_t>(reinterpret_cast<int64_t *>(a.out.body) + g, c);
-            gst<int64_t>(a.out.counts + g, c);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (!ok[u]) continue;
+            if constexpr (VW == 1) {
+                x[u][0] = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off[u]);
+            } else {
+                const uint4 w = gld<uint4>(a.src.base + (uint64_t)off[u] * sizeof(T));
+                U e[VW];
+                __builtin_memcpy(e, &w, 16);
+#pragma unroll
+                for (int j = 0; j < VW; ++j) x[u][j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (!ok[u]) continue;
+            const uint64_t g = (g0 + (uint64_t)u * stride) * VW;
+            int64_t c[VW];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) {
+                if (a.kind == 0) c[j] = (!miss || included(a.miss, x[u][j], true)) ? 1 : 0;
+                else c[j] = (miss && is_missing(a.miss, x[u][j])) ? 0 : 1;
+            }
+            if (a.kind == 0) {
+#pragma unroll
+                for (int j = 0; j < VW; ++j) cnt += c[j];
+            }
+            if (a.kind != 2) {  // values
+                if constexpr (VW == 1) {
+                    gst<T>(reinterpret_cast<T *>(a.out.body) + g, x[u][0]);
+                } else {
+                    uint4 w;
+                    __builtin_memcpy(&w, x[u], 16);
+                    gst<uint4>(reinterpret_cast<T *>(a.out.body) + g, w);
+                }
+            }
+            if (a.kind != 0) {  // per-element counts (and the body itself for Count)
+#pragma unroll
+                for (int j = 0; j < VW; j += 2) {
+                    if constexpr (VW == 1) {
+                        gst<int64_t>(a.out.counts + g, c[0]);
+                        if (a.kind == 2) gst<int64_t>(reinterpret_cast<int64_t *>(a.out.body) + g, c[0]);
+                    } else {
+                        uint4 w;
+                        __builtin_memcpy(&w, &c[j], 16);
+                        gst<uint4>(a.out.counts + g + j, w);
+                        if (a.kind == 2) gst<uint4>(reinterpret_cast<int64_t *>(a.out.body) + g + j, w);
+                    }
+                }
+            }
         }
     }
     if (a.kind == 0) {
-        // integer count: order-free, one device atomic per workgroup
-        __shared__ int64_t part[kBlock / 64];
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) cnt += (int64_t)shfl_xor_u64((uint64_t)cnt, m);
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int64_t t = 0;
-            for (int k = 0; k < kBlock / 64; ++k) t += part[k];
-            if (t) __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(a.out.counts), (unsigned long long)t,
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (miss) finalize_count(cnt, a.out.counts, a.out.partials, a.out.tickets, gridDim.x, blockIdx.x);
+        else if (blockIdx.x == 0 && threadIdx.x == 0) a.out.counts[0] = (int64_t)v.n;  // sliced.len()
     }
 }
 
@@ -92,12 +137,16 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle_big(const uint8_t *__restr
 
 template <typename T>
 hipError_t launch_map_t(const KMap &a, int cus, hipStream_t s) {
-    uint64_t blocks = (a.view.n + kBlock - 1) / kBlock;
-    const uint64_t cap = (uint64_t)cus * 16;
+    constexpr int VW = 16 / sizeof(T);
+    const uint64_t vw = a.vec > 1 ? VW : 1;
+    uint64_t blocks = (a.view.n / vw + kBlock * 4 - 1) / (kBlock * 4);
+    const uint64_t cap = (uint64_t)cus * 8;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (a.src.fused) hipLaunchKernelGGL((k_map<T, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_map<T, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, s, a);
+    const dim3 grid((uint32_t)blocks), block(kBlock);
+    if (a.src.fused) hipLaunchKernelGGL((k_map<T, true, 1>), grid, block, 0, s, a);
+    else if (a.vec > 1) hipLaunchKernelGGL((k_map<T, false, VW>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_map<T, false, 1>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 

@@ -50,8 +50,14 @@ __device__ __forceinline__ V gld(const void *p) {
 
 template <typename V>
 __device__ __forceinline__ void gst(void *p, V v) {
-    typedef __attribute__((address_space(1))) V GV;
-    *(GV *)(p) = v;
+    if constexpr (std::is_same_v<V, uint4>) {
+        typedef __attribute__((address_space(1))) u32x4_t GV;
+        u32x4_t w = {v.x, v.y, v.z, v.w};
+        *(GV *)(p) = w;
+    } else {
+        typedef __attribute__((address_space(1))) V GV;
+        *(GV *)(p) = v;
+    }
 }
 
 __device__ __forceinline__ uint32_t bswap_u(uint32_t x) { return __builtin_bswap32(x); }
@@ -357,6 +363,51 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
         out.counts[chunk * out.counts_stride] = acc.cnt;
         if (out.status) out.status[chunk] = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
         __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Integer count across workgroups without a hot atomic: every workgroup publishes its count, the
+// sharded arrival counters elect the last one, which sums the counts (order-free: integers) and
+// writes `*dst`.  Same hand-off form as finalize_all.
+__device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint64_t *partials, uint32_t *tickets,
+                                      uint32_t nblocks, uint32_t b) {
+    __shared__ int64_t part[kBlock / 64];
+    __shared__ uint32_t s_last;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) cnt += (int64_t)shfl_xor_u64((uint64_t)cnt, m);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int k = 0; k < kBlock / 64; ++k) t += part[k];
+        __hip_atomic_store(partials + b, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t nsh = nblocks < kTicketShards ? nblocks : kTicketShards;
+        const uint32_t sh = b % kTicketShards;
+        const uint32_t members = (nblocks - sh + kTicketShards - 1) / kTicketShards;
+        bool last = false;
+        const uint32_t p1 = __hip_atomic_fetch_add(tickets + (1 + sh) * kTicketStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p1 == members - 1) {
+            __hip_atomic_store(tickets + (1 + sh) * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    int64_t t = 0;
+    for (uint32_t j = threadIdx.x; j < nblocks; j += kBlock)
+        t += (int64_t)__hip_atomic_load(partials + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) t += (int64_t)shfl_xor_u64((uint64_t)t, m);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t tot = 0;
+        for (int k = 0; k < kBlock / 64; ++k) tot += part[k];
+        *dst = tot;
+        __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -91,6 +91,8 @@ struct KAllStrided {
     KView view;
     uint32_t filter_semantics;
     uint32_t blocks_per_chunk;
+    uint32_t vec;       // elements per 16-byte lane load along the contiguous inner dim (1 = scalar)
+    uint32_t pad;
 };
 
 // Reduction over a subset of axes.  Output o (C order over kept dims) reduces the elements
@@ -119,7 +121,7 @@ struct KMap {
     KView view;
     uint32_t kind;    // 0 = select (values + non-missing count), 1 = zero-axes values+0/1 counts,
                       // 2 = zero-axes counts only (Count op: body = counts)
-    uint32_t pad;
+    uint32_t vec;     // elements per 16-byte lane load/store (1 = scalar)
 };
 
 }  // namespace rdx

@@ -138,6 +138,23 @@ uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
     return (uint32_t)bpc;
 }
 
+// Lanes may move 16 bytes of a view at once when its innermost dim is a contiguous, aligned run.
+uint32_t vec_width(const KView &v, uint32_t esz, const uint8_t *base, const uint8_t *const *ptrs, uint64_t n_chunks,
+                   bool fused) {
+    const uint32_t vw = 16 / esz;
+    if (fused || env_int("RDX_NO_VEC", 0)) return 1;
+    if (v.ndim < 1 || v.vstride[0] != 1 || v.count[0] % vw != 0 || v.base_off % (int64_t)vw != 0) return 1;
+    for (int k = 1; k < v.ndim; ++k)
+        if (v.vstride[k] % (int64_t)vw != 0) return 1;
+    if (ptrs) {
+        for (uint64_t i = 0; i < n_chunks; ++i)
+            if ((uintptr_t)ptrs[i] % 16) return 1;
+    } else if ((uintptr_t)base % 16) {
+        return 1;
+    }
+    return vw;
+}
+
 // Everything after planning for n_chunks chunks that share the plan (device pointers only).
 rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, const uint8_t *const *h_ptrs,
                       uint64_t n_chunks, uint64_t len, uint8_t *d_body, int64_t *d_counts, uint32_t *d_status,
@@ -208,7 +225,15 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
         }
         case Mode::AllStrided: {
             KAllStrided a = p.all_strided;
-            a.blocks_per_chunk = pick_bpc((a.view.n + 1023) / 1024, n_chunks, ws->cus);
+            a.vec = vec_width(a.view, p.esz, src, n_chunks > 1 ? h_ptrs : nullptr, n_chunks, p.fused);
+            {   // one round trip per lane when possible: kU vectors of `vec` elements per lane
+                const uint64_t per_block = (uint64_t)kBlock * (a.vec > 1 ? 4 : 8);
+                const uint64_t want = (a.view.n / a.vec + per_block - 1) / per_block;
+                uint64_t cap = ((uint64_t)ws->cus * 8 + n_chunks - 1) / n_chunks;
+                a.blocks_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min(want, std::max<uint64_t>(cap, 1)));
+                const int force = env_int("RDX_FORCE_BPC", 0);
+                if (force > 0) a.blocks_per_chunk = (uint32_t)force;
+            }
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
@@ -245,9 +270,19 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
         }
         case Mode::Map: {
             KMap a = p.map;
+            a.vec = vec_width(a.view, p.esz, src, nullptr, 1, p.fused);
+            if ((uintptr_t)d_body % 16 || (a.kind != 0 && (uintptr_t)d_counts % 16)) a.vec = 1;
             if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
-            if (a.kind == 0) RDX_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t), s));
-            if (a.view.n == 0) return RDX_OK;
+            if (a.view.n == 0) {
+                if (a.kind == 0) RDX_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t), s));
+                return RDX_OK;
+            }
+            if (a.kind == 0) {
+                if ((st = ensure(ws, ws->partials, (uint64_t)ws->cus * 8, s))) return st;
+                if ((st = ensure(ws, ws->tickets, kTicketWords, s, true))) return st;
+                out.partials = ws->partials.p;
+                out.tickets = ws->tickets.p;
+            }
             a.src = ksrc;
             a.miss = miss;
             a.out = out;

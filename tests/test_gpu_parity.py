@@ -82,6 +82,9 @@ def test_larger_strided_views(engine, dtype, op):
         ([64, 48, 40], [[60, 3, -1], [1, 47, 3], [-1, -41, -2]], None, "F"),
         ([64, 48, 40], [[3, 60, 1], [0, 48, 2], [5, 37, 1]], [1], "C"),
         ([64, 48, 40], None, [0, 2], "C"),
+        ([64, 48, 40], [[3, 60, 1], [0, 48, 2], [8, 40, 1]], None, "C"),     # 16-B vector lanes
+        ([64, 48, 40], [[3, 60, 1], [0, 48, 2], [8, 40, 1]], [], "C"),
+        ([64, 48, 40], [[3, 60, 1], [0, 48, 2], [8, 40, 1]], [], "F"),
         ([64, 48, 40], None, [2], "F"),
         ([300, 500], None, 0, "C"),
         ([300, 500], [[0, 300, 1], [10, 490, 7]], 1, "C"),

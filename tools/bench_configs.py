@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Per-config measurements beyond bench.py's headline (BASELINE.json configs 3 and 5, single-chunk
+C2, host-inclusive rates).  Device-resident timings: HIP events on the launch stream around K
+back-to-back launches over rotating buffers whose total exceeds the 256 MiB Infinity Cache.
+Prints one JSON object per measurement."""
+import ctypes as C
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "reductionist-rs_amd"), str(ROOT)]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from reductionist_amd import Engine, _abi  # noqa: E402
+
+PEAK = 8000.0
+eng = Engine([0])
+ws = eng.workspace(0)
+lib = _abi.lib()
+stream = torch.cuda.current_stream()
+SH = C.c_void_p(stream.cuda_stream)
+
+
+def dev_time(creq, bufs, nbytes, out_bytes, k=50):
+    body = torch.empty(max(16, out_bytes), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(1 << 20, dtype=torch.int64, device="cuda")
+    status = torch.zeros(4, dtype=torch.int32, device="cuda")
+    info = _abi.rdx_response_info()
+    args = [(ws.ws, creq.ref, C.c_void_p(b.data_ptr()), nbytes, C.c_void_p(body.data_ptr()),
+             C.c_void_p(counts.data_ptr()), C.c_void_p(status.data_ptr()), SH, C.byref(info)) for b in bufs]
+    for i in range(5):
+        assert lib.rdx_execute_device(*args[i % len(args)]) == 0
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for i in range(k):
+        lib.rdx_execute_device(*args[i % len(args)])
+    e1.record(stream)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    return e0.elapsed_time(e1) / 1e3 / k
+
+
+def report(name, t, alg_bytes, chunk_bytes, **kw):
+    d = {"config": name, "us_per_launch": round(t * 1e6, 2), "bytes_alg": alg_bytes,
+         "GBs_alg": round(alg_bytes / t / 1e9, 1), "roofline_frac": round(alg_bytes / t / 1e9 / PEAK, 4),
+         "GiBs_chunk": round(chunk_bytes / t / 2 ** 30, 1)}
+    d.update(kw)
+    print(json.dumps(d), flush=True)
+
+
+# ---- C3: f64 [128,128,128], selection, missing_value -9999 @5 %, min / max / valid_range ----------------
+rng = np.random.default_rng(0x5EED0005)
+v = rng.standard_normal(128 ** 3) * 100
+v[rng.random(v.size) < 0.05] = -9999.0
+c3 = [torch.from_numpy(v.view(np.uint8).copy()).cuda() for _ in range(20)]  # 320 MiB rotating
+sel = [[8, 120, 1], [0, 128, 2], [16, 112, 1]]
+n_sel = 112 * 64 * 96
+for op, miss in (("min", ("missing_value", -9999.0)), ("max", ("missing_value", -9999.0)),
+                 ("max", ("valid_range", [-250.0, 250.0])), ("sum", ("missing_value", -9999.0))):
+    vals = miss[1] if isinstance(miss[1], list) else [miss[1]]
+    mv = b"".join(np.float64(x).tobytes() for x in vals)
+    creq = _abi.CRequest(op, "float64", shape=[128, 128, 128], selection=sel, missing_kind=miss[0],
+                         missing_values=mv, n_missing=len(vals))
+    t = dev_time(creq, c3, 128 ** 3 * 8, 8)
+    report(f"c3_{op}_{miss[0]}", t, n_sel * 8 + 16, 128 ** 3 * 8, n_selected=n_sel)
+del c3
+
+# ---- C5: i64 [512,256,256] select [[0,512,1],[64,192,1],[0,256,1]] -> 128 MiB out ----------------------
+g = torch.Generator(device="cuda")
+g.manual_seed(0x5EED0006)
+c5 = [torch.randint(-2 ** 62, 2 ** 62, (512 * 256 * 256,), dtype=torch.int64, device="cuda", generator=g).view(torch.uint8)
+      for _ in range(2)]
+creq5 = _abi.CRequest("select", "int64", shape=[512, 256, 256], selection=[[0, 512, 1], [64, 192, 1], [0, 256, 1]])
+t = dev_time(creq5, c5, 256 << 20, 128 << 20, k=20)
+report("c5_select_device", t, (128 << 20) * 2, 256 << 20, note="128 MiB read + 128 MiB written")
+
+# host-inclusive C5: host chunk in (pageable), 128 MiB body out (pageable) through rdx_execute
+host5 = c5[0].cpu().numpy().tobytes()
+del c5
+t0 = time.perf_counter()
+reps = 3
+for _ in range(reps):
+    st, info, body, counts = eng.execute_raw(creq5, host5)
+    assert st == 0
+t = (time.perf_counter() - t0) / reps
+print(json.dumps({"config": "c5_select_host_inclusive", "ms_per_call": round(t * 1e3, 2),
+                  "GiBs_chunk": round((256 << 20) / t / 2 ** 30, 2),
+                  "note": "rdx_execute: pageable H2D 256 MiB + kernel + pageable D2H 128 MiB + ctypes copies"}), flush=True)
+
+# ---- C2 host-inclusive: 64 MiB shuffled big-endian f32 from host memory ---------------------------------
+vals = np.random.default_rng(4).random(16 << 20, dtype=np.float32)
+host2 = vals.astype(">f4").view(np.uint8).reshape(-1, 4).T.copy().tobytes()
+creq2 = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
+for _ in range(2):
+    eng.execute_raw(creq2, host2)
+t0 = time.perf_counter()
+reps = 10
+for _ in range(reps):
+    st, info, body, counts = eng.execute_raw(creq2, host2)
+t = (time.perf_counter() - t0) / reps
+print(json.dumps({"config": "c2_host_inclusive", "ms_per_call": round(t * 1e3, 3),
+                  "GiBs_chunk": round((64 << 20) / t / 2 ** 30, 2),
+                  "note": "rdx_execute: pageable H2D 64 MiB + kernel + 16 B D2H"}), flush=True)
+ws.close()
+eng.close()
