@@ -109,9 +109,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local_rank)
-
     from reductionist_amd import Engine, _abi
+    from reductionist_amd.sharding import device_for, shard_range
+
+    device = device_for(local_rank, torch.cuda.device_count())
+    torch.cuda.set_device(device)
 
     def barrier():
         if world > 1:
@@ -124,8 +126,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    eng = Engine([local_rank])
-    ws = eng.workspace(local_rank)
+    eng = Engine([device])
+    ws = eng.workspace(device)
     lib = _abi.lib()
     stream = torch.cuda.current_stream()
     sh = C.c_void_p(stream.cuda_stream)
@@ -209,8 +211,9 @@ def main():
 
     # ---- C4 (extra): 1024 x 4 MiB chunks, one batched launch per step ----------------------------------
     if not args.no_c4:
-        n_local = C4_CHUNKS // world + (1 if rank < C4_CHUNKS % world else 0)
-        g.manual_seed(0x5EED1000 + rank)
+        lo4, hi4 = shard_range(C4_CHUNKS, rank, world)
+        n_local = hi4 - lo4
+        g.manual_seed(0x5EED1000 + lo4)
         v4 = torch.rand(n_local, C4_ELEMS, device="cuda", generator=g, dtype=torch.float32)
         ex4 = v4.double().sum(dim=1).cpu()
         # native byte order, shuffle es=4

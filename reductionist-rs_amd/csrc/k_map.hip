@@ -26,15 +26,19 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
     const bool bswap = a.src.bswap;
     int64_t cnt = 0;
     const uint64_t nv = v.n / VW;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t g0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g0 < nv; g0 += stride * kU) {
+    // each workgroup streams one contiguous stretch of the output (and of each input row)
+    const uint64_t per = ((nv + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+    const uint64_t g_begin = (uint64_t)blockIdx.x * per;
+    const uint64_t g_end = g_begin + per < nv ? g_begin + per : nv;
+    const uint64_t stride = kBlock;
+    for (uint64_t g0 = g_begin + threadIdx.x; g0 < g_end; g0 += stride * kU) {
         int64_t off[kU];
         bool ok[kU];
         T x[kU][VW];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const uint64_t g = g0 + (uint64_t)u * stride;
-            ok[u] = g < nv;
+            ok[u] = g < g_end;
             uint32_t q = (uint32_t)(g * VW);
             int64_t o = v.base_off;
             for (int k = 0; k < v.ndim; ++k) {
