@@ -162,6 +162,13 @@ rdx_status rdx_missing_from_i64(uint32_t dtype, int64_t v, void *out);
 rdx_status rdx_missing_from_u64(uint32_t dtype, uint64_t v, void *out);
 rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out);
 
+/* Page-locked host buffers: a host that downloads chunks straight into these (s3_client.rs:215-233
+ * today copies into an 8-byte aligned Vec) lets rdx_execute DMA them without a staging copy, and
+ * large responses (select) come back at full PCIe rate.  Any host pointer is accepted by
+ * rdx_execute; pinned ones are detected and used directly. */
+rdx_status rdx_host_alloc(rdx_context *ctx, uint64_t bytes, void **out);
+void rdx_host_free(rdx_context *ctx, void *p);
+
 /* ---- execution ------------------------------------------------------------------------------------ */
 /* Host-resident chunk in, host-resident response out (the drop-in for operation<T>()).
  * `chunk` is borrowed read-only; body/counts are caller-provided with capacities from rdx_plan.

@@ -473,6 +473,18 @@ rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out) {
     return RDX_E_INVALID_ARGUMENT;
 }
 
+rdx_status rdx_host_alloc(rdx_context *ctx, uint64_t bytes, void **out) {
+    if (!ctx || !out) return RDX_E_INVALID_ARGUMENT;
+    RDX_HIP(hipSetDevice(ctx->devices[0]));
+    RDX_HIP(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable));
+    return RDX_OK;
+}
+
+void rdx_host_free(rdx_context *ctx, void *p) {
+    (void)ctx;
+    if (p) (void)hipHostFree(p);
+}
+
 rdx_status rdx_workspace_create(rdx_context *ctx, int device, rdx_workspace **out) {
     if (!ctx || !out) return RDX_E_INVALID_ARGUMENT;
     return create_workspace(device, out);

@@ -138,6 +138,8 @@ def _declare(lib):
         "rdx_missing_from_u64": (C.c_int, [C.c_uint32, C.c_uint64, VP]),
         "rdx_missing_from_f64": (C.c_int, [C.c_uint32, C.c_double, VP]),
         "rdx_execute": (C.c_int, [VP, req_p, VP, U64, VP, U64, P(C.c_int64), U64, info_p]),
+        "rdx_host_alloc": (C.c_int, [VP, U64, P(VP)]),
+        "rdx_host_free": (None, [VP, VP]),
         "rdx_workspace_create": (C.c_int, [VP, C.c_int, P(VP)]),
         "rdx_workspace_destroy": (None, [VP]),
         "rdx_execute_device": (C.c_int, [VP, req_p, VP, U64, VP, VP, VP, VP, info_p]),
@@ -153,7 +155,8 @@ def _declare(lib):
 _LIB = None
 EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_context_create",
             "rdx_context_destroy", "rdx_validate_request", "rdx_plan", "rdx_missing_from_i64",
-            "rdx_missing_from_u64", "rdx_missing_from_f64", "rdx_execute", "rdx_workspace_create",
+            "rdx_missing_from_u64", "rdx_missing_from_f64", "rdx_execute", "rdx_host_alloc", "rdx_host_free",
+            "rdx_workspace_create",
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device"]
 
 
