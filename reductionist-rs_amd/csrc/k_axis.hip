@@ -5,11 +5,13 @@
 // zero in the reference's fold order: F order over the reduced axes in request order (fold_axis
 // over the first axis, then over the partials along the next, operations.rs:229-258).
 //
-//  k_axis_rows — innermost memory dim is reduced: one wave per (output, slice); lanes stride the
-//                reduced elements (coalesced), butterfly reduce.
-//  k_axis_cols — innermost memory dim is kept: one lane per (output, slice); consecutive lanes
-//                read consecutive addresses, each walks its reduced elements.
-//  k_axis_combine — when the reduced range is split into slices, fold the slices in order.
+//  k_axis_rows<VW> — the innermost memory dim is reduced: one wave per (output, slice); each lane
+//                    loads VW consecutive elements (16 B when VW > 1), 4 loads in flight, butterfly.
+//  k_axis_cols<VW> — otherwise: a workgroup owns a tile of 64 lanes x VW consecutive outputs along
+//                    the innermost kept dim (16 B loads across lanes = coalesced rows); its 4 waves
+//                    split the slice's reduced elements (8 loads in flight per lane) and combine
+//                    through LDS.
+//  k_axis_combine  — when the reduced range is split into slices, fold the slices in order.
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
 
@@ -33,6 +35,12 @@ __device__ __forceinline__ void write_partial(const KOut &out, uint64_t idx, con
     r.to_words(w);
 #pragma unroll
     for (int i = 0; i < kPartialWords; ++i) out.partials[idx * kPartialWords + i] = w[i];
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void emit(const KAxis &a, uint64_t oi, uint64_t s, const Red<T, OP> &r) {
+    if (a.slices == 1) write_result(a.out, oi, r);
+    else write_partial(a.out, oi * a.slices + s, r);
 }
 
 __device__ __forceinline__ int64_t kept_offset(const KView &kv, uint32_t t, int64_t &out_index) {
@@ -64,71 +72,122 @@ __device__ __forceinline__ int64_t red_offset(const KView &rv, uint32_t r, int64
     return off;
 }
 
-template <typename T, int OP, bool FUSED>
+// VW consecutive elements at element offset `off` (16-byte aligned when VW > 1).
+template <typename T, bool FUSED, int VW>
+__device__ __forceinline__ void load_vec(const KSrc &src, int64_t off, T (&x)[VW]) {
+    using U = typename UIntOf<T>::type;
+    if constexpr (VW == 1) {
+        x[0] = load_elem<T, FUSED>(src.base, src.plane, src.bswap, (uint64_t)off);
+    } else {
+        const uint4 w = gld<uint4>(src.base + (uint64_t)off * sizeof(T));
+        U e[VW];
+        __builtin_memcpy(e, &w, 16);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) x[j] = from_u<T>(src.bswap ? bswap_u(e[j]) : e[j]);
+    }
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void fold_in(Red<T, OP> &r, const KMissing &miss, bool has_miss, T x, int64_t rank) {
+    if (has_miss && is_missing(miss, x)) return;
+    if constexpr (OP == OP_COUNT) r.cnt += 1;
+    else r.add(x, [&]() { return rank; });
+}
+
+template <typename T, int OP, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
+    constexpr int kU = 4;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
     const uint64_t items = a.n_out * a.slices;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
-    const bool bswap = a.src.bswap;
+    const uint64_t nrv = a.n_red / VW;  // reduced vectors per output
     for (uint64_t it = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); it < items; it += nw) {
         const uint64_t o = it / a.slices, s = it - o * a.slices;
         int64_t oi;
         const int64_t koff = kept_offset(a.kept, (uint32_t)o, oi);
-        const uint64_t r_lo = s * a.n_red / a.slices, r_hi = (s + 1) * a.n_red / a.slices;
+        const uint64_t r_lo = s * nrv / a.slices, r_hi = (s + 1) * nrv / a.slices;
         Red<T, OP> r;
         r.init();
-        for (uint64_t ri = r_lo + lane; ri < r_hi; ri += 64) {
-            int64_t rk;
-            const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)ri, rk);
-            const T x = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
-            if (miss && is_missing(a.miss, x)) continue;
-            if constexpr (OP == OP_COUNT) r.cnt += 1;
-            else r.add(x, [&]() { return rk; });
+        for (uint64_t r0 = r_lo + lane; r0 < r_hi; r0 += 64 * kU) {
+            T x[kU][VW];
+            int64_t rk[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t rv = r0 + (uint64_t)u * 64;
+                if (rv < r_hi) {
+                    const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)(rv * VW), rk[u]);
+                    load_vec<T, FUSED, VW>(a.src, off, x[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                if (r0 + (uint64_t)u * 64 >= r_hi) continue;
+#pragma unroll
+                for (int j = 0; j < VW; ++j) fold_in(r, a.miss, miss, x[u][j], rk[u] + (int64_t)j * a.red.rstride[0]);
+            }
         }
         wave_reduce(r);
-        if (lane == 0) {
-            if (a.slices == 1) write_result(a.out, (uint64_t)oi, r);
-            else write_partial(a.out, (uint64_t)oi * a.slices + s, r);
-        }
+        if (lane == 0) emit(a, (uint64_t)oi, s, r);
     }
 }
 
-template <typename T, int OP, bool FUSED>
+template <typename T, int OP, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    constexpr int kU = 8;
+    constexpr int kWaves = kBlock / 64;
+    __shared__ uint64_t lds[kWaves - 1][64][VW][kPartialWords];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t nkv = a.n_out / VW;             // kept vectors
+    const uint64_t kv = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t s = blockIdx.y;
-    if (t >= a.n_out) return;
+    const bool active = kv < nkv;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
-    const bool bswap = a.src.bswap;
-    int64_t oi;
-    const int64_t koff = kept_offset(a.kept, (uint32_t)t, oi);
+    int64_t oi = 0, koff = 0;
+    if (active) koff = kept_offset(a.kept, (uint32_t)(kv * VW), oi);
     const uint64_t r_lo = s * a.n_red / a.slices, r_hi = (s + 1) * a.n_red / a.slices;
-    Red<T, OP> r;
-    r.init();
-    constexpr int kU = 4;
-    for (uint64_t r0 = r_lo; r0 < r_hi; r0 += kU) {
-        T x[kU];
-        int64_t rk[kU];
+    Red<T, OP> r[VW];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (r0 + u < r_hi) {
-                const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)(r0 + u), rk[u]);
-                x[u] = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off);
+    for (int j = 0; j < VW; ++j) r[j].init();
+    if (active) {
+        for (uint64_t r0 = r_lo + wave; r0 < r_hi; r0 += (uint64_t)kWaves * kU) {
+            T x[kU][VW];
+            int64_t rk[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t rr = r0 + (uint64_t)u * kWaves;
+                if (rr < r_hi) {
+                    const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)rr, rk[u]);
+                    load_vec<T, FUSED, VW>(a.src, off, x[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                if (r0 + (uint64_t)u * kWaves >= r_hi) continue;
+#pragma unroll
+                for (int j = 0; j < VW; ++j) fold_in(r[j], a.miss, miss, x[u][j], rk[u]);
             }
         }
+    }
+    // combine the 4 waves' partial states of each output in wave order
+    if (wave > 0) {
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (r0 + u >= r_hi) continue;
-            if (miss && is_missing(a.miss, x[u])) continue;
-            if constexpr (OP == OP_COUNT) r.cnt += 1;
-            else r.add(x[u], [&]() { return rk[u]; });
+        for (int j = 0; j < VW; ++j) r[j].to_words(lds[wave - 1][lane][j]);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            for (int w = 0; w < kWaves - 1; ++w) {
+                Red<T, OP> o;
+                o.from_words(lds[w][lane][j]);
+                r[j].merge(o);
+            }
+            emit(a, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), s, r[j]);
         }
     }
-    if (a.slices == 1) write_result(a.out, (uint64_t)oi, r);
-    else write_partial(a.out, (uint64_t)oi * a.slices + s, r);
 }
 
 template <typename T, int OP>
@@ -145,8 +204,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_combine(const KAxis a) {
     write_result(a.out, o, acc);
 }
 
-template <typename T, int OP>
-hipError_t launch_axis_t(const KAxis &a, int cus, hipStream_t st) {
+template <typename T, int OP, int VW>
+void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
     const dim3 block(kBlock);
     if (a.mode == 0) {
         const uint64_t items = a.n_out * a.slices;
@@ -154,15 +213,22 @@ hipError_t launch_axis_t(const KAxis &a, int cus, hipStream_t st) {
         const uint64_t cap = (uint64_t)cus * 16;
         if (blocks > cap) blocks = cap;
         if (blocks == 0) blocks = 1;
-        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true>), dim3((uint32_t)blocks), block, 0, st, a);
-        else hipLaunchKernelGGL((k_axis_rows<T, OP, false>), dim3((uint32_t)blocks), block, 0, st, a);
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true, 1>), dim3((uint32_t)blocks), block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW>), dim3((uint32_t)blocks), block, 0, st, a);
     } else {
-        const dim3 grid((uint32_t)((a.n_out + kBlock - 1) / kBlock), a.slices);
-        if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((k_axis_cols<T, OP, false>), grid, block, 0, st, a);
+        const dim3 grid((uint32_t)((a.n_out / VW + 63) / 64), a.slices);
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_cols<T, OP, false, VW>), grid, block, 0, st, a);
     }
+}
+
+template <typename T, int OP>
+hipError_t launch_axis_t(const KAxis &a, int cus, hipStream_t st) {
+    if (a.vec > 1 && !a.src.fused) launch_axis_vw<T, OP, 16 / sizeof(T)>(a, cus, st);
+    else launch_axis_vw<T, OP, 1>(a, cus, st);
     if (a.slices > 1)
-        hipLaunchKernelGGL((k_axis_combine<T, OP>), dim3((uint32_t)((a.n_out + kBlock - 1) / kBlock)), block, 0, st, a);
+        hipLaunchKernelGGL((k_axis_combine<T, OP>), dim3((uint32_t)((a.n_out + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           st, a);
     return hipGetLastError();
 }
 

@@ -108,7 +108,9 @@ struct KAxis {
     uint64_t n_out;
     uint64_t n_red;
     uint32_t slices;
-    uint32_t mode;   // 0 = rows (a wave per output), 1 = cols (a thread per output)
+    uint32_t mode;   // 0 = rows (a wave per output), 1 = cols (a lane per output)
+    uint32_t vec;    // elements per 16-byte lane load (1 = scalar)
+    uint32_t pad;
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

@@ -517,9 +517,12 @@ rdx_status make_plan(const rdx_request &req, uint64_t len, ExecPlan &p) {
     int64_t minK = INT64_MAX, minR = INT64_MAX;
     for (const CDim &d : K) minK = std::min<int64_t>(minK, std::llabs(d.vs));
     for (const CDim &d : R) minR = std::min<int64_t>(minR, d.vs);
-    ax.mode = (minR <= minK) ? 0u : 1u;  // 0 rows: innermost memory dim is reduced
     std::stable_sort(R.begin(), R.end(), [](const CDim &a, const CDim &b) { return a.vs < b.vs; });
     R = merge_inner_first(R, p.need_rank);
+    // rows (a wave per output) when the innermost memory dim is reduced AND its contiguous run fills
+    // at least a 64-lane x 4 B wave access; otherwise a lane per output along the innermost kept dim.
+    const bool long_run = !R.empty() && R[0].vs == 1 && R[0].count * p.esz >= 256;
+    ax.mode = (minR <= minK && (long_run || K.empty())) ? 0u : 1u;
     if (ax.mode == 1)
         std::stable_sort(K.begin(), K.end(), [](const CDim &a, const CDim &b) { return std::llabs(a.vs) < std::llabs(b.vs); });
     else

@@ -249,12 +249,23 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
             if (a.n_out == 0) return RDX_OK;
             uint64_t slices = 1;
+            {   // 16-byte lanes when every stride keeps vectors aligned and inside one dim
+                const uint32_t vw = 16 / p.esz;
+                const KView &inner = a.mode == 0 ? a.red : a.kept;
+                bool ok = !p.fused && !env_int("RDX_NO_VEC", 0) && inner.ndim >= 1 && inner.vstride[0] == 1 &&
+                          inner.count[0] % vw == 0 && a.kept.base_off % (int64_t)vw == 0 && (uintptr_t)src % 16 == 0;
+                for (int k = 0; k < a.kept.ndim; ++k) ok = ok && (a.mode == 1 && k == 0 ? true : a.kept.vstride[k] % (int64_t)vw == 0);
+                for (int k = 0; k < a.red.ndim; ++k) ok = ok && (a.mode == 0 && k == 0 ? true : a.red.vstride[k] % (int64_t)vw == 0);
+                a.vec = ok ? vw : 1;
+            }
             if (a.mode == 0) {
-                const uint64_t target = (uint64_t)ws->cus * 64;
-                if (a.n_out < target) slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (a.n_red + 1023) / 1024);
+                const uint64_t target = (uint64_t)ws->cus * 16;                      // waves
+                const uint64_t nrv = a.n_red / a.vec;
+                if (a.n_out < target) slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (nrv + 255) / 256);
             } else {
-                const uint64_t target = (uint64_t)ws->cus * 256;
-                if (a.n_out < target) slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (a.n_red + 63) / 64);
+                const uint64_t tiles = (a.n_out / a.vec + 63) / 64;
+                const uint64_t target = (uint64_t)ws->cus * 4;                       // workgroups
+                if (tiles < target) slices = std::min<uint64_t>((target + tiles - 1) / tiles, (a.n_red + 31) / 32);
             }
             slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, 65535));
             a.slices = (uint32_t)slices;

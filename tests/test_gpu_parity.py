@@ -91,6 +91,11 @@ def test_larger_strided_views(engine, dtype, op):
         ([7, 9000], None, 1, "C"),
         ([9000, 7], None, 0, "C"),
         ([9000, 7], None, [], "F"),
+        ([16, 8, 128], None, [2], "C"),          # rows mode, 16-B lanes
+        ([4, 20000], None, 1, "C"),              # rows mode, few outputs -> slices
+        ([20000, 8], None, 0, "C"),              # cols mode, 16-B lanes, slices
+        ([8, 20000], None, 0, "F"),              # F order: kept dim contiguous
+        ([32, 64, 24], [[0, 32, 1], [8, 64, 2], [0, 24, 1]], [0, 1], "C"),
     ):
         n = int(np.prod(shape))
         vals = rng.integers(-100, 100, n).astype(NP[dtype]) if dtype.startswith("float") else \

@@ -24,8 +24,11 @@ SH = C.c_void_p(stream.cuda_stream)
 
 
 def dev_time(creq, bufs, nbytes, out_bytes, k=50):
-    body = torch.empty(max(16, out_bytes), dtype=torch.uint8, device="cuda")
-    counts = torch.zeros(1 << 20, dtype=torch.int64, device="cuda")
+    info = _abi.rdx_response_info()
+    assert lib.rdx_plan(creq.ref, nbytes, C.byref(info)) == 0
+    assert out_bytes >= info.body_bytes, "body buffer smaller than the planned response"
+    body = torch.empty(max(16, info.body_bytes), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(max(1, info.n_counts), dtype=torch.int64, device="cuda")  # sized from rdx_plan
     status = torch.zeros(4, dtype=torch.int32, device="cuda")
     info = _abi.rdx_response_info()
     args = [(ws.ws, creq.ref, C.c_void_p(b.data_ptr()), nbytes, C.c_void_p(body.data_ptr()),
@@ -41,6 +44,25 @@ def dev_time(creq, bufs, nbytes, out_bytes, k=50):
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
     return e0.elapsed_time(e1) / 1e3 / k
+
+
+def cpu_time(creq, data, seconds=3.0):
+    """Oracle (sequential restatement of the reference path) on one host core."""
+    from oracle import py_oracle as oracle
+    L = oracle.lib()
+    src = C.create_string_buffer(data, len(data))
+    cap = len(data) + 64
+    body = (C.c_uint8 * cap)()
+    counts = (C.c_int64 * (len(data) // 4 + 8))()
+    info = _abi.rdx_response_info()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        assert L.oracle_execute(C.addressof(creq.c), src, len(data), body, cap, counts, len(data) // 4 + 8,
+                                C.byref(info)) == 0
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    return (time.perf_counter() - t0) / reps
 
 
 def report(name, t, alg_bytes, chunk_bytes, **kw):
@@ -65,8 +87,47 @@ for op, miss in (("min", ("missing_value", -9999.0)), ("max", ("missing_value", 
     creq = _abi.CRequest(op, "float64", shape=[128, 128, 128], selection=sel, missing_kind=miss[0],
                          missing_values=mv, n_missing=len(vals))
     t = dev_time(creq, c3, 128 ** 3 * 8, 8)
-    report(f"c3_{op}_{miss[0]}", t, n_sel * 8 + 16, 128 ** 3 * 8, n_selected=n_sel)
+    tc = cpu_time(creq, v.tobytes())
+    report(f"c3_{op}_{miss[0]}", t, n_sel * 8 + 16, 128 ** 3 * 8, n_selected=n_sel,
+           cpu_oracle_us=round(tc * 1e6, 1), gpu_over_cpu=round(tc / t, 1))
 del c3
+
+# ---- C1 (CPU-only config in BASELINE): f32 4 MiB contiguous sum; D-int and D-real ------------------------
+for seed, real in ((0x5EED0001, False), (0x5EED0002, True)):
+    r1 = np.random.default_rng(seed)
+    v1 = (r1.random(1 << 20, dtype=np.float32) if real else r1.integers(-8, 9, 1 << 20).astype(np.float32))
+    creq1 = _abi.CRequest("sum", "float32")
+    tc = cpu_time(creq1, v1.tobytes())
+    bufs = [torch.from_numpy(v1.view(np.uint8).copy()).cuda() for _ in range(80)]   # 320 MiB rotating
+    t = dev_time(creq1, bufs, 4 << 20, 4)
+    report("c1_sum_4MiB_" + ("real" if real else "int"), t, 4 << 20, 4 << 20, cpu_oracle_us=round(tc * 1e6, 1),
+           cpu_oracle_GiBs=round((4 << 20) / tc / 2 ** 30, 3), gpu_over_cpu=round(tc / t, 1))
+    del bufs
+
+# ---- axis reductions ---------------------------------------------------------------------------------
+ra = np.random.default_rng(7)
+for name, dtype, shape, axis, op in (("axis1_f32_4096x4096_sum", "float32", [4096, 4096], 1, "sum"),
+                                     ("axis0_f32_4096x4096_sum", "float32", [4096, 4096], 0, "sum"),
+                                     ("axes02_f64_128cube_max", "float64", [128, 128, 128], [0, 2], "max"),
+                                     ("axis1_f32_64x1024x256_sum", "float32", [64, 1024, 256], 1, "sum"),
+                                     ("axis2_i32_256x256x256_count_missing", "int32", [256, 256, 256], 2, "count"),
+                                     ("axisnone_f32_16M_min_map", "float32", [4096, 4096], [], "min")):
+    n = int(np.prod(shape))
+    vals = (ra.standard_normal(n) if dtype.startswith("f") else ra.integers(-100, 100, n)).astype(dtype)
+    mk, mv, nm = (None, b"", 0)
+    if op == "count":
+        mk, mv, nm = "valid_min", np.int32(0).tobytes(), 1
+    creq = _abi.CRequest(op, dtype, shape=shape, axis=axis, missing_kind=mk, missing_values=mv, n_missing=nm)
+    info = _abi.rdx_response_info()
+    assert lib.rdx_plan(creq.ref, vals.nbytes, C.byref(info)) == 0
+    reps = max(2, (320 << 20) // vals.nbytes + 1)
+    bufs = [torch.from_numpy(vals.view(np.uint8)).cuda() for _ in range(reps)]
+    t = dev_time(creq, bufs, vals.nbytes, info.body_bytes, k=30)
+    tc = cpu_time(creq, vals.tobytes(), seconds=2.0)
+    alg = vals.nbytes + info.body_bytes + 8 * info.n_counts
+    report(name, t, alg, vals.nbytes, outputs=int(info.n_counts), cpu_oracle_us=round(tc * 1e6, 1),
+           gpu_over_cpu=round(tc / t, 1))
+    del bufs
 
 # ---- C5: i64 [512,256,256] select [[0,512,1],[64,192,1],[0,256,1]] -> 128 MiB out ----------------------
 g = torch.Generator(device="cuda")
@@ -75,10 +136,12 @@ c5 = [torch.randint(-2 ** 62, 2 ** 62, (512 * 256 * 256,), dtype=torch.int64, de
       for _ in range(2)]
 creq5 = _abi.CRequest("select", "int64", shape=[512, 256, 256], selection=[[0, 512, 1], [64, 192, 1], [0, 256, 1]])
 t = dev_time(creq5, c5, 256 << 20, 128 << 20, k=20)
-report("c5_select_device", t, (128 << 20) * 2, 256 << 20, note="128 MiB read + 128 MiB written")
+host5 = c5[0].cpu().numpy().tobytes()
+tc = cpu_time(creq5, host5, seconds=3.0)
+report("c5_select_device", t, (128 << 20) * 2, 256 << 20, note="128 MiB read + 128 MiB written",
+       cpu_oracle_us=round(tc * 1e6, 1), gpu_over_cpu=round(tc / t, 1))
 
 # host-inclusive C5: host chunk in (pageable), 128 MiB body out (pageable) through rdx_execute
-host5 = c5[0].cpu().numpy().tobytes()
 del c5
 t0 = time.perf_counter()
 reps = 3
