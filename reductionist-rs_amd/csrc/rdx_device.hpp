@@ -269,6 +269,18 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+// Which of the kPartialWords a reduction state actually carries (the rest stay at their identity).
+template <typename T, int OP>
+__device__ __forceinline__ constexpr bool word_used(int i) {
+    constexpr bool kRank = Red<T, OP>::kRank;
+    switch (i) {
+        case 0: return OP != OP_COUNT;                                              // value / sum
+        case 1: return OP == OP_SUM && std::is_same_v<T, double>;                   // compensation
+        case 2: return true;                                                        // count
+        default: return kRank;                                                      // zero ranks, NaN flag
+    }
+}
+
 // Deterministic butterfly over the 64 lanes; every lane ends with the wave total.
 template <typename T, int OP>
 __device__ __forceinline__ void wave_reduce(Red<T, OP> &r) {
@@ -277,7 +289,7 @@ __device__ __forceinline__ void wave_reduce(Red<T, OP> &r) {
         uint64_t w[kPartialWords], o[kPartialWords];
         r.to_words(w);
 #pragma unroll
-        for (int i = 0; i < kPartialWords; ++i) o[i] = shfl_xor_u64(w[i], m);
+        for (int i = 0; i < kPartialWords; ++i) o[i] = word_used<T, OP>(i) ? shfl_xor_u64(w[i], m) : w[i];
         Red<T, OP> other;
         other.from_words(o);
         r.merge(other);

@@ -66,8 +66,6 @@ struct KAllContig {
     int64_t r0, rs;
     uint32_t filter_semantics;  // Count(All) uses missing_filter (operations.rs:25-33)
     uint32_t blocks_per_chunk;
-    uint32_t unroll;            // tiles in flight per lane (2 or 4)
-    uint32_t pad;
 };
 
 // A strided view: dims innermost-first.  offset(e) = base_off + sum idx_k * vstride_k,

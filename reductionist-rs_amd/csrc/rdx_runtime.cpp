@@ -67,12 +67,10 @@ struct rdx_workspace {
     DevBuf<uint8_t> body;
     DevBuf<int64_t> counts;
     DevBuf<uint32_t> status;
-    hipStream_t bound_stream = nullptr;
 };
 
 struct rdx_context {
     std::vector<int> devices;
-    std::vector<int> cus;
     std::mutex mu;
     std::vector<std::vector<rdx_workspace *>> free_ws;  // per device index
     std::vector<rdx_workspace *> all_ws;
@@ -212,7 +210,6 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             KAllContig a = p.all_contig;
             const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus);
-            a.unroll = (uint32_t)env_int("RDX_UNROLL", 2) >= 4 ? 4u : 2u;
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;

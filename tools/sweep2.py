@@ -50,13 +50,11 @@ def run(req, nbytes):
     return f
 
 
-os.environ["RDX_UNROLL"] = "2"
 for bpc in (1, 8, 64, 256, 512, 1024, 2048):
     os.environ["RDX_FORCE_BPC"] = str(bpc)
     print(f"fixed overhead, 16 KiB plain sum, bpc={bpc:5d}: {timeit(run(plain, 16384)):7.2f} us")
 for bpc in (128, 256, 384, 512, 768, 1024):
-    for u in (2, 4):
-        os.environ["RDX_FORCE_BPC"] = str(bpc); os.environ["RDX_UNROLL"] = str(u)
-        t = timeit(run(creq, C2_BYTES))
-        t2 = timeit(run(plain, C2_BYTES))
-        print(f"C2 fused bpc={bpc:5d} unroll={u}: {t:7.2f} us ({C2_BYTES/t/1e3:6.0f} GB/s)   plain: {t2:7.2f} us ({C2_BYTES/t2/1e3:6.0f} GB/s)")
+    os.environ["RDX_FORCE_BPC"] = str(bpc)
+    t = timeit(run(creq, C2_BYTES))
+    t2 = timeit(run(plain, C2_BYTES))
+    print(f"C2 fused bpc={bpc:5d}: {t:7.2f} us ({C2_BYTES/t/1e3:6.0f} GB/s)   plain: {t2:7.2f} us ({C2_BYTES/t2/1e3:6.0f} GB/s)")
