@@ -90,6 +90,26 @@ for op, miss in (("min", ("missing_value", -9999.0)), ("max", ("missing_value", 
     tc = cpu_time(creq, v.tobytes())
     report(f"c3_{op}_{miss[0]}", t, n_sel * 8 + 16, 128 ** 3 * 8, n_selected=n_sel,
            cpu_oracle_us=round(tc * 1e6, 1), gpu_over_cpu=round(tc / t, 1))
+# C3 as a batch: 20 independent 16 MiB chunks per launch (rdx_execute_batch_device), min
+creqb = _abi.CRequest("min", "float64", shape=[128, 128, 128], selection=sel, missing_kind="missing_value",
+                      missing_values=np.float64(-9999.0).tobytes(), n_missing=1)
+bb = torch.zeros(len(c3), dtype=torch.float64, device="cuda")
+bc = torch.zeros(len(c3), dtype=torch.int64, device="cuda")
+bs = torch.zeros(len(c3), dtype=torch.int32, device="cuda")
+for _ in range(3):
+    ws.execute_batch_device(creqb, [b.data_ptr() for b in c3], 128 ** 3 * 8, bb.data_ptr(), bc.data_ptr(),
+                            bs.data_ptr(), stream.cuda_stream)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(stream)
+for _ in range(20):
+    ws.execute_batch_device(creqb, [b.data_ptr() for b in c3], 128 ** 3 * 8, bb.data_ptr(), bc.data_ptr(),
+                            bs.data_ptr(), stream.cuda_stream)
+e1.record(stream)
+torch.cuda.synchronize()
+tb = e0.elapsed_time(e1) / 1e3 / 20
+report("c3_min_missing_value_batch20", tb, len(c3) * (n_sel * 8 + 16), len(c3) * 128 ** 3 * 8,
+       chunks_per_launch=len(c3), us_per_chunk=round(tb / len(c3) * 1e6, 2))
 del c3
 
 # ---- C1 (CPU-only config in BASELINE): f32 4 MiB contiguous sum; D-int and D-real ------------------------
