@@ -39,6 +39,20 @@ int env_int(const char *name, int dflt) {
     return v ? std::atoi(v) : dflt;
 }
 
+// Tuning knobs, read from the environment once (getenv scans the whole environment: microseconds per
+// request if done per launch).
+struct Tuning {
+    int blocks_per_cu = env_int("RDX_BLOCKS_PER_CU", 2);
+    int min_tiles = env_int("RDX_MIN_TILES_PER_BLOCK", 2);
+    int force_bpc = env_int("RDX_FORCE_BPC", 0);   // tuning only
+    int no_vec = env_int("RDX_NO_VEC", 0);
+};
+
+const Tuning &tuning() {
+    static const Tuning t;
+    return t;
+}
+
 template <class T>
 struct DevBuf {
     T *p = nullptr;
@@ -124,14 +138,14 @@ rdx_status upload(rdx_workspace *ws, void *dst, const void *src, size_t bytes, s
 }
 
 uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
-    const uint64_t target = (uint64_t)cus * (uint64_t)env_int("RDX_BLOCKS_PER_CU", 2);
+    const uint64_t target = (uint64_t)cus * (uint64_t)tuning().blocks_per_cu;
     uint64_t bpc = (target + n_chunks - 1) / n_chunks;
-    const uint64_t min_tiles = (uint64_t)env_int("RDX_MIN_TILES_PER_BLOCK", 2);
+    const uint64_t min_tiles = (uint64_t)tuning().min_tiles;
     uint64_t cap = (tiles + min_tiles - 1) / min_tiles;
     if (bpc > cap) bpc = cap;
     if (bpc < 1) bpc = 1;
     if (bpc > 65536) bpc = 65536;
-    const int force = env_int("RDX_FORCE_BPC", 0);  // tuning only
+    const int force = tuning().force_bpc;
     if (force > 0) bpc = (uint64_t)force;
     return (uint32_t)bpc;
 }
@@ -140,7 +154,7 @@ uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
 uint32_t vec_width(const KView &v, uint32_t esz, const uint8_t *base, const uint8_t *const *ptrs, uint64_t n_chunks,
                    bool fused) {
     const uint32_t vw = 16 / esz;
-    if (fused || env_int("RDX_NO_VEC", 0)) return 1;
+    if (fused || tuning().no_vec) return 1;
     if (v.ndim < 1 || v.vstride[0] != 1 || v.count[0] % vw != 0 || v.base_off % (int64_t)vw != 0) return 1;
     for (int k = 1; k < v.ndim; ++k)
         if (v.vstride[k] % (int64_t)vw != 0) return 1;
@@ -228,7 +242,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 const uint64_t want = (a.view.n / a.vec + per_block - 1) / per_block;
                 uint64_t cap = ((uint64_t)ws->cus * 8 + n_chunks - 1) / n_chunks;
                 a.blocks_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min(want, std::max<uint64_t>(cap, 1)));
-                const int force = env_int("RDX_FORCE_BPC", 0);
+                const int force = tuning().force_bpc;
                 if (force > 0) a.blocks_per_chunk = (uint32_t)force;
             }
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
@@ -249,7 +263,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             {   // 16-byte lanes when every stride keeps vectors aligned and inside one dim
                 const uint32_t vw = 16 / p.esz;
                 const KView &inner = a.mode == 0 ? a.red : a.kept;
-                bool ok = !p.fused && !env_int("RDX_NO_VEC", 0) && inner.ndim >= 1 && inner.vstride[0] == 1 &&
+                bool ok = !p.fused && !tuning().no_vec && inner.ndim >= 1 && inner.vstride[0] == 1 &&
                           inner.count[0] % vw == 0 && a.kept.base_off % (int64_t)vw == 0 && (uintptr_t)src % 16 == 0;
                 for (int k = 0; k < a.kept.ndim; ++k) ok = ok && (a.mode == 1 && k == 0 ? true : a.kept.vstride[k] % (int64_t)vw == 0);
                 for (int k = 0; k < a.red.ndim; ++k) ok = ok && (a.mode == 0 && k == 0 ? true : a.red.vstride[k] % (int64_t)vw == 0);

@@ -38,16 +38,24 @@ def dev_time(creq, bufs, nbytes, out_bytes, k=50):
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
+    h0 = time.perf_counter()
     for i in range(k):
         lib.rdx_execute_device(*args[i % len(args)])
+    HOST["us"] = round((time.perf_counter() - h0) / k * 1e6, 2)   # host cost per call (plan + launch + ctypes)
     e1.record(stream)
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
     return e0.elapsed_time(e1) / 1e3 / k
 
 
+HOST = {}
+NO_CPU = "--no-cpu" in sys.argv   # profiling runs: skip the oracle timings
+
+
 def cpu_time(creq, data, seconds=3.0):
     """Oracle (sequential restatement of the reference path) on one host core."""
+    if NO_CPU:
+        return float("nan")
     from oracle import py_oracle as oracle
     L = oracle.lib()
     src = C.create_string_buffer(data, len(data))
@@ -69,6 +77,8 @@ def report(name, t, alg_bytes, chunk_bytes, **kw):
     d = {"config": name, "us_per_launch": round(t * 1e6, 2), "bytes_alg": alg_bytes,
          "GBs_alg": round(alg_bytes / t / 1e9, 1), "roofline_frac": round(alg_bytes / t / 1e9 / PEAK, 4),
          "GiBs_chunk": round(chunk_bytes / t / 2 ** 30, 1)}
+    if HOST:
+        d["host_us_per_call"] = HOST.pop("us")
     d.update(kw)
     print(json.dumps(d), flush=True)
 
