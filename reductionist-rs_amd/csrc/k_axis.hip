@@ -31,10 +31,7 @@ __device__ __forceinline__ void write_result(const KOut &out, uint64_t o, const 
 
 template <typename T, int OP>
 __device__ __forceinline__ void write_partial(const KOut &out, uint64_t idx, const Red<T, OP> &r) {
-    uint64_t w[kPartialWords];
-    r.to_words(w);
-#pragma unroll
-    for (int i = 0; i < kPartialWords; ++i) out.partials[idx * kPartialWords + i] = w[i];
+    store_packed<T, OP, false>(out.partials + idx * packed_words<T, OP>(), r);
 }
 
 template <typename T, int OP>
@@ -198,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_combine(const KAxis a) {
     acc.init();
     for (uint32_t s = 0; s < a.slices; ++s) {
         Red<T, OP> p;
-        p.from_words(a.out.partials + (o * a.slices + s) * kPartialWords);
+        load_packed<T, OP, false>(a.out.partials + (o * a.slices + s) * packed_words<T, OP>(), p);
         acc.merge(p);
     }
     write_result(a.out, o, acc);

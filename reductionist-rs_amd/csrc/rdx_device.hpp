@@ -281,6 +281,46 @@ __device__ __forceinline__ constexpr bool word_used(int i) {
     }
 }
 
+// Partial records in memory carry only the used words, packed (f32 sum: 2 words, float min/max: 5).
+template <typename T, int OP>
+__device__ __forceinline__ constexpr int packed_words() {
+    int n = 0;
+    for (int i = 0; i < kPartialWords; ++i) n += word_used<T, OP>(i) ? 1 : 0;
+    return n;
+}
+
+// AGENT = agent-scope (sc1) accesses for the cross-workgroup hand-off.
+template <typename T, int OP, bool AGENT>
+__device__ __forceinline__ void store_packed(uint64_t *P, const Red<T, OP> &r) {
+    uint64_t w[kPartialWords];
+    r.to_words(w);
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < kPartialWords; ++i) {
+        if (!word_used<T, OP>(i)) continue;
+        if constexpr (AGENT) __hip_atomic_store(P + k, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else P[k] = w[i];
+        ++k;
+    }
+}
+
+template <typename T, int OP, bool AGENT>
+__device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r) {
+    Red<T, OP> id;
+    id.init();
+    uint64_t w[kPartialWords];
+    id.to_words(w);
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < kPartialWords; ++i) {
+        if (!word_used<T, OP>(i)) continue;
+        if constexpr (AGENT) w[i] = __hip_atomic_load(P + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else w[i] = P[k];
+        ++k;
+    }
+    r.from_words(w);
+}
+
 // Deterministic butterfly over the 64 lanes; every lane ends with the wave total.
 template <typename T, int OP>
 __device__ __forceinline__ void wave_reduce(Red<T, OP> &r) {
@@ -332,11 +372,8 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
     __shared__ uint32_t s_last;
     block_reduce(r);
     if (threadIdx.x == 0) {
-        uint64_t w[kPartialWords];
-        r.to_words(w);
-        uint64_t *P = out.partials + ((uint64_t)chunk * bpc + b) * kPartialWords;
-#pragma unroll
-        for (int i = 0; i < kPartialWords; ++i) __hip_atomic_store(P + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        constexpr int kW = packed_words<T, OP>();
+        store_packed<T, OP, true>(out.partials + ((uint64_t)chunk * bpc + b) * kW, r);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t *tk = out.tickets + (uint64_t)chunk * kTicketWords;
         const uint32_t nsh = bpc < kTicketShards ? bpc : kTicketShards;
@@ -355,14 +392,11 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
     if (!s_last) return;
     Red<T, OP> acc;
     acc.init();
-    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kPartialWords;
+    constexpr int kW = packed_words<T, OP>();
+    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kW;
     for (uint32_t j = threadIdx.x; j < bpc; j += kBlock) {
-        uint64_t w[kPartialWords];
-#pragma unroll
-        for (int i = 0; i < kPartialWords; ++i)
-            w[i] = __hip_atomic_load(P + (uint64_t)j * kPartialWords + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         Red<T, OP> o;
-        o.from_words(w);
+        load_packed<T, OP, true>(P + (uint64_t)j * kW, o);
         acc.merge(o);
     }
     block_reduce(acc);
