@@ -78,6 +78,44 @@ static void cpu_tests() {
     r.missing = Missing{Missing::Kind::MissingValue, {DValue(int64_t(-1))}};
     EXPECT(error_kind([&] { r.validate(); }) == K::RequestDataValidation);  // missing.rs:144-149
 
+    // models.rs:741-911 request-level validation (test_utils.rs:7-29 defaults: int32, nothing else)
+    auto invalid = [](RequestData q) { return error_kind([&] { q.validate(); }) == K::RequestDataValidation; };
+    RequestData d;
+    d.validate();
+    r = d;
+    r.size = 1;
+    EXPECT(invalid(r));                                                    // test_invalid_size_for_dtype
+    r = d;
+    r.size = 4;
+    r.shape = std::vector<uint64_t>{1, 2};
+    EXPECT(invalid(r));                                                    // test_invalid_size_for_shape
+    r = d;
+    r.shape = std::vector<uint64_t>{1, 2};
+    r.selection = std::vector<Slice>{{1, 2, 1}};
+    EXPECT(invalid(r));                                                    // test_shape_selection_mismatch
+    r = d;
+    r.selection = std::vector<Slice>{{1, 2, 1}};
+    EXPECT(invalid(r));                                                    // test_selection_without_shape
+    r = d;
+    r.axis = ReductionAxes::one(1);
+    EXPECT(invalid(r));                                                    // test_axis_without_shape
+    r = d;
+    r.shape = std::vector<uint64_t>{1, 2};
+    r.axis = ReductionAxes::multi({1, 1});
+    EXPECT(invalid(r));                                                    // test_axis_duplicates
+    r = d;
+    r.missing = Missing{Missing::Kind::MissingValue, {DValue(std::numeric_limits<int64_t>::max())}};
+    EXPECT(invalid(r));                                                    // test_missing_invalid_value_for_dtype
+    r = d;
+    r.interface_type.clear();
+    EXPECT(invalid(r));                                                    // test_invalid_interface_type
+    for (Slice sl : {Slice{1, 0, 1}, Slice{1, 0, -1}, Slice{5, 5, 1}, Slice{-5, 5, 1}, Slice{1, -5, 1}}) {
+        r = d;                                                             // models.rs:724-803: valid numpy slices
+        r.shape = std::vector<uint64_t>{4};
+        r.selection = std::vector<Slice>{sl};
+        r.validate();
+    }
+
     // dvalue.rs conversions
     EXPECT(dvalue_bytes(DValue(int64_t(42)), DType::Int32) == bytes_of<int32_t>({42}));
     EXPECT(error_kind([&] { dvalue_bytes(DValue(int64_t(1) << 31), DType::Int32); }) == K::IncompatibleMissing);
