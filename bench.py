@@ -99,6 +99,40 @@ def cpu_baseline(seconds):
                       f"oracle/rdx_oracle.cpp g++ -O2 on 1 host core, {el:.1f} s"}
 
 
+def cpu_baseline_c4(threads, distinct=64):
+    """C4 on the host the way the reference serves it: independent requests on a worker pool
+    (thread_limit = num_cpus - 1, src/app_state.rs:22; capped at the box's CPU share).  1024 chunks of
+    4 MiB (64 distinct, cycled), unshuffle + f32 sum each, by the oracle; ctypes releases the GIL."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import py_oracle as oracle
+    from reductionist_amd import _abi
+    lib = oracle.lib()
+    creq = _abi.CRequest("sum", "float32", filters=[{"id": "shuffle", "element_size": 4}])
+    rng = np.random.default_rng(0x5EED1000)
+    srcs = []
+    for _ in range(distinct):
+        v = rng.random(C4_ELEMS, dtype=np.float32)
+        b = v.view(np.uint8).reshape(C4_ELEMS, 4).T.copy().tobytes()
+        srcs.append(C.create_string_buffer(b, len(b)))
+
+    def one(i):
+        body = (C.c_uint8 * 64)()
+        counts = (C.c_int64 * 8)()
+        info = _abi.rdx_response_info()
+        assert lib.oracle_execute(C.addressof(creq.c), srcs[i % distinct], 4 * C4_ELEMS, body, 64, counts, 8,
+                                  C.byref(info)) == 0
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, range(threads)))                      # warm the pool
+        t0 = time.perf_counter()
+        list(ex.map(one, range(C4_CHUNKS)))
+        el = time.perf_counter() - t0
+    return {"value": round(C4_CHUNKS * 4 * C4_ELEMS / el / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "sample": f"all {C4_CHUNKS} chunks ({distinct} distinct, cycled), {threads} worker "
+                                      f"threads, oracle g++ -O2, {el:.2f} s"}
+
+
 def main():
     args = parse()
     import torch
@@ -251,6 +285,8 @@ def main():
             "chunks_per_rank": n_local,
             "roofline_frac": round(n_local * 4 * C4_ELEMS / k4 / 1e9 / PEAK_GBS, 4)}
         del c4
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            extra["c4_batch"]["cpu_baseline"] = cpu_baseline_c4(max(1, min(15, (os.cpu_count() or 2) - 1)))
 
     line = {
         "metric": "GiB/s device-resident chunk unshuffle+reduce (f32 sum), 1/2/4/8 MI355X",
