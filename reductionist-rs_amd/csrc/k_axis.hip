@@ -5,8 +5,10 @@
 // zero in the reference's fold order: F order over the reduced axes in request order (fold_axis
 // over the first axis, then over the partials along the next, operations.rs:229-258).
 //
-//  k_axis_rows<VW> — the innermost memory dim is reduced: one wave per (output, slice); each lane
-//                    loads VW consecutive elements (16 B when VW > 1), 4 loads in flight, butterfly.
+//  k_axis_rows<VW> — the innermost memory dim is reduced: a group of `group` lanes per (output,
+//                    slice) (the whole wave for long rows, 64/group outputs per wave for short ones);
+//                    each lane loads VW consecutive elements (16 B when VW > 1), 4 loads in flight,
+//                    butterfly within the group.
 //  k_axis_cols<VW> — otherwise: a workgroup owns a tile of 64 lanes x VW consecutive outputs along
 //                    the innermost kept dim (16 B loads across lanes = coalesced rows); its 4 waves
 //                    split the slice's reduced elements (8 loads in flight per lane) and combine
@@ -96,23 +98,27 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
     constexpr int kU = 4;
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t L = a.group, G = 64 / L;        // lanes per item, items per wave pass
+    const uint32_t l = lane & (L - 1), g = lane / L;
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
     const uint64_t items = a.n_out * a.slices;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
     const uint64_t nrv = a.n_red / VW;  // reduced vectors per output
-    for (uint64_t it = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); it < items; it += nw) {
-        const uint64_t o = it / a.slices, s = it - o * a.slices;
-        int64_t oi;
-        const int64_t koff = kept_offset(a.kept, (uint32_t)o, oi);
-        const uint64_t r_lo = s * nrv / a.slices, r_hi = (s + 1) * nrv / a.slices;
+    for (uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w0 * G < items; w0 += nw) {
+        const uint64_t it = w0 * G + g;
+        const bool valid = it < items;
+        const uint64_t o = valid ? it / a.slices : 0, s = valid ? it - o * a.slices : 0;
+        int64_t oi = 0, koff = 0;
+        if (valid) koff = kept_offset(a.kept, (uint32_t)o, oi);
+        const uint64_t r_lo = s * nrv / a.slices, r_hi = valid ? (s + 1) * nrv / a.slices : 0;
         Red<T, OP> r;
         r.init();
-        for (uint64_t r0 = r_lo + lane; r0 < r_hi; r0 += 64 * kU) {
+        for (uint64_t r0 = r_lo + l; r0 < r_hi; r0 += (uint64_t)L * kU) {
             T x[kU][VW];
             int64_t rk[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const uint64_t rv = r0 + (uint64_t)u * 64;
+                const uint64_t rv = r0 + (uint64_t)u * L;
                 if (rv < r_hi) {
                     const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)(rv * VW), rk[u]);
                     load_vec<T, FUSED, VW>(a.src, off, x[u]);
@@ -120,13 +126,13 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                if (r0 + (uint64_t)u * 64 >= r_hi) continue;
+                if (r0 + (uint64_t)u * L >= r_hi) continue;
 #pragma unroll
                 for (int j = 0; j < VW; ++j) fold_in(r, a.miss, miss, x[u][j], rk[u] + (int64_t)j * a.red.rstride[0]);
             }
         }
-        wave_reduce(r);
-        if (lane == 0) emit(a, (uint64_t)oi, s, r);
+        group_reduce(r, L);
+        if (valid && l == 0) emit(a, (uint64_t)oi, s, r);
     }
 }
 
@@ -205,8 +211,8 @@ template <typename T, int OP, int VW>
 void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
     const dim3 block(kBlock);
     if (a.mode == 0) {
-        const uint64_t items = a.n_out * a.slices;
-        uint64_t blocks = (items + kBlock / 64 - 1) / (kBlock / 64);
+        const uint64_t waves = (a.n_out * a.slices + 64 / a.group - 1) / (64 / a.group);
+        uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
         const uint64_t cap = (uint64_t)cus * 16;
         if (blocks > cap) blocks = cap;
         if (blocks == 0) blocks = 1;

@@ -321,19 +321,28 @@ __device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r) {
     r.from_words(w);
 }
 
+template <typename T, int OP>
+__device__ __forceinline__ void xor_merge(Red<T, OP> &r, int m) {
+    uint64_t w[kPartialWords], o[kPartialWords];
+    r.to_words(w);
+#pragma unroll
+    for (int i = 0; i < kPartialWords; ++i) o[i] = word_used<T, OP>(i) ? shfl_xor_u64(w[i], m) : w[i];
+    Red<T, OP> other;
+    other.from_words(o);
+    r.merge(other);
+}
+
 // Deterministic butterfly over the 64 lanes; every lane ends with the wave total.
 template <typename T, int OP>
 __device__ __forceinline__ void wave_reduce(Red<T, OP> &r) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t w[kPartialWords], o[kPartialWords];
-        r.to_words(w);
-#pragma unroll
-        for (int i = 0; i < kPartialWords; ++i) o[i] = word_used<T, OP>(i) ? shfl_xor_u64(w[i], m) : w[i];
-        Red<T, OP> other;
-        other.from_words(o);
-        r.merge(other);
-    }
+    for (int m = 32; m >= 1; m >>= 1) xor_merge(r, m);
+}
+
+// The same within aligned groups of `width` lanes (a power of two <= 64).
+template <typename T, int OP>
+__device__ __forceinline__ void group_reduce(Red<T, OP> &r, uint32_t width) {
+    for (int m = (int)width >> 1; m >= 1; m >>= 1) xor_merge(r, m);
 }
 
 // Workgroup total in thread 0 (waves merged in wave order).

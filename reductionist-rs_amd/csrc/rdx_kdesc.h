@@ -108,7 +108,7 @@ struct KAxis {
     uint32_t slices;
     uint32_t mode;   // 0 = rows (a wave per output), 1 = cols (a lane per output)
     uint32_t vec;    // elements per 16-byte lane load (1 = scalar)
-    uint32_t pad;
+    uint32_t group;  // rows mode: lanes per output (power of two <= 64); 64/group outputs per wave
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

@@ -269,10 +269,15 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 for (int k = 0; k < a.red.ndim; ++k) ok = ok && (a.mode == 0 && k == 0 ? true : a.red.vstride[k] % (int64_t)vw == 0);
                 a.vec = ok ? vw : 1;
             }
+            a.group = 64;
             if (a.mode == 0) {
                 const uint64_t target = (uint64_t)ws->cus * 16;                      // waves
                 const uint64_t nrv = a.n_red / a.vec;
-                if (a.n_out < target) slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (nrv + 255) / 256);
+                // short rows: just enough lanes per output for 4 loads in flight per lane
+                const uint64_t want = (nrv + 3) / 4;
+                while (a.group > 1 && a.group / 2 >= want) a.group /= 2;
+                if (a.group == 64 && a.n_out < target)
+                    slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (nrv + 255) / 256);
             } else {
                 const uint64_t tiles = (a.n_out / a.vec + 63) / 64;
                 const uint64_t target = (uint64_t)ws->cus * 4;                       // workgroups
