@@ -13,7 +13,9 @@
 //                    the innermost kept dim (16 B loads across lanes = coalesced rows); its 4 waves
 //                    split the slice's reduced elements (8 loads in flight per lane) and combine
 //                    through LDS.
-//  k_axis_combine  — when the reduced range is split into slices, fold the slices in order.
+//  When the reduced range is split into slices (few outputs), every slice publishes a partial and
+//  the last slice to arrive for an output (rows) or tile (cols) folds them: one launch, no
+//  second kernel.
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
 
@@ -29,17 +31,6 @@ __device__ __forceinline__ void write_result(const KOut &out, uint64_t o, const 
         if (r.nan && out.status)
             __hip_atomic_fetch_or(out.status, (uint32_t)RDX_E_NAN_UNORDERED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-template <typename T, int OP>
-__device__ __forceinline__ void write_partial(const KOut &out, uint64_t idx, const Red<T, OP> &r) {
-    store_packed<T, OP, false>(out.partials + idx * packed_words<T, OP>(), r);
-}
-
-template <typename T, int OP>
-__device__ __forceinline__ void emit(const KAxis &a, uint64_t oi, uint64_t s, const Red<T, OP> &r) {
-    if (a.slices == 1) write_result(a.out, oi, r);
-    else write_partial(a.out, oi * a.slices + s, r);
 }
 
 __device__ __forceinline__ int64_t kept_offset(const KView &kv, uint32_t t, int64_t &out_index) {
@@ -132,7 +123,30 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
             }
         }
         group_reduce(r, L);
-        if (valid && l == 0) emit(a, (uint64_t)oi, s, r);
+        if (a.slices == 1) {
+            if (valid && l == 0) write_result(a.out, (uint64_t)oi, r);
+            continue;
+        }
+        // sliced (group == 64, one item per wave): publish, and the last slice to arrive folds them
+        constexpr int kW = packed_words<T, OP>();
+        uint32_t last = 0;
+        if (lane == 0) {
+            store_packed<T, OP, true>(a.out.partials + it * kW, r);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t *tk = a.out.tickets + o;
+            last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
+            if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!__shfl(last, 0, 64)) continue;
+        Red<T, OP> acc;
+        acc.init();
+        for (uint32_t q = lane; q < a.slices; q += 64) {
+            Red<T, OP> p;
+            load_packed<T, OP, true>(a.out.partials + (o * a.slices + q) * kW, p);
+            acc.merge(p);
+        }
+        wave_reduce(acc);
+        if (lane == 0) write_result(a.out, (uint64_t)oi, acc);
     }
 }
 
@@ -175,6 +189,69 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
         }
     }
     // combine the 4 waves' partial states of each output in wave order
+    __shared__ uint32_t s_last;
+    if (wave > 0) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) r[j].to_words(lds[wave - 1][lane][j]);
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            for (int w = 0; w < kWaves - 1; ++w) {
+                Red<T, OP> o;
+                o.from_words(lds[w][lane][j]);
+                r[j].merge(o);
+            }
+        }
+    }
+    if (a.slices == 1) {
+        if (wave == 0 && active) {
+#pragma unroll
+            for (int j = 0; j < VW; ++j) write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r[j]);
+        }
+        return;
+    }
+    // Sliced: publish this slice's tile partials ([tile][slice][lane][j], coalesced), count arrivals
+    // per tile; the last slice's workgroup folds all slices (its 4 waves split them, LDS combine).
+    constexpr int kW = packed_words<T, OP>();
+    const uint64_t tile_rec = (uint64_t)64 * VW;
+    uint64_t *P = a.out.partials + (uint64_t)blockIdx.x * a.slices * tile_rec * kW;
+    if (wave == 0) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) store_packed<T, OP, true>(P + ((uint64_t)s * tile_rec + lane * VW + j) * kW, r[j]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            uint32_t *tk = a.out.tickets + blockIdx.x;
+            const bool last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
+            if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = last;
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const uint32_t q_lo = wave * a.slices / kWaves, q_hi = (wave + 1) * a.slices / kWaves;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) r[j].init();
+    if (active) {
+        constexpr int kQ = 4;  // slices' records in flight per lane
+        for (uint32_t q0 = q_lo; q0 < q_hi; q0 += kQ) {
+            Red<T, OP> p[kQ][VW];
+#pragma unroll
+            for (int u = 0; u < kQ; ++u) {
+#pragma unroll
+                for (int j = 0; j < VW; ++j) {
+                    if (q0 + u < q_hi) load_packed<T, OP, true>(P + ((uint64_t)(q0 + u) * tile_rec + lane * VW + j) * kW, p[u][j]);
+                    else p[u][j].init();
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kQ; ++u) {
+#pragma unroll
+                for (int j = 0; j < VW; ++j) r[j].merge(p[u][j]);
+            }
+        }
+    }
     if (wave > 0) {
 #pragma unroll
         for (int j = 0; j < VW; ++j) r[j].to_words(lds[wave - 1][lane][j]);
@@ -188,23 +265,9 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
                 o.from_words(lds[w][lane][j]);
                 r[j].merge(o);
             }
-            emit(a, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), s, r[j]);
+            write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r[j]);
         }
     }
-}
-
-template <typename T, int OP>
-__global__ __launch_bounds__(kBlock) void k_axis_combine(const KAxis a) {
-    const uint64_t o = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (o >= a.n_out) return;
-    Red<T, OP> acc;
-    acc.init();
-    for (uint32_t s = 0; s < a.slices; ++s) {
-        Red<T, OP> p;
-        load_packed<T, OP, false>(a.out.partials + (o * a.slices + s) * packed_words<T, OP>(), p);
-        acc.merge(p);
-    }
-    write_result(a.out, o, acc);
 }
 
 template <typename T, int OP, int VW>
@@ -229,9 +292,6 @@ template <typename T, int OP>
 hipError_t launch_axis_t(const KAxis &a, int cus, hipStream_t st) {
     if (a.vec > 1 && !a.src.fused) launch_axis_vw<T, OP, 16 / sizeof(T)>(a, cus, st);
     else launch_axis_vw<T, OP, 1>(a, cus, st);
-    if (a.slices > 1)
-        hipLaunchKernelGGL((k_axis_combine<T, OP>), dim3((uint32_t)((a.n_out + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           st, a);
     return hipGetLastError();
 }
 

@@ -285,9 +285,15 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             }
             slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, 65535));
             a.slices = (uint32_t)slices;
-            if (slices > 1) {
-                if ((st = ensure(ws, ws->partials, a.n_out * slices * kPartialWords, s))) return st;
+            if (slices > 1) {   // partial records + one self-resetting arrival counter per output / tile
+                const uint64_t tiles = (a.n_out / a.vec + 63) / 64;
+                const uint64_t recs = a.mode == 0 ? a.n_out : tiles * 64 * a.vec;
+                if ((st = ensure(ws, ws->partials, recs * slices * kPartialWords, s))) return st;
+                if ((st = ensure(ws, ws->tickets, std::max<uint64_t>(a.mode == 0 ? a.n_out : tiles, kTicketWords), s,
+                                 true)))
+                    return st;
                 out.partials = ws->partials.p;
+                out.tickets = ws->tickets.p;
             }
             a.src = ksrc;
             a.miss = miss;
