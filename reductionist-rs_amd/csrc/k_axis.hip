@@ -95,6 +95,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     const uint64_t items = a.n_out * a.slices;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
     const uint64_t nrv = a.n_red / VW;  // reduced vectors per output
+    // only float min/max can report an error (NaN); the host clears the status word for those
+    if (!RANK && blockIdx.x == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;
     for (uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w0 * G < items; w0 += nw) {
         const uint64_t it = w0 * G + g;
         const bool valid = it < items;
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     const uint64_t nkv = a.n_out / VW;             // kept vectors
     const uint64_t kv = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t s = blockIdx.y;
+    if (!RANK && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;
     const bool active = kv < nkv;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
     int64_t oi = 0, koff = 0;

@@ -257,7 +257,10 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
         }
         case Mode::Axis: {
             KAxis a = p.axis;
-            if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
+            // the kernels clear the status word themselves unless a NaN can set it (float min/max)
+            const bool can_fail = (p.dtype == RDX_DTYPE_FLOAT32 || p.dtype == RDX_DTYPE_FLOAT64) &&
+                                  (p.op == RDX_OP_MIN || p.op == RDX_OP_MAX);
+            if (d_status && (can_fail || a.n_out == 0)) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
             if (a.n_out == 0) return RDX_OK;
             uint64_t slices = 1;
             {   // 16-byte lanes when every stride keeps vectors aligned and inside one dim
@@ -305,8 +308,8 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             KMap a = p.map;
             a.vec = vec_width(a.view, p.esz, src, nullptr, 1, p.fused);
             if ((uintptr_t)d_body % 16 || (a.kind != 0 && (uintptr_t)d_counts % 16)) a.vec = 1;
-            if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
             if (a.view.n == 0) {
+                if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
                 if (a.kind == 0) RDX_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t), s));
                 return RDX_OK;
             }
