@@ -227,7 +227,6 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
 // lane normally needs a single round trip.
 template <typename T, int OP, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
-    using U = typename UIntOf<T>::type;
     constexpr int kU = VW > 1 ? 4 : 8;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
@@ -247,8 +246,9 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
         T x[kU][VW];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const uint64_t g = g0 + (uint64_t)u * kBlock;
+            uint64_t g = g0 + (uint64_t)u * kBlock;
             ok[u] = g < g_end;
+            if (!ok[u]) g = g0;  // clamped into the range: the load issues unconditionally
             uint32_t q = (uint32_t)(g * VW);
             int64_t o = v.base_off, rr = v.r0;
             for (int k = 0; k < v.ndim; ++k) {
@@ -261,19 +261,11 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
             off[u] = o;
             rk[u] = rr;
         }
+        Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (!ok[u]) continue;
-            if constexpr (VW == 1) {
-                x[u][0] = load_elem<T, FUSED>(base, a.src.plane, bswap, (uint64_t)off[u]);
-            } else {
-                const uint4 w = gld<uint4>(base + (uint64_t)off[u] * sizeof(T));
-                U e[VW];
-                __builtin_memcpy(e, &w, 16);
+        for (int u = 0; u < kU; ++u) raw_load(raw[u], base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) x[u][j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
-            }
-        }
+        for (int u = 0; u < kU; ++u) raw_cvt(raw[u], bswap, x[u]);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             if (!ok[u]) continue;

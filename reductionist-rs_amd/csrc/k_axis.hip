@@ -62,21 +62,6 @@ __device__ __forceinline__ int64_t red_offset(const KView &rv, uint32_t r, int64
     return off;
 }
 
-// VW consecutive elements at element offset `off` (16-byte aligned when VW > 1).
-template <typename T, bool FUSED, int VW>
-__device__ __forceinline__ void load_vec(const KSrc &src, int64_t off, T (&x)[VW]) {
-    using U = typename UIntOf<T>::type;
-    if constexpr (VW == 1) {
-        x[0] = load_elem<T, FUSED>(src.base, src.plane, src.bswap, (uint64_t)off);
-    } else {
-        const uint4 w = gld<uint4>(src.base + (uint64_t)off * sizeof(T));
-        U e[VW];
-        __builtin_memcpy(e, &w, 16);
-#pragma unroll
-        for (int j = 0; j < VW; ++j) x[j] = from_u<T>(src.bswap ? bswap_u(e[j]) : e[j]);
-    }
-}
-
 template <typename T, int OP>
 __device__ __forceinline__ void fold_in(Red<T, OP> &r, const KMissing &miss, bool has_miss, T x, int64_t rank) {
     if (has_miss && is_missing(miss, x)) return;
@@ -107,21 +92,23 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
         Red<T, OP> r;
         r.init();
         for (uint64_t r0 = r_lo + l; r0 < r_hi; r0 += (uint64_t)L * kU) {
-            T x[kU][VW];
-            int64_t rk[kU];
+            int64_t off[kU], rk[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const uint64_t rv = r0 + (uint64_t)u * L;
-                if (rv < r_hi) {
-                    const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)(rv * VW), rk[u]);
-                    load_vec<T, FUSED, VW>(a.src, off, x[u]);
-                }
+                uint64_t rv = r0 + (uint64_t)u * L;
+                if (rv >= r_hi) rv = r0;  // clamped: every load issues, the value is dropped below
+                off[u] = koff + red_offset<RANK>(a.red, (uint32_t)(rv * VW), rk[u]);
             }
+            Raw<T, FUSED, VW> raw[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 if (r0 + (uint64_t)u * L >= r_hi) continue;
+                T x[VW];
+                raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) fold_in(r, a.miss, miss, x[u][j], rk[u] + (int64_t)j * a.red.rstride[0]);
+                for (int j = 0; j < VW; ++j) fold_in(r, a.miss, miss, x[j], rk[u] + (int64_t)j * a.red.rstride[0]);
             }
         }
         group_reduce(r, L);
@@ -173,21 +160,23 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     for (int j = 0; j < VW; ++j) r[j].init();
     if (active) {
         for (uint64_t r0 = r_lo + wave; r0 < r_hi; r0 += (uint64_t)kWaves * kU) {
-            T x[kU][VW];
-            int64_t rk[kU];
+            int64_t off[kU], rk[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const uint64_t rr = r0 + (uint64_t)u * kWaves;
-                if (rr < r_hi) {
-                    const int64_t off = koff + red_offset<RANK>(a.red, (uint32_t)rr, rk[u]);
-                    load_vec<T, FUSED, VW>(a.src, off, x[u]);
-                }
+                uint64_t rr = r0 + (uint64_t)u * kWaves;
+                if (rr >= r_hi) rr = r0;  // clamped: every load issues, the value is dropped below
+                off[u] = koff + red_offset<RANK>(a.red, (uint32_t)rr, rk[u]);
             }
+            Raw<T, FUSED, VW> raw[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 if (r0 + (uint64_t)u * kWaves >= r_hi) continue;
+                T x[VW];
+                raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) fold_in(r[j], a.miss, miss, x[u][j], rk[u]);
+                for (int j = 0; j < VW; ++j) fold_in(r[j], a.miss, miss, x[j], rk[u]);
             }
         }
     }

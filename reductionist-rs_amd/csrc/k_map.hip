@@ -19,7 +19,6 @@ namespace {
 // the traversal order), so each lane moves VW elements with one 16-byte load and one 16-byte store.
 template <typename T, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
-    using U = typename UIntOf<T>::type;
     constexpr int kU = 4;
     const KView &v = a.view;
     const bool miss = a.miss.kind != RDX_MISSING_NONE;
@@ -38,8 +37,9 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
         T x[kU][VW];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const uint64_t g = g0 + (uint64_t)u * stride;
+            uint64_t g = g0 + (uint64_t)u * stride;
             ok[u] = g < g_end;
+            if (!ok[u]) g = g0;  // clamped into the range: the load issues unconditionally
             uint32_t q = (uint32_t)(g * VW);
             int64_t o = v.base_off;
             for (int k = 0; k < v.ndim; ++k) {
@@ -49,19 +49,11 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
             }
             off[u] = o;
         }
+        Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (!ok[u]) continue;
-            if constexpr (VW == 1) {
-                x[u][0] = load_elem<T, FUSED>(a.src.base, a.src.plane, bswap, (uint64_t)off[u]);
-            } else {
-                const uint4 w = gld<uint4>(a.src.base + (uint64_t)off[u] * sizeof(T));
-                U e[VW];
-                __builtin_memcpy(e, &w, 16);
+        for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) x[u][j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
-            }
-        }
+        for (int u = 0; u < kU; ++u) raw_cvt(raw[u], bswap, x[u]);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             if (!ok[u]) continue;

@@ -89,6 +89,49 @@ __device__ __forceinline__ T load_elem(const uint8_t *base, uint64_t plane, bool
     return from_u<T>(u);
 }
 
+// Two-phase loads for gathers: a lane first issues the raw loads of all its kU vectors (offsets
+// clamped into the view, so no load sits in a branch), then converts and consumes them.  A
+// conversion placed right after a conditional load makes the compiler wait for that load, which
+// serialises the lane's loads into kU round trips.
+template <typename T, bool FUSED, int VW>
+struct Raw {
+    using U = typename UIntOf<T>::type;
+    uint4 w;                               // VW > 1: 16 bytes
+    U e;                                   // VW == 1, plain: one element
+    uint32_t b[FUSED ? sizeof(T) : 1];     // VW == 1, fused: its bytes from the planes
+};
+
+template <typename T, bool FUSED, int VW>
+__device__ __forceinline__ void raw_load(Raw<T, FUSED, VW> &r, const uint8_t *base, uint64_t plane, uint64_t off) {
+    using U = typename UIntOf<T>::type;
+    if constexpr (VW > 1) {
+        r.w = gld<uint4>(base + off * sizeof(T));
+    } else if constexpr (FUSED) {
+#pragma unroll
+        for (int k = 0; k < (int)sizeof(T); ++k) r.b[k] = gld<uint8_t>(base + (uint64_t)k * plane + off);
+    } else {
+        r.e = gld<U>(reinterpret_cast<const U *>(base) + off);
+    }
+}
+
+template <typename T, bool FUSED, int VW>
+__device__ __forceinline__ void raw_cvt(const Raw<T, FUSED, VW> &r, bool bswap, T (&x)[VW]) {
+    using U = typename UIntOf<T>::type;
+    if constexpr (VW > 1) {
+        U e[VW];
+        __builtin_memcpy(e, &r.w, 16);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) x[j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
+    } else if constexpr (FUSED) {
+        U u = 0;
+#pragma unroll
+        for (int k = 0; k < (int)sizeof(T); ++k) u |= (U)(r.b[k] & 0xffu) << (8 * k);
+        x[0] = from_u<T>(bswap ? bswap_u(u) : u);
+    } else {
+        x[0] = from_u<T>(bswap ? bswap_u(r.e) : r.e);
+    }
+}
+
 // ---- missing-data predicate ---------------------------------------------------------------------
 // Missing::is_missing (src/types/missing.rs:114-122).
 template <typename T>

@@ -46,6 +46,8 @@ struct Tuning {
     int min_tiles = env_int("RDX_MIN_TILES_PER_BLOCK", 2);
     int force_bpc = env_int("RDX_FORCE_BPC", 0);   // tuning only
     int no_vec = env_int("RDX_NO_VEC", 0);
+    int axis_rows_waves = env_int("RDX_AXIS_ROWS_WAVES_PER_CU", 16);   // sliced-rows fill target
+    int axis_cols_wgs = env_int("RDX_AXIS_COLS_WGS_PER_CU", 4);        // sliced-cols fill target
 };
 
 const Tuning &tuning() {
@@ -274,7 +276,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             }
             a.group = 64;
             if (a.mode == 0) {
-                const uint64_t target = (uint64_t)ws->cus * 16;                      // waves
+                const uint64_t target = (uint64_t)ws->cus * tuning().axis_rows_waves;     // waves
                 const uint64_t nrv = a.n_red / a.vec;
                 // short rows: just enough lanes per output for 4 loads in flight per lane
                 const uint64_t want = (nrv + 3) / 4;
@@ -283,7 +285,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                     slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (nrv + 255) / 256);
             } else {
                 const uint64_t tiles = (a.n_out / a.vec + 63) / 64;
-                const uint64_t target = (uint64_t)ws->cus * 4;                       // workgroups
+                const uint64_t target = (uint64_t)ws->cus * tuning().axis_cols_wgs;      // workgroups
                 if (tiles < target) slices = std::min<uint64_t>((target + tiles - 1) / tiles, (a.n_red + 31) / 32);
             }
             slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, 65535));
