@@ -9,10 +9,10 @@
 //                    slice) (the whole wave for long rows, 64/group outputs per wave for short ones);
 //                    each lane loads VW consecutive elements (16 B when VW > 1), 4 loads in flight,
 //                    butterfly within the group.
-//  k_axis_cols<VW> — otherwise: a workgroup owns a tile of 64 lanes x VW consecutive outputs along
-//                    the innermost kept dim (16 B loads across lanes = coalesced rows); its 4 waves
-//                    split the slice's reduced elements (8 loads in flight per lane) and combine
-//                    through LDS.
+//  k_axis_cols<VW> — otherwise: a workgroup owns a tile of W lanes x VW consecutive outputs along
+//                    the innermost kept dim (W = 64, or fewer when there are few outputs, and then
+//                    64/W rows per wave access); its lanes split the slice's reduced rows (8-16 loads
+//                    in flight per lane) and combine by shuffles and LDS.
 //  When the reduced range is split into slices (few outputs), every slice publishes a partial and
 //  the last slice to arrive for an output (rows) or tile (cols) folds them: one launch, no
 //  second kernel.
@@ -139,15 +139,47 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     }
 }
 
+// Merge the states of lanes that hold the same columns (lane bits >= W, i.e. other rows) and then
+// the 4 waves through LDS, in wave order; the workgroup total for column c ends in wave 0, lane c.
+template <typename T, int OP, int VW>
+__device__ __forceinline__ void cols_combine(Red<T, OP> (&r)[VW], uint64_t *lds, uint32_t W) {
+    constexpr int kWaves = kBlock / 64;
+    constexpr int kW = packed_words<T, OP>();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t m = W; m < 64; m <<= 1) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) xor_merge(r[j], (int)m);
+    }
+    if (wave > 0 && lane < W) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) store_packed<T, OP, false>(lds + (((wave - 1) * 64 + lane) * VW + j) * kW, r[j]);
+    }
+    __syncthreads();
+    if (wave == 0 && lane < W) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            for (int w = 0; w < kWaves - 1; ++w) {
+                Red<T, OP> o;
+                load_packed<T, OP, false>(lds + ((w * 64 + lane) * VW + j) * kW, o);
+                r[j].merge(o);
+            }
+        }
+    }
+}
+
 template <typename T, int OP, bool FUSED, int VW>
 __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
-    constexpr int kU = 8;
+    constexpr int kU = VW * sizeof(T) >= 16 ? 8 : 16;   // loads in flight per lane
     constexpr int kWaves = kBlock / 64;
-    __shared__ uint64_t lds[kWaves - 1][64][VW][kPartialWords];
+    constexpr int kW = packed_words<T, OP>();
+    __shared__ uint64_t lds[(kWaves - 1) * 64 * VW * kW];
+    __shared__ uint32_t s_last;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t nkv = a.n_out / VW;             // kept vectors
-    const uint64_t kv = (uint64_t)blockIdx.x * 64 + lane;
+    const uint32_t W = a.group, R = 64 / W;              // lanes per row of the tile, rows per wave access
+    const uint32_t c = lane & (W - 1), rsub = lane / W;
+    const uint64_t nkv = a.n_out / VW;                   // kept vectors
+    const uint64_t kv = (uint64_t)blockIdx.x * W + c;
     const uint64_t s = blockIdx.y;
     if (!RANK && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;
     const bool active = kv < nkv;
@@ -159,11 +191,12 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
 #pragma unroll
     for (int j = 0; j < VW; ++j) r[j].init();
     if (active) {
-        for (uint64_t r0 = r_lo + wave; r0 < r_hi; r0 += (uint64_t)kWaves * kU) {
+        const uint64_t step = (uint64_t)kWaves * R;      // rows between a lane's consecutive loads
+        for (uint64_t r0 = r_lo + wave * R + rsub; r0 < r_hi; r0 += step * kU) {
             int64_t off[kU], rk[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                uint64_t rr = r0 + (uint64_t)u * kWaves;
+                uint64_t rr = r0 + (uint64_t)u * step;
                 if (rr >= r_hi) rr = r0;  // clamped: every load issues, the value is dropped below
                 off[u] = koff + red_offset<RANK>(a.red, (uint32_t)rr, rk[u]);
             }
@@ -172,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                if (r0 + (uint64_t)u * kWaves >= r_hi) continue;
+                if (r0 + (uint64_t)u * step >= r_hi) continue;
                 T x[VW];
                 raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
@@ -180,38 +213,25 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             }
         }
     }
-    // combine the 4 waves' partial states of each output in wave order
-    __shared__ uint32_t s_last;
-    if (wave > 0) {
-#pragma unroll
-        for (int j = 0; j < VW; ++j) r[j].to_words(lds[wave - 1][lane][j]);
-    }
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-            for (int w = 0; w < kWaves - 1; ++w) {
-                Red<T, OP> o;
-                o.from_words(lds[w][lane][j]);
-                r[j].merge(o);
-            }
-        }
-    }
+    cols_combine<T, OP, VW>(r, lds, W);
+    if (a.probe == 2) return;
     if (a.slices == 1) {
-        if (wave == 0 && active) {
+        if (wave == 0 && lane < W && active) {
 #pragma unroll
             for (int j = 0; j < VW; ++j) write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r[j]);
         }
         return;
     }
-    // Sliced: publish this slice's tile partials ([tile][slice][lane][j], coalesced), count arrivals
-    // per tile; the last slice's workgroup folds all slices (its 4 waves split them, LDS combine).
-    constexpr int kW = packed_words<T, OP>();
-    const uint64_t tile_rec = (uint64_t)64 * VW;
+    // Sliced: publish this slice's records ([tile][slice][c][j], coalesced) and count arrivals per
+    // tile; the workgroup of the last slice to arrive folds all slices: its 256/W lane groups take
+    // contiguous slice ranges, then the same lane + LDS combine.
+    const uint64_t tile_rec = (uint64_t)W * VW;
     uint64_t *P = a.out.partials + (uint64_t)blockIdx.x * a.slices * tile_rec * kW;
     if (wave == 0) {
+        if (lane < W) {
 #pragma unroll
-        for (int j = 0; j < VW; ++j) store_packed<T, OP, true>(P + ((uint64_t)s * tile_rec + lane * VW + j) * kW, r[j]);
+            for (int j = 0; j < VW; ++j) store_packed<T, OP, true>(P + ((uint64_t)s * tile_rec + c * VW + j) * kW, r[j]);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
             uint32_t *tk = a.out.tickets + blockIdx.x;
@@ -221,8 +241,9 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
         }
     }
     __syncthreads();
-    if (!s_last) return;
-    const uint32_t q_lo = wave * a.slices / kWaves, q_hi = (wave + 1) * a.slices / kWaves;
+    if (!s_last || a.probe == 1) return;
+    const uint32_t G = kBlock / W, grp = threadIdx.x / W;    // parallel slice streams
+    const uint32_t q_lo = (uint32_t)((uint64_t)grp * a.slices / G), q_hi = (uint32_t)((uint64_t)(grp + 1) * a.slices / G);
 #pragma unroll
     for (int j = 0; j < VW; ++j) r[j].init();
     if (active) {
@@ -233,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             for (int u = 0; u < kQ; ++u) {
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
-                    if (q0 + u < q_hi) load_packed<T, OP, true>(P + ((uint64_t)(q0 + u) * tile_rec + lane * VW + j) * kW, p[u][j]);
+                    if (q0 + u < q_hi) load_packed<T, OP, true>(P + ((uint64_t)(q0 + u) * tile_rec + c * VW + j) * kW, p[u][j]);
                     else p[u][j].init();
                 }
             }
@@ -244,21 +265,10 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             }
         }
     }
-    if (wave > 0) {
+    cols_combine<T, OP, VW>(r, lds, W);
+    if (wave == 0 && lane < W && active) {
 #pragma unroll
-        for (int j = 0; j < VW; ++j) r[j].to_words(lds[wave - 1][lane][j]);
-    }
-    __syncthreads();
-    if (wave == 0 && active) {
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-            for (int w = 0; w < kWaves - 1; ++w) {
-                Red<T, OP> o;
-                o.from_words(lds[w][lane][j]);
-                r[j].merge(o);
-            }
-            write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r[j]);
-        }
+        for (int j = 0; j < VW; ++j) write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r[j]);
     }
 }
 
@@ -274,7 +284,7 @@ void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
         if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true, 1>), dim3((uint32_t)blocks), block, 0, st, a);
         else hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW>), dim3((uint32_t)blocks), block, 0, st, a);
     } else {
-        const dim3 grid((uint32_t)((a.n_out / VW + 63) / 64), a.slices);
+        const dim3 grid((uint32_t)((a.n_out / VW + a.group - 1) / a.group), a.slices);
         if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((k_axis_cols<T, OP, false, VW>), grid, block, 0, st, a);
     }
@@ -282,8 +292,10 @@ void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
 
 template <typename T, int OP>
 hipError_t launch_axis_t(const KAxis &a, int cus, hipStream_t st) {
-    if (a.vec > 1 && !a.src.fused) launch_axis_vw<T, OP, 16 / sizeof(T)>(a, cus, st);
-    else launch_axis_vw<T, OP, 1>(a, cus, st);
+    if (a.src.fused || a.vec <= 1) launch_axis_vw<T, OP, 1>(a, cus, st);
+    else if (a.vec == 2) launch_axis_vw<T, OP, 2>(a, cus, st);
+    else if constexpr (sizeof(T) == 4) launch_axis_vw<T, OP, 4>(a, cus, st);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -96,40 +96,39 @@ __device__ __forceinline__ T load_elem(const uint8_t *base, uint64_t plane, bool
 template <typename T, bool FUSED, int VW>
 struct Raw {
     using U = typename UIntOf<T>::type;
-    uint4 w;                               // VW > 1: 16 bytes
-    U e;                                   // VW == 1, plain: one element
-    uint32_t b[FUSED ? sizeof(T) : 1];     // VW == 1, fused: its bytes from the planes
+    static constexpr int kBytes = VW * (int)sizeof(T);
+    // VW > 1: one 8- or 16-byte load; VW == 1: one element (fused: its bytes from the planes)
+    using V = std::conditional_t<kBytes == 16, uint4, std::conditional_t<kBytes == 8, uint64_t, U>>;
+    V w;
+    uint32_t b[FUSED ? sizeof(T) : 1];
 };
 
 template <typename T, bool FUSED, int VW>
 __device__ __forceinline__ void raw_load(Raw<T, FUSED, VW> &r, const uint8_t *base, uint64_t plane, uint64_t off) {
-    using U = typename UIntOf<T>::type;
-    if constexpr (VW > 1) {
-        r.w = gld<uint4>(base + off * sizeof(T));
-    } else if constexpr (FUSED) {
+    using V = typename Raw<T, FUSED, VW>::V;
+    if constexpr (FUSED) {
+        static_assert(VW == 1, "fused loads are per element");
 #pragma unroll
         for (int k = 0; k < (int)sizeof(T); ++k) r.b[k] = gld<uint8_t>(base + (uint64_t)k * plane + off);
     } else {
-        r.e = gld<U>(reinterpret_cast<const U *>(base) + off);
+        r.w = gld<V>(base + off * sizeof(T));
     }
 }
 
 template <typename T, bool FUSED, int VW>
 __device__ __forceinline__ void raw_cvt(const Raw<T, FUSED, VW> &r, bool bswap, T (&x)[VW]) {
     using U = typename UIntOf<T>::type;
-    if constexpr (VW > 1) {
-        U e[VW];
-        __builtin_memcpy(e, &r.w, 16);
-#pragma unroll
-        for (int j = 0; j < VW; ++j) x[j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
-    } else if constexpr (FUSED) {
+    U e[VW];
+    if constexpr (FUSED) {
         U u = 0;
 #pragma unroll
         for (int k = 0; k < (int)sizeof(T); ++k) u |= (U)(r.b[k] & 0xffu) << (8 * k);
-        x[0] = from_u<T>(bswap ? bswap_u(u) : u);
+        e[0] = u;
     } else {
-        x[0] = from_u<T>(bswap ? bswap_u(r.e) : r.e);
+        __builtin_memcpy(e, &r.w, sizeof(e));
     }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) x[j] = from_u<T>(bswap ? bswap_u(e[j]) : e[j]);
 }
 
 // ---- missing-data predicate ---------------------------------------------------------------------

@@ -95,7 +95,8 @@ struct KAllStrided {
 
 // Reduction over a subset of axes.  Output o (C order over kept dims) reduces the elements
 // base_off + okept(o) + sum over reduced dims.  Work is split into `slices` slices of the reduced
-// index range; slices > 1 write partials [o][slice] combined by k_axis_combine.
+// index range; with slices > 1 every slice publishes a partial record and the last slice to arrive
+// for an output (rows) or output tile (cols) folds them in the same launch.
 struct KAxis {
     KSrc src;
     KMissing miss;
@@ -109,6 +110,8 @@ struct KAxis {
     uint32_t mode;   // 0 = rows (a wave per output), 1 = cols (a lane per output)
     uint32_t vec;    // elements per 16-byte lane load (1 = scalar)
     uint32_t group;  // rows mode: lanes per output (power of two <= 64); 64/group outputs per wave
+    uint32_t probe;  // tuning probe only (RDX_AXIS_PROBE): 1 = skip the slice fold, 2 = stop after streaming
+    uint32_t pad;
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

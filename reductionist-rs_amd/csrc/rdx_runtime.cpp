@@ -48,6 +48,7 @@ struct Tuning {
     int no_vec = env_int("RDX_NO_VEC", 0);
     int axis_rows_waves = env_int("RDX_AXIS_ROWS_WAVES_PER_CU", 16);   // sliced-rows fill target
     int axis_cols_wgs = env_int("RDX_AXIS_COLS_WGS_PER_CU", 4);        // sliced-cols fill target
+    int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
 };
 
 const Tuning &tuning() {
@@ -265,17 +266,22 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             if (d_status && (can_fail || a.n_out == 0)) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
             if (a.n_out == 0) return RDX_OK;
             uint64_t slices = 1;
-            {   // 16-byte lanes when every stride keeps vectors aligned and inside one dim
-                const uint32_t vw = 16 / p.esz;
+            // vw-element lanes when every stride keeps vectors aligned and inside one dim
+            auto vec_ok = [&](uint32_t vw) {
+                if (vw == 1) return true;
                 const KView &inner = a.mode == 0 ? a.red : a.kept;
                 bool ok = !p.fused && !tuning().no_vec && inner.ndim >= 1 && inner.vstride[0] == 1 &&
-                          inner.count[0] % vw == 0 && a.kept.base_off % (int64_t)vw == 0 && (uintptr_t)src % 16 == 0;
+                          inner.count[0] % vw == 0 && a.kept.base_off % (int64_t)vw == 0 &&
+                          (uintptr_t)src % (vw * p.esz) == 0;
                 for (int k = 0; k < a.kept.ndim; ++k) ok = ok && (a.mode == 1 && k == 0 ? true : a.kept.vstride[k] % (int64_t)vw == 0);
                 for (int k = 0; k < a.red.ndim; ++k) ok = ok && (a.mode == 0 && k == 0 ? true : a.red.vstride[k] % (int64_t)vw == 0);
-                a.vec = ok ? vw : 1;
-            }
+                return ok;
+            };
+            const uint32_t vmax = 16 / p.esz;
             a.group = 64;
+            a.probe = (uint32_t)tuning().axis_probe;
             if (a.mode == 0) {
+                a.vec = vec_ok(vmax) ? vmax : 1;
                 const uint64_t target = (uint64_t)ws->cus * tuning().axis_rows_waves;     // waves
                 const uint64_t nrv = a.n_red / a.vec;
                 // short rows: just enough lanes per output for 4 loads in flight per lane
@@ -284,15 +290,40 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 if (a.group == 64 && a.n_out < target)
                     slices = std::min<uint64_t>((target + a.n_out - 1) / a.n_out, (nrv + 255) / 256);
             } else {
-                const uint64_t tiles = (a.n_out / a.vec + 63) / 64;
+                // Tile width W lanes x vw outputs; slices of the reduced rows fill the chip, bounded so
+                // that the last slice's fold (one workgroup, 256/W parallel slice streams) stays short:
+                // fold bytes per tile <= 64 KiB (128 KiB with >= 8 streams), <= 16 slices per stream.
+                const bool frank = (p.dtype == RDX_DTYPE_FLOAT32 || p.dtype == RDX_DTYPE_FLOAT64) &&
+                                   (p.op == RDX_OP_MIN || p.op == RDX_OP_MAX);
+                const uint64_t rec = 8 * ((p.op != RDX_OP_COUNT) + (p.op == RDX_OP_SUM && p.dtype == RDX_DTYPE_FLOAT64) +
+                                          1 + (frank ? 3 : 0));
                 const uint64_t target = (uint64_t)ws->cus * tuning().axis_cols_wgs;      // workgroups
-                if (tiles < target) slices = std::min<uint64_t>((target + tiles - 1) / tiles, (a.n_red + 31) / 32);
+                uint64_t best_wgs = 0;
+                for (uint32_t vw = vmax; vw >= 1; vw /= 2) {
+                    if (!vec_ok(vw)) continue;
+                    const uint64_t nkv = a.n_out / vw;
+                    uint32_t W = 64;
+                    while (W > 1 && W / 2 >= nkv) W /= 2;
+                    const uint64_t tiles = (nkv + W - 1) / W, G = kBlock / W, R = 64 / W;
+                    const uint64_t budget = std::min<uint64_t>(65536 * std::max<uint64_t>(1, G / 4), 131072);
+                    const uint64_t smax = std::max<uint64_t>(
+                        1, std::min({budget / (W * vw * rec), 16 * G, a.n_red / (16 * R)}));
+                    const uint64_t sl = std::max<uint64_t>(1, std::min((target + tiles - 1) / tiles, smax));
+                    const uint64_t wgs = tiles * sl;
+                    if (wgs > best_wgs) {
+                        best_wgs = wgs;
+                        a.vec = vw;
+                        a.group = W;
+                        slices = sl;
+                    }
+                    if (wgs * 2 >= target) break;   // the widest lanes that fill the chip
+                }
             }
             slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, 65535));
             a.slices = (uint32_t)slices;
             if (slices > 1) {   // partial records + one self-resetting arrival counter per output / tile
-                const uint64_t tiles = (a.n_out / a.vec + 63) / 64;
-                const uint64_t recs = a.mode == 0 ? a.n_out : tiles * 64 * a.vec;
+                const uint64_t tiles = (a.n_out / a.vec + a.group - 1) / a.group;
+                const uint64_t recs = a.mode == 0 ? a.n_out : tiles * a.group * a.vec;
                 if ((st = ensure(ws, ws->partials, recs * slices * kPartialWords, s))) return st;
                 if ((st = ensure(ws, ws->tickets, std::max<uint64_t>(a.mode == 0 ? a.n_out : tiles, kTicketWords), s,
                                  true)))

@@ -154,6 +154,31 @@ def test_nan_raises_like_reference_panic(engine):
             assert_parity(engine, op, {"dtype": dtype, "shape": [64, 64], "axis": []}, v.tobytes())
 
 
+@pytest.mark.parametrize("shape,axis,dtype,op", [
+    ([65536, 32], 0, "float64", "min"),       # narrow tile: 16 lanes x 2 per row, 4 rows per access, long fold
+    ([4096, 48], 0, "float32", "sum"),        # 12 vectors -> 16-lane tile
+    ([3000, 130], 0, "int32", "max"),         # 130 % 4 != 0 -> 8-byte lanes
+    ([2048, 1024], 0, "float32", "sum"),      # narrower lanes chosen to bound the fold
+    ([64, 512, 96], 1, "uint64", "count"),    # cols over a middle axis, missing filter
+    ([8, 4096, 3], 1, "float32", "max"),      # odd inner width, scalar lanes
+    ([40000, 2], 0, "int64", "sum"),          # 2 outputs
+])
+def test_cols_tilings(engine, shape, axis, dtype, op):
+    """Column-mode tile shapes (k_axis_cols): W lanes x VW outputs, several rows per wave access,
+    sliced reductions folded by the last slice; bit-exact vs the oracle."""
+    rng = np.random.default_rng(11)
+    n = int(np.prod(shape))
+    real = dtype.startswith("float") and op != "sum"   # float sums: exactly summable values (bit-exact)
+    v = (rng.standard_normal(n) * 100 if real else rng.integers(-1000, 1000, n)).astype(NP[dtype])
+    req = {"dtype": dtype, "shape": shape, "axis": axis}
+    if op == "count":
+        req["missing"] = {"valid_min": 0}
+    if dtype.startswith("float") and op in ("min", "max"):
+        v[rng.integers(0, n, 50)] = 0.0
+        v[rng.integers(0, n, 50)] = -0.0           # ±0 ties across slices
+    assert_parity(engine, op, req, v.tobytes())
+
+
 def test_long_missing_values_list(engine):
     rng = np.random.default_rng(3)
     for dtype in NP:
