@@ -71,7 +71,7 @@ __device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *bas
         const uint64_t e = t0 + threadIdx.x * 16;
         if (FULL || e + 16 <= vb) {
 #pragma unroll
-            for (int k = 0; k < (int)sizeof(T); ++k) tl.p[k] = gld<uint4>(base + (uint64_t)k * plane + e);
+            for (int k = 0; k < (int)sizeof(T); ++k) tl.p[k] = gld_stream<uint4>(base + (uint64_t)k * plane + e);
         }
     } else {
         const uint8_t *b = base + t0 * sizeof(T);
@@ -79,7 +79,7 @@ __device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *bas
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
-            if (FULL || o + 16 <= lim) tl.p[m] = gld<uint4>(b + o);
+            if (FULL || o + 16 <= lim) tl.p[m] = gld_stream<uint4>(b + o);
         }
     }
 }

@@ -11,7 +11,8 @@ from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent          # reductionist-rs_amd/
 REPO_ROOT = PKG_ROOT.parent
-LIB_PATH = PKG_ROOT / "librdx.so"
+# RDX_LIB_PATH: an alternative in-tree build of the same library (A/B tuning measurements only)
+LIB_PATH = Path(os.environ.get("RDX_LIB_PATH", str(PKG_ROOT / "librdx.so")))
 
 RDX_ABI_VERSION = 1
 RDX_MAX_NDIM = 32
