@@ -296,7 +296,9 @@ void launch_contig_u(const KAllContig &a, dim3 grid, hipStream_t s) {
 template <typename T, int OP>
 hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
     const dim3 grid(a.blocks_per_chunk * n_chunks);
-    launch_contig_u<T, OP, 2>(a, grid, s);  // 4 tiles in flight measured no faster (tools/sweep2.py)
+    // 2 tiles in flight per lane at one workgroup per CU: 4 tiles, or 2/4/6/8 workgroups per CU,
+    // measured slower with non-temporal loads (tools/gpu_bpcu.sh, gpurun_out/bpcu*).
+    launch_contig_u<T, OP, 2>(a, grid, s);
     return hipGetLastError();
 }
 
@@ -334,28 +336,14 @@ hipError_t launch_strided_op(uint32_t op, const KAllStrided &a, uint32_t n, hipS
 
 }  // namespace
 
-hipError_t launch_all_contig(uint32_t dtype, uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
-    switch (dtype) {
-        case RDX_DTYPE_INT32: return launch_contig_op<int32_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_INT64: return launch_contig_op<int64_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_UINT32: return launch_contig_op<uint32_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_UINT64: return launch_contig_op<uint64_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_FLOAT32: return launch_contig_op<float>(op, a, n_chunks, s);
-        case RDX_DTYPE_FLOAT64: return launch_contig_op<double>(op, a, n_chunks, s);
-    }
-    return hipErrorInvalidValue;
+// One dtype per translation unit (the Makefile builds this file once per RDX_T, in parallel); the
+// dtype switch lives in k_dispatch.cpp.
+hipError_t RDX_KFN(launch_all_contig)(uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
+    return launch_contig_op<RDX_T>(op, a, n_chunks, s);
 }
 
-hipError_t launch_all_strided(uint32_t dtype, uint32_t op, const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
-    switch (dtype) {
-        case RDX_DTYPE_INT32: return launch_strided_op<int32_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_INT64: return launch_strided_op<int64_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_UINT32: return launch_strided_op<uint32_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_UINT64: return launch_strided_op<uint64_t>(op, a, n_chunks, s);
-        case RDX_DTYPE_FLOAT32: return launch_strided_op<float>(op, a, n_chunks, s);
-        case RDX_DTYPE_FLOAT64: return launch_strided_op<double>(op, a, n_chunks, s);
-    }
-    return hipErrorInvalidValue;
+hipError_t RDX_KFN(launch_all_strided)(uint32_t op, const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
+    return launch_strided_op<RDX_T>(op, a, n_chunks, s);
 }
 
 }  // namespace rdx

@@ -312,16 +312,9 @@ hipError_t launch_axis_op(uint32_t op, const KAxis &a, int cus, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_axis(uint32_t dtype, uint32_t op, const KAxis &a, int cus, hipStream_t s) {
-    switch (dtype) {
-        case RDX_DTYPE_INT32: return launch_axis_op<int32_t>(op, a, cus, s);
-        case RDX_DTYPE_INT64: return launch_axis_op<int64_t>(op, a, cus, s);
-        case RDX_DTYPE_UINT32: return launch_axis_op<uint32_t>(op, a, cus, s);
-        case RDX_DTYPE_UINT64: return launch_axis_op<uint64_t>(op, a, cus, s);
-        case RDX_DTYPE_FLOAT32: return launch_axis_op<float>(op, a, cus, s);
-        case RDX_DTYPE_FLOAT64: return launch_axis_op<double>(op, a, cus, s);
-    }
-    return hipErrorInvalidValue;
+// One dtype per translation unit (see k_all.hip); the dtype switch lives in k_dispatch.cpp.
+hipError_t RDX_KFN(launch_axis)(uint32_t op, const KAxis &a, int cus, hipStream_t s) {
+    return launch_axis_op<RDX_T>(op, a, cus, s);
 }
 
 }  // namespace rdx

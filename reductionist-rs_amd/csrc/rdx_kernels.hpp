@@ -1,8 +1,14 @@
 // Launch entry points of the gfx950 kernels (k_all.hip, k_axis.hip, k_map.hip).
+// k_all.hip and k_axis.hip are compiled once per dtype (RDX_T / RDX_TNAME, Makefile) so the
+// template-heavy kernels build in parallel; k_dispatch.cpp switches on the runtime dtype.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include "rdx_kdesc.h"
+
+#define RDX_KCAT2(a, b) a##_##b
+#define RDX_KCAT(a, b) RDX_KCAT2(a, b)
+#define RDX_KFN(name) RDX_KCAT(name, RDX_TNAME)
 
 namespace rdx {
 
@@ -11,5 +17,17 @@ hipError_t launch_all_strided(uint32_t dtype, uint32_t op, const KAllStrided &a,
 hipError_t launch_axis(uint32_t dtype, uint32_t op, const KAxis &a, int cus, hipStream_t s);
 hipError_t launch_map(uint32_t dtype, const KMap &a, int cus, hipStream_t s);
 hipError_t launch_unshuffle(const uint8_t *in, uint8_t *out, uint64_t len, uint64_t es, int cus, hipStream_t s);
+
+#define RDX_DECLARE_DTYPE(tn)                                                                                  \
+    hipError_t launch_all_contig_##tn(uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s);    \
+    hipError_t launch_all_strided_##tn(uint32_t op, const KAllStrided &a, uint32_t n_chunks, hipStream_t s);  \
+    hipError_t launch_axis_##tn(uint32_t op, const KAxis &a, int cus, hipStream_t s);
+RDX_DECLARE_DTYPE(i32)
+RDX_DECLARE_DTYPE(i64)
+RDX_DECLARE_DTYPE(u32)
+RDX_DECLARE_DTYPE(u64)
+RDX_DECLARE_DTYPE(f32)
+RDX_DECLARE_DTYPE(f64)
+#undef RDX_DECLARE_DTYPE
 
 }  // namespace rdx

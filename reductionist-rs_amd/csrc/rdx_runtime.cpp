@@ -42,7 +42,7 @@ int env_int(const char *name, int dflt) {
 // Tuning knobs, read from the environment once (getenv scans the whole environment: microseconds per
 // request if done per launch).
 struct Tuning {
-    int blocks_per_cu = env_int("RDX_BLOCKS_PER_CU", 2);
+    int blocks_per_cu = env_int("RDX_BLOCKS_PER_CU", 1);  // k_all_contig fill target (gpurun_out/bpcu2)
     int min_tiles = env_int("RDX_MIN_TILES_PER_BLOCK", 2);
     int force_bpc = env_int("RDX_FORCE_BPC", 0);   // tuning only
     int no_vec = env_int("RDX_NO_VEC", 0);
