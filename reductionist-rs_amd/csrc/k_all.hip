@@ -38,11 +38,11 @@ __device__ __forceinline__ uint32_t comp(const uint4 &v, int j) {
     return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
-template <typename T, int OP, bool MISS>
+template <typename T, int OP, int MK>
 __device__ __forceinline__ void consume(Red<T, OP> &r, T x, const KAllContig &a, uint64_t e) {
     auto rank = [&]() -> int64_t { return a.r0 + (int64_t)(e - a.off) * a.rs; };
-    if constexpr (MISS) {
-        if (!included(a.miss, x, a.filter_semantics)) return;
+    if constexpr (MK != MK_NONE) {
+        if (!included_mk<T, MK>(a.miss, x, a.filter_semantics)) return;
     }
     if constexpr (OP == OP_COUNT) r.cnt += 1;
     else r.add(x, rank);
@@ -84,7 +84,7 @@ __device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *bas
     }
 }
 
-template <typename T, int OP, bool FUSED, bool MISS, bool FULL>
+template <typename T, int OP, bool FUSED, int MK, bool FULL>
 __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED> &tl, const KAllContig &a, uint64_t t0,
                                              uint64_t vb, uint32_t selA, uint32_t selB) {
     using U = typename UIntOf<T>::type;
@@ -92,7 +92,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
     if constexpr (FUSED) {
         const uint64_t e = t0 + threadIdx.x * 16;
         if (!FULL && e + 16 > vb) return;
-        if constexpr (OP == OP_COUNT && !MISS) {
+        if constexpr (OP == OP_COUNT && MK == MK_NONE) {
             r.cnt += 16;
             return;
         }
@@ -101,7 +101,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
             uint32_t lo[4];
             if constexpr (sizeof(T) == 4) {
                 transpose4(comp(tl.p[0], j), comp(tl.p[1], j), comp(tl.p[2], j), comp(tl.p[3], j), selA, selB, lo);
-                if constexpr (OP == OP_SUM && std::is_same_v<T, float> && !MISS) {
+                if constexpr (OP == OP_SUM && std::is_same_v<T, float> && MK == MK_NONE) {
                     // pairwise f64 partial of 4 elements (ILP), then one dependent add
                     const double s01 = (double)__builtin_bit_cast(float, lo[0]) + (double)__builtin_bit_cast(float, lo[1]);
                     const double s23 = (double)__builtin_bit_cast(float, lo[2]) + (double)__builtin_bit_cast(float, lo[3]);
@@ -109,7 +109,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
                     r.cnt += 4;
                 } else {
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) consume<T, OP, MISS>(r, from_u<T>((U)lo[m]), a, e + j * 4 + m);
+                    for (int m = 0; m < 4; ++m) consume<T, OP, MK>(r, from_u<T>((U)lo[m]), a, e + j * 4 + m);
                 }
             } else {
                 // 8-byte elements: low dwords from planes 0-3, high from 4-7 (swapped + reversed
@@ -122,7 +122,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
                            selA, selB, hi);
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
-                    consume<T, OP, MISS>(r, from_u<T>((U)(((uint64_t)hi[m] << 32) | lo[m])), a, e + j * 4 + m);
+                    consume<T, OP, MK>(r, from_u<T>((U)(((uint64_t)hi[m] << 32) | lo[m])), a, e + j * 4 + m);
             }
         }
     } else {
@@ -133,13 +133,13 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
             const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
             if (!FULL && o + 16 > lim) continue;
             const uint64_t e = t0 + o / sizeof(T);
-            if constexpr (OP == OP_COUNT && !MISS) {
+            if constexpr (OP == OP_COUNT && MK == MK_NONE) {
                 r.cnt += kPer;
                 continue;
             }
             if constexpr (sizeof(T) == 4) {
                 uint32_t w[4] = {tl.p[m].x, tl.p[m].y, tl.p[m].z, tl.p[m].w};
-                if constexpr (OP == OP_SUM && std::is_same_v<T, float> && !MISS) {
+                if constexpr (OP == OP_SUM && std::is_same_v<T, float> && MK == MK_NONE) {
                     float f[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) f[q] = __builtin_bit_cast(float, bswap ? bswap_u(w[q]) : w[q]);
@@ -149,7 +149,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const uint32_t u = bswap ? bswap_u(w[q]) : w[q];
-                        consume<T, OP, MISS>(r, from_u<T>((U)u), a, e + q);
+                        consume<T, OP, MK>(r, from_u<T>((U)u), a, e + q);
                     }
                 }
             } else {
@@ -157,14 +157,14 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const uint64_t u = bswap ? bswap_u(w[q]) : w[q];
-                    consume<T, OP, MISS>(r, from_u<T>((U)u), a, e + q);
+                    consume<T, OP, MK>(r, from_u<T>((U)u), a, e + q);
                 }
             }
         }
     }
 }
 
-template <typename T, int OP, bool FUSED, bool MISS, int UNR>
+template <typename T, int OP, bool FUSED, int MK, int UNR>
 __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
@@ -188,9 +188,9 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     // scalar head and tail (< G elements each), owned by workgroup 0 of the chunk
     if (b == 0) {
         for (uint64_t e = lo + threadIdx.x; e < va; e += kBlock)
-            consume<T, OP, MISS>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
+            consume<T, OP, MK>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
         for (uint64_t e = vb + threadIdx.x; e < hi; e += kBlock)
-            consume<T, OP, MISS>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
+            consume<T, OP, MK>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
     }
     // vector body: full tiles split into contiguous per-workgroup ranges, UNR tiles in flight per
     // lane; the one partial tile (if any) goes to workgroup 0 with the scalar head/tail.
@@ -205,17 +205,17 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, va + (t + u) * te, vb);
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MISS, true>(r, x[u], a, va + (t + u) * te, vb, selA, selB);
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, va + (t + u) * te, vb, selA, selB);
     }
     for (; t < t_end; ++t) {
         Tile<T, FUSED> x0;
         load_tile<T, FUSED, true>(x0, base, a.src.plane, va + t * te, vb);
-        consume_tile<T, OP, FUSED, MISS, true>(r, x0, a, va + t * te, vb, selA, selB);
+        consume_tile<T, OP, FUSED, MK, true>(r, x0, a, va + t * te, vb, selA, selB);
     }
     if (b == 0 && va + nfull * te < vb) {
         Tile<T, FUSED> x0;
         load_tile<T, FUSED, false>(x0, base, a.src.plane, va + nfull * te, vb);
-        consume_tile<T, OP, FUSED, MISS, false>(r, x0, a, va + nfull * te, vb, selA, selB);
+        consume_tile<T, OP, FUSED, MK, false>(r, x0, a, va + nfull * te, vb, selA, selB);
     }
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
@@ -225,15 +225,66 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
 // multiples of VW and the origin is VW-aligned, so each lane loads VW consecutive elements with one
 // 16-byte global_load.  U vectors per lane are in flight at once; the host sizes the grid so a
 // lane normally needs a single round trip.
-template <typename T, int OP, bool FUSED, int VW>
+// ND > 0: the view has exactly ND canonical dims, known at compile time.  The dims' counts, magic
+// divisors and strides are then read from the kernel arguments once, up front (all scalar loads
+// issued together), instead of inside the per-vector decomposition loop, where every dim of every
+// vector waited for its own scalar-cache miss on a cold launch (~5 us of an 11 us C3 launch).
+// ND == 0: any ndim (<= kMaxKDims), read in the loop.
+template <int ND>
+struct DimRegs {
+    static constexpr int N = ND > 0 ? ND : 1;
+    uint32_t count[N];
+    uint64_t magic[N];
+    int64_t vstride[N], rstride[N];
+    __device__ __forceinline__ void load(const KView &v) {
+        if constexpr (ND > 0) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                count[k] = v.count[k];
+                magic[k] = v.div[k].magic;
+                vstride[k] = v.vstride[k];
+                rstride[k] = v.rstride[k];
+            }
+        }
+    }
+};
+
+// element offset and fold rank of flattened index q (innermost-first digits)
+template <int ND, bool RANK>
+__device__ __forceinline__ void decompose(const KView &v, const DimRegs<ND> &d, uint32_t q, int64_t &o, int64_t &rr) {
+    o = v.base_off;
+    rr = v.r0;
+    if constexpr (ND > 0) {
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+            const uint32_t qn = udiv(q, d.magic[k]);
+            const uint32_t idx = q - qn * d.count[k];
+            o += (int64_t)idx * d.vstride[k];
+            if constexpr (RANK) rr += (int64_t)idx * d.rstride[k];
+            q = qn;
+        }
+    } else {
+        for (int k = 0; k < v.ndim; ++k) {
+            const uint32_t qn = udiv(q, v.div[k].magic);
+            const uint32_t idx = q - qn * v.count[k];
+            o += (int64_t)idx * v.vstride[k];
+            if constexpr (RANK) rr += (int64_t)idx * v.rstride[k];
+            q = qn;
+        }
+    }
+}
+
+template <typename T, int OP, bool FUSED, int VW, int ND, int MK>
 __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
     constexpr int kU = VW > 1 ? 4 : 8;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
     const uint8_t *base = chunk_base(a.src, chunk);
     const bool bswap = a.src.bswap;
-    const bool miss = a.miss.kind != RDX_MISSING_NONE;
     const KView &v = a.view;
+    DimRegs<ND> d;
+    d.load(v);
+    const int64_t rs0 = ND > 0 ? d.rstride[0] : v.rstride[0];
     Red<T, OP> r;
     r.init();
     const uint64_t nv = v.n / VW;
@@ -249,17 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
             uint64_t g = g0 + (uint64_t)u * kBlock;
             ok[u] = g < g_end;
             if (!ok[u]) g = g0;  // clamped into the range: the load issues unconditionally
-            uint32_t q = (uint32_t)(g * VW);
-            int64_t o = v.base_off, rr = v.r0;
-            for (int k = 0; k < v.ndim; ++k) {
-                const uint32_t qn = udiv(q, v.div[k].magic);
-                const uint32_t idx = q - qn * v.count[k];
-                o += (int64_t)idx * v.vstride[k];
-                if constexpr (Red<T, OP>::kRank) rr += (int64_t)idx * v.rstride[k];
-                q = qn;
-            }
-            off[u] = o;
-            rk[u] = rr;
+            decompose<ND, Red<T, OP>::kRank>(v, d, (uint32_t)(g * VW), off[u], rk[u]);
         }
         Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
@@ -271,26 +312,35 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
             if (!ok[u]) continue;
 #pragma unroll
             for (int j = 0; j < VW; ++j) {
-                if (miss && !included(a.miss, x[u][j], a.filter_semantics)) continue;
+                if (!included_mk<T, MK>(a.miss, x[u][j], a.filter_semantics)) continue;
                 if constexpr (OP == OP_COUNT) r.cnt += 1;
-                else r.add(x[u][j], [&]() { return rk[u] + (int64_t)j * v.rstride[0]; });
+                else r.add(x[u][j], [&]() { return rk[u] + (int64_t)j * rs0; });
             }
         }
     }
+#ifdef RDX_X_NOFIN      // timing experiments only (wrong results)
+    block_reduce(r);
+    if (threadIdx.x == 0) store_packed<T, OP, false>(a.out.partials + (uint64_t)blockIdx.x * kPartialWords, r);
+#else
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
+#endif
 }
 
 template <typename T, int OP, int UNR>
 void launch_contig_u(const KAllContig &a, dim3 grid, hipStream_t s) {
     const dim3 block(kBlock);
-    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    const int mk = miss_kind_of(a.miss.kind);
+#define RDX_CONTIG(F, M) hipLaunchKernelGGL((k_all_contig<T, OP, F, M, UNR>), grid, block, 0, s, a)
     if (a.src.fused) {
-        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, true, true, UNR>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_all_contig<T, OP, true, false, UNR>), grid, block, 0, s, a);
+        if (mk == MK_NONE) RDX_CONTIG(true, MK_NONE);
+        else if (mk == MK_CMP) RDX_CONTIG(true, MK_CMP);
+        else RDX_CONTIG(true, MK_ANY);
     } else {
-        if (miss) hipLaunchKernelGGL((k_all_contig<T, OP, false, true, UNR>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_all_contig<T, OP, false, false, UNR>), grid, block, 0, s, a);
+        if (mk == MK_NONE) RDX_CONTIG(false, MK_NONE);
+        else if (mk == MK_CMP) RDX_CONTIG(false, MK_CMP);
+        else RDX_CONTIG(false, MK_ANY);
     }
+#undef RDX_CONTIG
 }
 
 template <typename T, int OP>
@@ -302,13 +352,33 @@ hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s
     return hipGetLastError();
 }
 
+template <typename T, int OP, bool FUSED, int VW, int MK>
+void launch_strided_nd(const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
+    const dim3 grid(a.blocks_per_chunk * n_chunks), block(kBlock);
+    switch (a.view.ndim) {   // canonical views of up to 4 dims cover the 1-4-D arrays of the API
+        case 1: hipLaunchKernelGGL((k_all_strided<T, OP, FUSED, VW, 1, MK>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_all_strided<T, OP, FUSED, VW, 2, MK>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_all_strided<T, OP, FUSED, VW, 3, MK>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_all_strided<T, OP, FUSED, VW, 4, MK>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_all_strided<T, OP, FUSED, VW, 0, MK>), grid, block, 0, s, a); break;
+    }
+}
+
+template <typename T, int OP, bool FUSED, int VW>
+void launch_strided_mk(const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
+    switch (miss_kind_of(a.miss.kind)) {
+        case MK_NONE: launch_strided_nd<T, OP, FUSED, VW, MK_NONE>(a, n_chunks, s); break;
+        case MK_CMP: launch_strided_nd<T, OP, FUSED, VW, MK_CMP>(a, n_chunks, s); break;
+        default: launch_strided_nd<T, OP, FUSED, VW, MK_ANY>(a, n_chunks, s); break;
+    }
+}
+
 template <typename T, int OP>
 hipError_t launch_strided_t(const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
-    const dim3 grid(a.blocks_per_chunk * n_chunks), block(kBlock);
     constexpr int VW = 16 / sizeof(T);
-    if (a.src.fused) hipLaunchKernelGGL((k_all_strided<T, OP, true, 1>), grid, block, 0, s, a);
-    else if (a.vec > 1) hipLaunchKernelGGL((k_all_strided<T, OP, false, VW>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_all_strided<T, OP, false, 1>), grid, block, 0, s, a);
+    if (a.src.fused) launch_strided_mk<T, OP, true, 1>(a, n_chunks, s);
+    else if (a.vec > 1) launch_strided_mk<T, OP, false, VW>(a, n_chunks, s);
+    else launch_strided_mk<T, OP, false, 1>(a, n_chunks, s);
     return hipGetLastError();
 }
 

@@ -194,6 +194,37 @@ __device__ __forceinline__ bool included(const KMissing &m, T x, bool filter_sem
     return inc;
 }
 
+// The predicate specialised at compile time by the kernels' MK parameter:
+//   MK 0: no missing data;  MK 1: one comparison form (missing_value / valid_min / valid_max /
+//   valid_range) evaluated branch-free from wave-uniform flags;  MK 2: anything (missing_values lists).
+// Small kernels pay for code size (a cold instruction cache per CU): the generic switch of
+// `included` in every element loop cost ~1.2 us of a 10 us C3 launch.
+enum MissKind : int { MK_NONE = 0, MK_CMP = 1, MK_ANY = 2 };
+
+template <typename T, int MK>
+__device__ __forceinline__ bool included_mk(const KMissing &m, T x, bool filter_semantics) {
+    if constexpr (MK == MK_NONE) {
+        return true;
+    } else if constexpr (MK == MK_ANY) {
+        return included(m, x, filter_semantics);
+    } else {
+        const uint32_t k = m.kind;
+        const T a = from_bits64<T>(m.v0), b = from_bits64<T>(m.v1);
+        const bool eq_on = k == RDX_MISSING_VALUE;
+        const bool lo_on = k == RDX_MISSING_VALID_MIN || k == RDX_MISSING_VALID_RANGE;
+        const bool hi_on = k == RDX_MISSING_VALID_MAX || k == RDX_MISSING_VALID_RANGE;
+        const T hi = k == RDX_MISSING_VALID_MAX ? a : b;
+        const bool missing = (eq_on & (x == a)) | (lo_on & (x < a)) | (hi_on & (x > hi));
+        bool inc = !missing;
+        if constexpr (std::is_floating_point_v<T>) inc = inc & !(filter_semantics & (lo_on | hi_on) & (x != x));
+        return inc;
+    }
+}
+
+__host__ __device__ inline int miss_kind_of(uint32_t kind) {
+    return kind == RDX_MISSING_NONE ? MK_NONE : kind == RDX_MISSING_VALUES ? MK_ANY : MK_CMP;
+}
+
 // ---- reduction state ------------------------------------------------------------------------------
 // SUM:   integers wrap (release profile) — accumulated in u64 and truncated to T;
 //        f32 accumulated in f64 and rounded once; f64 Neumaier-compensated (operations.rs:622-632
