@@ -17,11 +17,17 @@ namespace {
 
 // VW > 1: contiguous, VW-aligned inner runs in BOTH the input view and the output (output order is
 // the traversal order), so each lane moves VW elements with one 16-byte load and one 16-byte store.
-template <typename T, bool FUSED, int VW>
+// KIND (a.kind) and MK (missing-predicate form) are compile-time, so the element loop carries no
+// runtime switches.
+// Offsets: a lane's kU vectors lie kBlock vectors apart in output order; the first is decomposed
+// into (inner index, outer offset) with one magic division per dim, the others are the same row
+// moved along the inner dim (vstride[0]) while they stay inside it — only a vector that crosses a
+// row end is decomposed in full.  Select's long rows (C5: 32768-element runs) thus cost one
+// decomposition per kU vectors instead of kU full ones (the map was ALU-bound on them).
+template <typename T, bool FUSED, int VW, int KIND, int MK>
 __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
     constexpr int kU = 4;
     const KView &v = a.view;
-    const bool miss = a.miss.kind != RDX_MISSING_NONE;
     const bool bswap = a.src.bswap;
     int64_t cnt = 0;
     const uint64_t nv = v.n / VW;
@@ -30,24 +36,41 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
     const uint64_t g_begin = (uint64_t)blockIdx.x * per;
     const uint64_t g_end = g_begin + per < nv ? g_begin + per : nv;
     const uint64_t stride = kBlock;
+    const uint32_t count0 = v.count[0];
+    const uint64_t magic0 = v.div[0].magic;
+    const int64_t vs0 = v.vstride[0];
+    auto outer = [&](uint32_t q) -> int64_t {   // offset of outer index q (dims 1..ndim-1)
+        int64_t o = v.base_off;
+        for (int k = 1; k < v.ndim; ++k) {
+            const uint32_t qn = udiv(q, v.div[k].magic);
+            o += (int64_t)(q - qn * v.count[k]) * v.vstride[k];
+            q = qn;
+        }
+        return o;
+    };
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;  // nothing here can fail
     for (uint64_t g0 = g_begin + threadIdx.x; g0 < g_end; g0 += stride * kU) {
         int64_t off[kU];
         bool ok[kU];
         T x[kU][VW];
+        {
+            const uint32_t q = (uint32_t)(g0 * VW);
+            const uint32_t q1 = udiv(q, magic0);
+            const uint32_t i0 = q - q1 * count0;
+            const int64_t ob = outer(q1);
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            uint64_t g = g0 + (uint64_t)u * stride;
-            ok[u] = g < g_end;
-            if (!ok[u]) g = g0;  // clamped into the range: the load issues unconditionally
-            uint32_t q = (uint32_t)(g * VW);
-            int64_t o = v.base_off;
-            for (int k = 0; k < v.ndim; ++k) {
-                const uint32_t qn = udiv(q, v.div[k].magic);
-                o += (int64_t)(q - qn * v.count[k]) * v.vstride[k];
-                q = qn;
+            for (int u = 0; u < kU; ++u) {
+                uint64_t g = g0 + (uint64_t)u * stride;
+                ok[u] = g < g_end;
+                if (!ok[u]) g = g0;  // clamped into the range: the load issues unconditionally
+                const uint64_t iu = (uint64_t)i0 + (g - g0) * VW;
+                if (iu < count0) {
+                    off[u] = ob + (int64_t)iu * vs0;
+                } else {
+                    const uint32_t qq = (uint32_t)(g * VW), qq1 = udiv(qq, magic0);
+                    off[u] = outer(qq1) + (int64_t)(qq - qq1 * count0) * vs0;
+                }
             }
-            off[u] = o;
         }
         Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
@@ -61,14 +84,14 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
             int64_t c[VW];
 #pragma unroll
             for (int j = 0; j < VW; ++j) {
-                if (a.kind == 0) c[j] = (!miss || included(a.miss, x[u][j], true)) ? 1 : 0;
-                else c[j] = (miss && is_missing(a.miss, x[u][j])) ? 0 : 1;
+                if constexpr (KIND == 0) c[j] = included_mk<T, MK>(a.miss, x[u][j], true) ? 1 : 0;
+                else c[j] = included_mk<T, MK>(a.miss, x[u][j], false) ? 1 : 0;
             }
-            if (a.kind == 0) {
+            if constexpr (KIND == 0 && MK != MK_NONE) {
 #pragma unroll
                 for (int j = 0; j < VW; ++j) cnt += c[j];
             }
-            if (a.kind != 2) {  // values
+            if constexpr (KIND != 2) {  // values
                 if constexpr (VW == 1) {
                     gst<T>(reinterpret_cast<T *>(a.out.body) + g, x[u][0]);
                 } else {
@@ -77,24 +100,24 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
                     gst<uint4>(reinterpret_cast<T *>(a.out.body) + g, w);
                 }
             }
-            if (a.kind != 0) {  // per-element counts (and the body itself for Count)
+            if constexpr (KIND != 0) {  // per-element counts (and the body itself for Count)
 #pragma unroll
                 for (int j = 0; j < VW; j += 2) {
                     if constexpr (VW == 1) {
                         gst<int64_t>(a.out.counts + g, c[0]);
-                        if (a.kind == 2) gst<int64_t>(reinterpret_cast<int64_t *>(a.out.body) + g, c[0]);
+                        if constexpr (KIND == 2) gst<int64_t>(reinterpret_cast<int64_t *>(a.out.body) + g, c[0]);
                     } else {
                         uint4 w;
                         __builtin_memcpy(&w, &c[j], 16);
                         gst<uint4>(a.out.counts + g + j, w);
-                        if (a.kind == 2) gst<uint4>(reinterpret_cast<int64_t *>(a.out.body) + g + j, w);
+                        if constexpr (KIND == 2) gst<uint4>(reinterpret_cast<int64_t *>(a.out.body) + g + j, w);
                     }
                 }
             }
         }
     }
-    if (a.kind == 0) {
-        if (miss) finalize_count(cnt, a.out.counts, a.out.partials, a.out.tickets, gridDim.x, blockIdx.x);
+    if constexpr (KIND == 0) {
+        if constexpr (MK != MK_NONE) finalize_count(cnt, a.out.counts, a.out.partials, a.out.tickets, gridDim.x, blockIdx.x);
         else if (blockIdx.x == 0 && threadIdx.x == 0) a.out.counts[0] = (int64_t)v.n;  // sliced.len()
     }
 }
@@ -132,6 +155,23 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle_big(const uint8_t *__restr
     }
 }
 
+template <typename T, bool FUSED, int VW, int KIND>
+void launch_map_mk(const KMap &a, dim3 grid, hipStream_t s) {
+    const dim3 block(kBlock);
+    switch (miss_kind_of(a.miss.kind)) {
+        case MK_NONE: hipLaunchKernelGGL((k_map<T, FUSED, VW, KIND, MK_NONE>), grid, block, 0, s, a); break;
+        case MK_CMP: hipLaunchKernelGGL((k_map<T, FUSED, VW, KIND, MK_CMP>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_map<T, FUSED, VW, KIND, MK_ANY>), grid, block, 0, s, a); break;
+    }
+}
+
+template <typename T, bool FUSED, int VW>
+void launch_map_kind(const KMap &a, dim3 grid, hipStream_t s) {
+    if (a.kind == 0) launch_map_mk<T, FUSED, VW, 0>(a, grid, s);
+    else if (a.kind == 1) launch_map_mk<T, FUSED, VW, 1>(a, grid, s);
+    else launch_map_mk<T, FUSED, VW, 2>(a, grid, s);
+}
+
 template <typename T>
 hipError_t launch_map_t(const KMap &a, int cus, hipStream_t s) {
     constexpr int VW = 16 / sizeof(T);
@@ -140,10 +180,10 @@ hipError_t launch_map_t(const KMap &a, int cus, hipStream_t s) {
     const uint64_t cap = (uint64_t)cus * 8;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    const dim3 grid((uint32_t)blocks), block(kBlock);
-    if (a.src.fused) hipLaunchKernelGGL((k_map<T, true, 1>), grid, block, 0, s, a);
-    else if (a.vec > 1) hipLaunchKernelGGL((k_map<T, false, VW>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_map<T, false, 1>), grid, block, 0, s, a);
+    const dim3 grid((uint32_t)blocks);
+    if (a.src.fused) launch_map_kind<T, true, 1>(a, grid, s);
+    else if (a.vec > 1) launch_map_kind<T, false, VW>(a, grid, s);
+    else launch_map_kind<T, false, 1>(a, grid, s);
     return hipGetLastError();
 }
 
