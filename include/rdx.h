@@ -3,8 +3,8 @@
  *
  * This is the boundary a Reductionist host (Rust, through `extern "C"`) binds to replace the
  * synchronous part of a request: `operation<T>()` in src/app.rs:163-183, i.e.
- *   filter_pipeline()            src/filter_pipeline.rs:19-34 (byte unshuffle; decompression is NOT on
- *                                the device, see RDX_E_UNSUPPORTED)
+ *   filter_pipeline()            src/filter_pipeline.rs:19-34 (gzip / zlib decompression, byte unshuffle;
+ *                                blosc2 is not on the device, see RDX_E_UNSUPPORTED)
  *   validate_raw_size()          src/app.rs:169-172 -> src/models.rs:214-239
  *   T::execute(&RequestData,..)  src/operation.rs:53-96 -> src/operations.rs (Count/Max/Min/Select/Sum)
  *   build_array + slicing        src/array.rs:18-208 (byte-order swap, hyperslab)
@@ -41,12 +41,32 @@ typedef enum rdx_status {
     RDX_E_SHUFFLE_LENGTH = 6,      /* shuffle.rs:21 assert_eq!(len % element_size, 0) — reference panics    */
     RDX_E_NAN_UNORDERED = 7,       /* operations.rs:181-183,355-357 NaN in min/max — reference panics with
                                       "unexpected undefined order error for min"                            */
-    RDX_E_UNSUPPORTED = 8,         /* compression != none (decompression stays on the CPU) / rank > 32     */
+    RDX_E_UNSUPPORTED = 8,         /* compression blosc2 (not on the device) / rank > 32                    */
     RDX_E_DEVICE = 9,              /* HIP runtime error                                                      */
     RDX_E_OUT_OF_MEMORY = 10,      /* device or pinned allocation failed                                     */
     RDX_E_BUFFER_TOO_SMALL = 11,   /* caller-provided output buffer smaller than rdx_plan() reported        */
-    RDX_E_NO_DEVICE = 12           /* no usable gfx950 device                                                */
+    RDX_E_NO_DEVICE = 12,          /* no usable gfx950 device                                                */
+    RDX_E_DECOMPRESSION = 13       /* compression.rs:18-82 gzip/zlib stream invalid: ActiveStorageError::
+                                      DecompressionFlate2 / DecompressionZune (HTTP 400, error.rs:247-249);
+                                      the rdx_inflate_error detail: rdx_inflate_last_error()            */
 } rdx_status;
+
+/* Why a gzip / zlib stream failed to decompress (RDX_E_DECOMPRESSION).  The reference's messages are
+ * reproduced by rdx_inflate_error_string where its tests pin them (compression.rs:166-190). */
+typedef enum rdx_inflate_error {
+    RDX_INFLATE_OK = 0,
+    RDX_INFLATE_GZIP_HEADER = 1,     /* "invalid gzip header" (flate2): bad magic or CM != 8             */
+    RDX_INFLATE_ZLIB_METHOD = 2,     /* "Unknown zlib compression method N" (zune-inflate): CM != 8      */
+    RDX_INFLATE_ZLIB_HEADER = 3,     /* CINFO > 7, FCHECK not a multiple of 31, or a preset dictionary  */
+    RDX_INFLATE_TRUNCATED = 4,       /* the input ends inside the header, a block or the trailer         */
+    RDX_INFLATE_BLOCK_TYPE = 5,      /* reserved DEFLATE block type 3                                    */
+    RDX_INFLATE_STORED_LENGTH = 6,   /* stored block with LEN != ~NLEN                                    */
+    RDX_INFLATE_CODE_LENGTHS = 7,    /* invalid dynamic-block code lengths / incomplete or over-full code */
+    RDX_INFLATE_BAD_SYMBOL = 8,      /* a bit pattern with no code, or a length/distance symbol >= 286/30 */
+    RDX_INFLATE_DISTANCE = 9,        /* back-reference before the start of the output                    */
+    RDX_INFLATE_CHECKSUM = 10,       /* gzip CRC-32 / ISIZE or zlib Adler-32 mismatch                    */
+    RDX_INFLATE_OUTPUT_OVERFLOW = 11 /* more output than the capacity given (retry with a larger one)    */
+} rdx_inflate_error;
 
 /* ---- request enums (src/models.rs) ------------------------------------------------------------ */
 typedef enum rdx_op { /* routes /v2/{count,max,min,select,sum}, src/app.rs:61-71 */
@@ -120,7 +140,8 @@ typedef struct rdx_request {
     const rdx_slice *selection;    /* ndim entries or NULL */
     const uint64_t *axes;          /* n_axes entries or NULL */
     uint32_t n_filters;
-    uint32_t compression;          /* rdx_compression; anything but NONE -> RDX_E_UNSUPPORTED */
+    uint32_t compression;          /* rdx_compression: GZIP/ZLIB decompressed on the device; BLOSC2 ->
+                                      RDX_E_UNSUPPORTED */
     const rdx_filter *filters;     /* n_filters entries, in REQUEST order (decoded in reverse) */
     rdx_missing missing;
     uint32_t has_size;             /* RequestData.size is Some(..): app.rs:169 skips validate_raw_size */
@@ -155,12 +176,16 @@ void rdx_context_destroy(rdx_context *ctx);
 /* models.rs:242-313 validate_request_data (+ missing validation, missing.rs:47-80, with typed values). */
 rdx_status rdx_validate_request(const rdx_request *req);
 /* Shape / dtype / sizes of the response for a chunk of chunk_len bytes; runs every check
- * operation<T>() would run before touching the data (app.rs:163-183, array.rs:18-63). */
+ * operation<T>() would run before touching the data (app.rs:163-183, array.rs:18-63).  For a
+ * compressed request chunk_len is the DECOMPRESSED length (the response depends on it). */
 rdx_status rdx_plan(const rdx_request *req, uint64_t chunk_len, rdx_response_info *info);
 /* TryFromDValue (dvalue.rs:43-83): JSON number -> dtype value bytes (out: 8 bytes). */
 rdx_status rdx_missing_from_i64(uint32_t dtype, int64_t v, void *out);
 rdx_status rdx_missing_from_u64(uint32_t dtype, uint64_t v, void *out);
 rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out);
+/* Message for an rdx_inflate_error, and the detail of this thread's last RDX_E_DECOMPRESSION. */
+const char *rdx_inflate_error_string(uint32_t code);
+uint32_t rdx_inflate_last_error(void);
 
 /* Page-locked host buffers: a host that downloads chunks straight into these (s3_client.rs:215-233
  * today copies into an 8-byte aligned Vec) lets rdx_execute DMA them without a staging copy, and
@@ -172,7 +197,8 @@ void rdx_host_free(rdx_context *ctx, void *p);
 /* ---- execution ------------------------------------------------------------------------------------ */
 /* Host-resident chunk in, host-resident response out (the drop-in for operation<T>()).
  * `chunk` is borrowed read-only; body/counts are caller-provided with capacities from rdx_plan.
- * Blocks until the response is in host memory. */
+ * Blocks until the response is in host memory.  A gzip/zlib chunk crosses PCIe compressed and is
+ * inflated on the device (k_inflate); info describes the response of the decompressed chunk. */
 rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req,
                        const void *chunk, uint64_t chunk_len,
                        void *body, uint64_t body_capacity,
@@ -187,6 +213,8 @@ typedef struct rdx_workspace rdx_workspace;
 rdx_status rdx_workspace_create(rdx_context *ctx, int device, rdx_workspace **out);
 void rdx_workspace_destroy(rdx_workspace *ws);
 
+/* A compressed request (gzip/zlib) is inflated into workspace scratch first; the call then waits on
+ * `stream` once for the decompressed length before launching the operation. */
 rdx_status rdx_execute_device(rdx_workspace *ws, const rdx_request *req,
                               const void *d_chunk, uint64_t chunk_len,
                               void *d_body, int64_t *d_counts, uint32_t *d_status,
@@ -201,6 +229,18 @@ rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req,
                                     uint64_t chunk_len,
                                     void *d_bodies, int64_t *d_counts, uint32_t *d_status,
                                     void *stream, rdx_response_info *info);
+
+/* compression::decompress (src/compression.rs:18-27, gzip and zlib) for a batch of n device-resident
+ * compressed streams, asynchronous on `stream`: stream i (h_in_ptrs[i] device pointer, h_in_lens[i]
+ * bytes; HOST arrays) is inflated into d_out + i*out_capacity (out_capacity a multiple of 16, d_out
+ * 16-byte aligned); d_out_lens[i] = bytes produced, d_errors[i] = rdx_inflate_error (device arrays).
+ * RDX_INFLATE_OUTPUT_OVERFLOW means the stream needs more than out_capacity: the caller retries that
+ * stream with a larger capacity.  rdx_execute / rdx_execute_device call this for a compressed
+ * request (then synchronise once to learn the decompressed length) before planning the operation. */
+rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, uint64_t n,
+                                       const void *const *h_in_ptrs, const uint64_t *h_in_lens,
+                                       void *d_out, uint64_t out_capacity,
+                                       uint64_t *d_out_lens, uint32_t *d_errors, void *stream);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,10 @@ def lib():
         L.oracle_shuffle.argtypes = [VP, U64, U64, VP]
         L.oracle_deshuffle.restype = C.c_int
         L.oracle_deshuffle.argtypes = [VP, U64, U64, VP]
+        L.oracle_decompress.restype = C.c_uint32
+        L.oracle_decompress.argtypes = [C.c_uint32, VP, U64, VP, U64, C.POINTER(C.c_uint64)]
+        L.oracle_inflate_last_error.restype = C.c_uint32
+        L.oracle_inflate_last_error.argtypes = []
         L.oracle_missing_convert.restype = C.c_int
         L.oracle_missing_convert.argtypes = [C.c_uint32, C.c_uint32, C.c_int64, C.c_uint64, C.c_double, VP]
         _LIB = L
@@ -95,3 +99,15 @@ def convert(dtype: str, value):
             return 5, b""
         st = lib().oracle_missing_convert(DTYPE_CODE[dtype], 1, 0, value, 0.0, out)
     return st, bytes(out)[: DTYPE_SIZE[dtype]]
+
+
+def decompress(compression: int, data: bytes, cap: int | None = None):
+    """compression.rs:18-27 restated (oracle_inflate.cpp): returns (rdx_inflate_error, bytes)."""
+    L = lib()
+    if cap is None:
+        cap = 4 * len(data) + 4096
+    out = (C.c_uint8 * max(1, cap))()
+    got = C.c_uint64(0)
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    e = L.oracle_decompress(compression, src, len(data), out, cap, C.byref(got))
+    return int(e), bytes(out)[: min(got.value, cap)]

@@ -35,6 +35,9 @@
 #include <type_traits>
 #include <vector>
 
+extern "C" uint32_t oracle_decompress(uint32_t compression, const uint8_t *in, uint64_t len, uint8_t *out,
+                                      uint64_t cap, uint64_t *out_len);  // oracle_inflate.cpp
+
 namespace {
 
 using i64 = int64_t;
@@ -576,13 +579,38 @@ void validate_raw_size(u64 raw_size, uint32_t dtype, const rdx_request &req) {
     }
 }
 
+thread_local uint32_t g_inflate_error = 0;
+
 // src/app.rs:163-183 operation<T>
 Response operation(const rdx_request &req, const uint8_t *chunk, u64 len) {
-    std::vector<uint8_t> data(chunk, chunk + len);
-    // filter_pipeline.rs:19-34: decompress (not supported), then filters in reverse
-    if (req.compression != RDX_COMPRESSION_NONE) throw OracleError{RDX_E_UNSUPPORTED};
+    std::vector<uint8_t> data;
+    // filter_pipeline.rs:19-34: decompress (compression.rs:18-27, oracle_inflate.cpp), then the
+    // filters in reverse
+    g_inflate_error = 0;
+    if (req.compression == RDX_COMPRESSION_GZIP || req.compression == RDX_COMPRESSION_ZLIB) {
+        u64 cap = 4 * len + 4096, got = 0;
+        for (;;) {
+            data.resize(cap);
+            const uint32_t e = oracle_decompress(req.compression, chunk, len, data.data(), cap, &got);
+            if (e == RDX_INFLATE_OUTPUT_OVERFLOW) {
+                cap *= 4;
+                continue;
+            }
+            if (e != RDX_INFLATE_OK) {
+                g_inflate_error = e;
+                throw OracleError{RDX_E_DECOMPRESSION};
+            }
+            data.resize(got);
+            break;
+        }
+    } else if (req.compression != RDX_COMPRESSION_NONE) {
+        throw OracleError{RDX_E_UNSUPPORTED};  // blosc2: no restatement (the blusc crate is un-vendored)
+    } else {
+        data.assign(chunk, chunk + len);
+    }
     for (uint32_t k = req.n_filters; k-- > 0;) data = deshuffle(data, req.filters[k].element_size);
-    if (!req.has_size) validate_raw_size(data.size(), req.dtype, req);
+    // app.rs:169-172: the raw size is validated when compressed or when `size` was not given
+    if (req.compression != RDX_COMPRESSION_NONE || !req.has_size) validate_raw_size(data.size(), req.dtype, req);
     switch (req.dtype) {
         case RDX_DTYPE_INT32: return execute_t<int32_t>(req, data);
         case RDX_DTYPE_INT64: return execute_t<int64_t>(req, data);
@@ -675,6 +703,8 @@ int oracle_execute(const rdx_request *req, const void *chunk, uint64_t len, void
         return RDX_E_OUT_OF_MEMORY;
     }
 }
+
+uint32_t oracle_inflate_last_error(void) { return g_inflate_error; }
 
 int oracle_validate_request(const rdx_request *req) {
     try {

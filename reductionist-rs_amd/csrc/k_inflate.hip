@@ -1,0 +1,668 @@
+// k_inflate — the decompression stage of the filter pipeline (src/filter_pipeline.rs:23-25 ->
+// src/compression.rs:18-82) on gfx950: gzip (flate2 GzDecoder: RFC 1952 member, CRC-32 + ISIZE
+// checked, trailing bytes ignored) and zlib (zune-inflate decode_zlib: RFC 1950, Adler-32 checked),
+// both RFC 1951 DEFLATE.
+//
+// A DEFLATE stream is one serial bit stream (block boundaries and symbol positions are only known
+// after decoding everything before them), so the device parallelism is ACROSS streams: one
+// wavefront per compressed chunk, a batch of chunks per launch.  Inside a wave:
+//   * the symbol decode is wave-uniform serial code: every lane holds the same 64-bit bit buffer and
+//     walks the same symbols (no divergence; the SIMD executes it once per wave);
+//   * the compressed bytes are staged 2 KiB at a time into an LDS ring by all 64 lanes (one global
+//     load round trip per 2 KiB of input, not per refill);
+//   * Huffman codes decode through LDS root tables (10 bits literal/length, 8 bits distance; the
+//     rare longer codes by the canonical bit-serial walk), rebuilt per block by all lanes with
+//     ballot/popcount ranking instead of zlib's serial table construction;
+//   * the output goes through a 32 KiB LDS ring that IS the DEFLATE window: a back-reference copies
+//     up to 64 bytes per step, one byte per lane (src = out - dist + (j mod dist) keeps every source
+//     in already-written history, so overlapping matches need no serial byte loop), and full 4 KiB
+//     units are flushed to HBM with 16-byte stores;
+//   * the CRC-32 / Adler-32 of each flushed unit is computed by all lanes over 64-byte slices and
+//     combined (GF(2) polynomial shift for CRC-32, weighted sums for Adler-32).
+// LDS ≈ 44 KiB per wave (one wave per workgroup): 3 streams resident per CU, 768 chip-wide.
+#include "rdx_device.hpp"
+#include "rdx_kernels.hpp"
+
+namespace rdx {
+namespace {
+
+constexpr uint32_t kWin = 32768, kWinMask = kWin - 1;      // output ring = DEFLATE window
+constexpr uint32_t kInBytes = 4096, kInWords = kInBytes / 4;  // input ring
+constexpr uint32_t kStage = 2048;                             // bytes staged per refill of the ring
+constexpr uint32_t kLitRoot = 10, kDistRoot = 8, kClRoot = 7;
+constexpr uint32_t kFlush = 4096;                             // output unit written to HBM
+
+struct __attribute__((aligned(16))) InflateLds {
+    uint8_t win[kWin];
+    uint32_t in[kInWords];
+    uint32_t lit[1u << kLitRoot];
+    uint32_t dist[1u << kDistRoot];
+    uint32_t cl[1u << kClRoot];
+    uint32_t crc_tab[256];
+    uint32_t x2n[32];            // x^(2^k) mod P (CRC-32 combine)
+    uint32_t lbase[29];          // base | extra << 16
+    uint32_t dbase[30];
+    uint16_t lsym[288], dsym[32], clsym[20];
+    uint16_t lcount[16], dcount[16], clcount[16];
+    uint16_t offs[16], next[16];
+    uint8_t lens[320];
+};
+
+// ---- CRC-32 (reflected 0xEDB88320) algebra, as in zlib's crc32_combine ---------------------------
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = b & 1 ? (b >> 1) ^ 0xedb88320u : b >> 1;
+    }
+    return p;
+}
+
+// x^(8n) mod P
+__device__ __forceinline__ uint32_t x8n(const InflateLds &L, uint64_t n) {
+    uint32_t p = 1u << 31;
+    uint32_t k = 3;
+    while (n) {
+        if (n & 1) p = multmodp(L.x2n[k & 31], p);
+        n >>= 1;
+        ++k;
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint32_t crc_combine(const InflateLds &L, uint32_t c1, uint32_t c2, uint64_t len2) {
+    return multmodp(x8n(L, len2), c1) ^ c2;
+}
+
+constexpr uint32_t kAdlerMod = 65521;
+
+struct KInflateArgs {
+    const uint8_t *const *in;  // device array of stream pointers
+    const uint64_t *in_len;    // device array of stream lengths
+    uint8_t *out;              // stream i -> out + i * cap
+    uint64_t cap;
+    uint64_t *out_len;
+    uint32_t *err;
+    uint32_t format;           // RDX_COMPRESSION_GZIP / ZLIB
+};
+
+struct Inflater {
+    InflateLds &L;
+    const uint32_t lane;
+    // input: the stream as dwords from its 4-byte aligned base; byte q of that aligned stream is
+    // byte q - skew of the chunk
+    const uint32_t *srcw;
+    uint64_t end;     // skew + length: first byte past the stream (aligned-stream coordinates)
+    uint64_t staged;  // aligned-stream bytes [.., staged) are in the ring
+    uint64_t pos;     // next byte to move into the bit buffer
+    uint64_t bb;      // bit buffer (LSB first)
+    uint32_t bc;      // valid bits in bb
+    // output
+    uint8_t *dst;
+    uint64_t cap, out, flushed;
+    // checksums of the flushed output
+    uint32_t crc, s1, s2;
+    bool gzip;
+    uint32_t err;
+
+    // ---- input -----------------------------------------------------------------------------------
+    __device__ __forceinline__ void stage() {  // stage [start, start + kStage) with start >= pos rounded down
+        uint64_t start = pos & ~(uint64_t)(kStage - 1);
+        if (start < staged) start = staged;
+        const uint64_t w0 = start / 4 + (uint64_t)lane * (kStage / 4 / 64);
+#pragma unroll
+        for (int k = 0; k < (int)(kStage / 4 / 64); ++k) {
+            const uint64_t w = w0 + k;
+            uint32_t v = 0;
+            if (w * 4 < end) {
+                v = gld<uint32_t>(srcw + w);
+                const uint64_t valid = end - w * 4;  // zero the bytes past the stream
+                if (valid < 4) v &= (1u << (8 * valid)) - 1;
+            }
+            L.in[w & (kInWords - 1)] = v;
+        }
+        staged = start + kStage;
+        __syncthreads();
+    }
+    __device__ __forceinline__ uint32_t word_at(uint64_t p) const {
+        const uint32_t i = (uint32_t)(p >> 2) & (kInWords - 1), sh = (uint32_t)(p & 3) * 8;
+        const uint32_t lo = L.in[i], hi = L.in[(i + 1) & (kInWords - 1)];
+        return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+    }
+    __device__ __forceinline__ uint32_t byte_at(uint64_t p) const {
+        return (L.in[(p >> 2) & (kInWords - 1)] >> ((p & 3) * 8)) & 0xffu;
+    }
+    // at least 33 valid bits afterwards (unless the input is exhausted -> err)
+    __device__ __forceinline__ void refill() {
+        if (bc <= 32) {
+            if (pos + 8 > staged) stage();
+            bb |= (uint64_t)word_at(pos) << bc;
+            pos += 4;
+            bc += 32;
+            if (pos > end + 8 && !err) err = RDX_INFLATE_TRUNCATED;  // decoding the zero padding
+        }
+    }
+    __device__ __forceinline__ uint32_t bits(uint32_t n) {  // n <= 32, bc >= n
+        const uint32_t v = (uint32_t)(bb & ((1ull << n) - 1));
+        bb >>= n;
+        bc -= n;
+        return v;
+    }
+    __device__ __forceinline__ uint32_t need(uint32_t n) {  // n <= 32
+        if (bc < n) refill();
+        return bits(n);
+    }
+    // bytes consumed so far (aligned-stream coordinates)
+    __device__ __forceinline__ uint64_t consumed() const { return pos - bc / 8; }
+    __device__ __forceinline__ void align() {
+        const uint32_t r = bc & 7;
+        bb >>= r;
+        bc -= r;
+    }
+    __device__ __forceinline__ uint32_t byte() {  // byte-aligned read
+        const uint32_t v = need(8);
+        if (consumed() > end && !err) err = RDX_INFLATE_TRUNCATED;
+        return v;
+    }
+
+    // ---- output ----------------------------------------------------------------------------------
+    // Write [flushed, flushed + n) of the ring to HBM (n <= kFlush) and fold it into the checksum.
+    __device__ __forceinline__ void flush(uint32_t n) {
+        __syncthreads();
+        const uint32_t base = (uint32_t)(flushed & kWinMask);
+        const uint32_t lo = lane * 64;  // this lane's 64-byte slice of the unit
+        const uint32_t cnt = lo >= n ? 0 : (n - lo < 64 ? n - lo : 64);
+        uint8_t *d = dst + flushed + lo;
+        uint32_t c = 0, a = 0, b = 0;  // slice crc, s1, s2
+        if (cnt == 64 && ((uintptr_t)d & 15) == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(&L.win[base + lo + 16 * k]);
+                gst<uint4>(d + 16 * k, v);
+            }
+        } else {
+            for (uint32_t k = 0; k < cnt; ++k) d[k] = L.win[(base + lo + k) & kWinMask];
+        }
+        if (gzip) {
+            c = 0xffffffffu;
+            for (uint32_t k = 0; k < cnt; ++k) c = L.crc_tab[(c ^ L.win[(base + lo + k) & kWinMask]) & 0xff] ^ (c >> 8);
+            c ^= 0xffffffffu;
+            // combine the 64 slice CRCs in lane order (tree; right part length = its valid bytes)
+            uint32_t len = cnt;
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                const uint32_t oc = (uint32_t)__shfl_xor((int)c, m, 64);
+                const uint32_t ol = (uint32_t)__shfl_xor((int)len, m, 64);
+                if ((lane & m) == 0) {
+                    c = ol ? crc_combine(L, c, oc, ol) : c;
+                    len += ol;
+                }
+            }
+            c = (uint32_t)__shfl((int)c, 0, 64);
+            crc = flushed == 0 ? c : crc_combine(L, crc, c, n);
+        } else {
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t v = L.win[(base + lo + k) & kWinMask];
+                a += v;
+                b += (cnt - k) * v;
+            }
+            // s2(unit) = sum over slices of s2_l + (bytes after slice l) * s1_l
+            const uint64_t after = n - (lo + cnt > n ? n : lo + cnt);
+            uint64_t t1 = a % kAdlerMod, t2 = (b + (after % kAdlerMod) * (a % kAdlerMod)) % kAdlerMod;
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                t1 += (uint64_t)__shfl_xor((long long)t1, m, 64);
+                t2 += (uint64_t)__shfl_xor((long long)t2, m, 64);
+            }
+            t1 %= kAdlerMod;
+            t2 %= kAdlerMod;
+            s2 = (uint32_t)((s2 + (uint64_t)(n % kAdlerMod) * s1 + t2) % kAdlerMod);
+            s1 = (uint32_t)((s1 + t1) % kAdlerMod);
+        }
+        flushed += n;
+        __syncthreads();
+    }
+    // Flushing happens at ONE place per loop (the top of the symbol loop / stored-copy loop), so the
+    // flush code is inlined once there instead of behind every literal and copy; between two checks
+    // at most one copy (<= 258 bytes) is added, so the unflushed tail stays < kFlush + 258 bytes and
+    // never reaches ring slots that still hold unflushed output.
+    __device__ __forceinline__ void flush_full() {
+        while (out - flushed >= kFlush) flush(kFlush);
+    }
+    __device__ __forceinline__ bool room(uint64_t n) {
+        if (out + n > cap) {
+            if (!err) err = RDX_INFLATE_OUTPUT_OVERFLOW;
+            return false;
+        }
+        return true;
+    }
+    __device__ __forceinline__ void literal(uint32_t v) {
+        if (!room(1)) return;
+        if (lane == 0) L.win[out & kWinMask] = (uint8_t)v;
+        ++out;
+    }
+    __device__ __forceinline__ void copy(uint32_t len, uint32_t dist) {
+        if (!room(len)) return;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t j0 = 0; j0 < len; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            if (j < len) {
+                const uint32_t m = dist >= len ? j : j % dist;
+                const uint8_t v = L.win[(uint32_t)(out - dist + m) & kWinMask];
+                L.win[(uint32_t)(out + j) & kWinMask] = v;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        out += len;
+    }
+
+    // ---- Huffman ---------------------------------------------------------------------------------
+    // Canonical code of n lengths -> root table (2^root entries: symbol | length << 16, 0 = longer
+    // code) + count[] / sym[] for the bit-serial walk.  Returns 0 complete, > 0 incomplete,
+    // < 0 over-subscribed; count[0] = number of unused symbols.
+    __device__ __forceinline__ int build(const uint8_t *lens, uint32_t n, uint32_t *tab, uint32_t root, uint16_t *count,
+                         uint16_t *sym) {
+        uint32_t cnt[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) cnt[l] = 0;
+        for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+            const uint32_t s = b0 + lane;
+            const uint32_t l = s < n ? lens[s] : 16;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) cnt[q] += (uint32_t)__popcll(__ballot(l == (uint32_t)q));
+        }
+        int left = 1;
+        bool over = false;
+        uint32_t offs[16], next[16];
+        offs[1] = 0;
+        next[0] = 0;
+        uint32_t code = 0;
+#pragma unroll
+        for (int l = 1; l < 16; ++l) {
+            left <<= 1;
+            left -= (int)cnt[l];
+            over |= left < 0;
+            if (l < 15) offs[l + 1] = offs[l] + cnt[l];
+            code = (code + (l == 1 ? 0 : cnt[l - 1])) << 1;
+            next[l] = code;
+        }
+        for (uint32_t i = lane; i < (1u << root); i += 64) tab[i] = 0;
+        if (lane == 0) {
+#pragma unroll
+            for (int l = 0; l < 16; ++l) {
+                count[l] = (uint16_t)cnt[l];
+                L.offs[l] = (uint16_t)(l ? offs[l] : 0);
+                L.next[l] = (uint16_t)(l ? next[l] : 0);
+            }
+        }
+        __syncthreads();
+        if (cnt[0] == n) return 0;  // no codes at all: complete by convention (puff)
+        if (over) return -1;
+        uint32_t run[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) run[l] = 0;
+        const uint64_t lt = (1ull << lane) - 1;
+        for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+            const uint32_t s = b0 + lane;
+            const uint32_t l = s < n ? lens[s] : 0;
+            uint32_t rank = 0;
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const uint64_t m = __ballot(l == (uint32_t)q);
+                if (l == (uint32_t)q) rank = run[q] + (uint32_t)__popcll(m & lt);
+                run[q] += (uint32_t)__popcll(m);
+            }
+            if (l) {
+                sym[L.offs[l] + rank] = (uint16_t)s;
+                if (l <= root) {
+                    const uint32_t c = L.next[l] + rank;
+                    const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
+                    for (uint32_t k = r; k < (1u << root); k += 1u << l) tab[k] = s | (l << 16);
+                }
+            }
+        }
+        __syncthreads();
+        return left;
+    }
+    // decode one symbol (needs >= 15 valid bits): root table, else the canonical bit-serial walk
+    __device__ __forceinline__ int decode(const uint32_t *tab, uint32_t root, const uint16_t *count, const uint16_t *sym) {
+        const uint32_t e = tab[(uint32_t)bb & ((1u << root) - 1)];
+        const uint32_t l = e >> 16;
+        if (l) {
+            bb >>= l;
+            bc -= l;
+            return (int)(e & 0xffff);
+        }
+        int code = 0, first = 0, index = 0;
+        for (int len = 1; len < 16; ++len) {
+            code |= (int)(bb & 1);
+            bb >>= 1;
+            --bc;
+            const int c = count[len];
+            if (code - c < first) return sym[index + (code - first)];
+            index += c;
+            first += c;
+            first <<= 1;
+            code <<= 1;
+        }
+        return -1;
+    }
+
+    // ---- blocks ------------------------------------------------------------------------------------
+    __device__ __forceinline__ void fixed_tables() {
+        for (uint32_t s = lane; s < 288 + 30; s += 64)
+            L.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+        __syncthreads();
+        build(L.lens, 288, L.lit, kLitRoot, L.lcount, L.lsym);
+        build(L.lens + 288, 30, L.dist, kDistRoot, L.dcount, L.dsym);
+    }
+
+    __device__ __forceinline__ void dynamic_tables() {
+        refill();
+        const uint32_t nlen = bits(5) + 257, ndist = bits(5) + 1, ncode = bits(4) + 4;
+        if (nlen > 286 || ndist > 30) {
+            err = RDX_INFLATE_CODE_LENGTHS;
+            return;
+        }
+        // 19 code-length code lengths, 3 bits each, in the permuted order of RFC 1951 §3.2.7
+        refill();
+        const uint32_t n1 = ncode < 10 ? ncode : 10;
+        const uint64_t v1 = bits(3 * n1);
+        refill();
+        const uint32_t n2 = ncode - n1;
+        const uint64_t v2 = n2 ? bits(3 * n2) : 0;
+        if (lane < 19) {
+            constexpr uint32_t kOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+            uint32_t ord = 0;
+#pragma unroll
+            for (int i = 0; i < 19; ++i)
+                if ((uint32_t)i == lane) ord = kOrder[i];
+            uint32_t v = 0;
+            if (lane < ncode) v = lane < 10 ? (uint32_t)(v1 >> (3 * lane)) & 7 : (uint32_t)(v2 >> (3 * (lane - 10))) & 7;
+            L.lens[ord] = (uint8_t)v;
+        }
+        __syncthreads();
+        if (build(L.lens, 19, L.cl, kClRoot, L.clcount, L.clsym) != 0) {  // complete code required
+            err = RDX_INFLATE_CODE_LENGTHS;
+            return;
+        }
+        // literal/length + distance code lengths (run-length coded)
+        const uint32_t total = nlen + ndist;
+        uint32_t idx = 0, prev = 0;
+        bool has_eob = false;
+        while (idx < total && !err) {
+            refill();
+            const uint32_t e = L.cl[(uint32_t)bb & ((1u << kClRoot) - 1)];
+            const uint32_t l = e >> 16, sym = e & 0xffff;
+            bb >>= l;
+            bc -= l;
+            if (sym < 16) {
+                if (lane == 0) L.lens[idx] = (uint8_t)sym;
+                if (idx == 256) has_eob = sym != 0;
+                prev = sym;
+                ++idx;
+                continue;
+            }
+            uint32_t rep, val = 0;
+            if (sym == 16) {
+                if (idx == 0) {
+                    err = RDX_INFLATE_CODE_LENGTHS;
+                    break;
+                }
+                val = prev;
+                rep = 3 + bits(2);
+            } else if (sym == 17) {
+                rep = 3 + bits(3);
+            } else {
+                rep = 11 + bits(7);
+            }
+            if (idx + rep > total) {
+                err = RDX_INFLATE_CODE_LENGTHS;
+                break;
+            }
+            if (lane < rep) L.lens[idx + lane] = (uint8_t)val;
+            if (lane + 64 < rep) L.lens[idx + lane + 64] = (uint8_t)val;
+            if (lane + 128 < rep) L.lens[idx + lane + 128] = (uint8_t)val;
+            if (idx <= 256 && 256 < idx + rep) has_eob = val != 0;
+            prev = val;
+            idx += rep;
+        }
+        __syncthreads();
+        if (err) return;
+        if (!has_eob) {
+            err = RDX_INFLATE_CODE_LENGTHS;
+            return;
+        }
+        int r = build(L.lens, nlen, L.lit, kLitRoot, L.lcount, L.lsym);
+        if (r < 0 || (r > 0 && nlen != (uint32_t)L.lcount[0] + L.lcount[1])) {
+            err = RDX_INFLATE_CODE_LENGTHS;
+            return;
+        }
+        r = build(L.lens + nlen, ndist, L.dist, kDistRoot, L.dcount, L.dsym);
+        if (r < 0 || (r > 0 && ndist != (uint32_t)L.dcount[0] + L.dcount[1])) err = RDX_INFLATE_CODE_LENGTHS;
+    }
+
+    __device__ __forceinline__ void codes() {
+        while (!err) {
+            flush_full();
+            refill();
+            const int sym = decode(L.lit, kLitRoot, L.lcount, L.lsym);
+            if (sym < 256) {
+                if (sym < 0) {
+                    err = RDX_INFLATE_BAD_SYMBOL;
+                    break;
+                }
+                literal((uint32_t)sym);
+                continue;
+            }
+            if (sym == 256) break;
+            const uint32_t ls = (uint32_t)sym - 257;
+            if (ls >= 29) {
+                err = RDX_INFLATE_BAD_SYMBOL;
+                break;
+            }
+            const uint32_t le = L.lbase[ls];
+            const uint32_t len = (le & 0xffff) + bits(le >> 16);
+            refill();
+            const int ds = decode(L.dist, kDistRoot, L.dcount, L.dsym);
+            if (ds < 0 || ds >= 30) {
+                err = RDX_INFLATE_BAD_SYMBOL;
+                break;
+            }
+            const uint32_t de = L.dbase[ds];
+            const uint32_t dist = (de & 0xffff) + bits(de >> 16);
+            if (dist > out) {
+                err = RDX_INFLATE_DISTANCE;
+                break;
+            }
+            copy(len, dist);
+        }
+    }
+
+    __device__ __forceinline__ void stored() {
+        align();
+        const uint32_t len = byte() | byte() << 8;
+        const uint32_t nlen = byte() | byte() << 8;
+        if (err) return;
+        if (len != (~nlen & 0xffff)) {
+            err = RDX_INFLATE_STORED_LENGTH;
+            return;
+        }
+        uint32_t left = len;
+        while (left && bc >= 8 && !err) {  // whole bytes still in the bit buffer (< 8)
+            literal(bits(8));
+            --left;
+        }
+        // the rest straight from the input ring, 64 bytes per step
+        while (left && !err) {
+            flush_full();
+            if (pos + 64 > staged) stage();
+            const uint32_t m = left < 64 ? left : 64;
+            if (pos + m > end) {
+                err = RDX_INFLATE_TRUNCATED;
+                break;
+            }
+            if (!room(m)) break;
+            if (lane < m) L.win[(uint32_t)(out + lane) & kWinMask] = (uint8_t)byte_at(pos + lane);
+            __builtin_amdgcn_wave_barrier();
+            out += m;
+            pos += m;
+            left -= m;
+        }
+    }
+
+    __device__ __forceinline__ void run() {
+        bool last = false;
+        bool fixed_ready = false;
+        while (!last && !err) {
+            flush_full();
+            refill();
+            last = bits(1);
+            const uint32_t type = bits(2);
+            if (type == 0) {
+                stored();
+            } else if (type == 1) {
+                if (!fixed_ready) fixed_tables();
+                fixed_ready = true;
+                codes();
+            } else if (type == 2) {
+                fixed_ready = false;
+                dynamic_tables();
+                if (!err) codes();
+            } else {
+                err = RDX_INFLATE_BLOCK_TYPE;
+            }
+        }
+    }
+};
+
+__global__ __launch_bounds__(64) void k_inflate(const KInflateArgs a) {
+    __shared__ InflateLds L;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x;
+    const uint8_t *src = gld<const uint8_t *>(a.in + i);
+    const uint64_t len = gld<uint64_t>(a.in_len + i);
+    // constant tables
+    if (lane < 29) {
+        constexpr uint16_t kB[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+        uint32_t b = 0;
+#pragma unroll
+        for (int k = 0; k < 29; ++k)
+            if ((uint32_t)k == lane) b = kB[k];
+        const uint32_t e = lane < 8 || lane == 28 ? 0 : (lane - 4) / 4;
+        L.lbase[lane] = b | e << 16;
+    }
+    if (lane < 30) {
+        const uint32_t e = lane < 2 ? 0 : lane / 2 - 1;
+        const uint32_t b = lane < 4 ? lane + 1 : (1u << e) * (2 + (lane & 1)) + 1;
+        L.dbase[lane] = b | e << 16;
+    }
+    for (uint32_t t = lane; t < 256; t += 64) {
+        uint32_t c = t;
+        for (int k = 0; k < 8; ++k) c = c & 1 ? 0xedb88320u ^ (c >> 1) : c >> 1;
+        L.crc_tab[t] = c;
+    }
+    if (lane == 0) {
+        uint32_t p = 1u << 30;  // x^1
+        for (int k = 0; k < 32; ++k) {
+            L.x2n[k] = p;
+            p = multmodp(p, p);
+        }
+    }
+    __syncthreads();
+
+    const uint32_t skew = (uint32_t)((uintptr_t)src & 3);
+    Inflater f{L, lane};
+    f.srcw = reinterpret_cast<const uint32_t *>(src - skew);
+    f.end = skew + len;
+    f.staged = 0;
+    f.pos = skew;
+    f.bb = 0;
+    f.bc = 0;
+    f.dst = a.out + (uint64_t)i * a.cap;
+    f.cap = a.cap;
+    f.out = f.flushed = 0;
+    f.crc = 0;
+    f.s1 = 0;
+    f.s2 = 0;
+    f.gzip = a.format == RDX_COMPRESSION_GZIP;
+    f.err = 0;
+    f.stage();
+
+    if (f.gzip) {  // RFC 1952 member header (flate2 GzDecoder)
+        if (len < 2 || f.need(8) != 0x1f || f.need(8) != 0x8b) {
+            f.err = RDX_INFLATE_GZIP_HEADER;
+        } else if (f.byte() != 8) {
+            f.err = f.err ? f.err : RDX_INFLATE_GZIP_HEADER;
+        } else {
+            const uint32_t flg = f.byte();
+            for (int k = 0; k < 6; ++k) f.byte();  // MTIME, XFL, OS
+            if (flg & 4) {                         // FEXTRA
+                uint32_t xlen = f.byte();
+                xlen |= f.byte() << 8;
+                for (uint32_t k = 0; k < xlen && !f.err; ++k) f.byte();
+            }
+            if (flg & 8)
+                while (!f.err && f.byte() != 0) {}  // FNAME
+            if (flg & 16)
+                while (!f.err && f.byte() != 0) {}  // FCOMMENT
+            if (flg & 2) {                          // FHCRC (not verified, as the oracle)
+                f.byte();
+                f.byte();
+            }
+        }
+    } else {  // RFC 1950 (zune-inflate decode_zlib)
+        if (len < 2) {
+            f.err = RDX_INFLATE_TRUNCATED;
+        } else {
+            const uint32_t cmf = f.need(8), flg = f.need(8);
+            if ((cmf & 15) != 8) f.err = RDX_INFLATE_ZLIB_METHOD;
+            else if ((cmf >> 4) > 7 || (cmf * 256 + flg) % 31 != 0 || (flg & 0x20)) f.err = RDX_INFLATE_ZLIB_HEADER;
+        }
+    }
+    if (!f.err) {
+        f.run();
+        // the reference decoders read bit by bit and stop at the first bit past the input: any
+        // failure met after the stream's end is "input truncated" there (oracle_inflate.cpp BitIn)
+        if (f.err && f.pos * 8 - f.bc > f.end * 8) f.err = RDX_INFLATE_TRUNCATED;
+    }
+    if (!f.err) {
+        f.flush_full();
+        if (f.out > f.flushed) f.flush((uint32_t)(f.out - f.flushed));
+    }
+    if (!f.err) {  // trailer
+        f.align();
+        if (f.gzip) {
+            uint32_t crc = 0, isize = 0;
+            for (int k = 0; k < 4; ++k) crc |= f.byte() << (8 * k);
+            for (int k = 0; k < 4; ++k) isize |= f.byte() << (8 * k);
+            if (!f.err && (crc != f.crc || isize != (uint32_t)f.out)) f.err = RDX_INFLATE_CHECKSUM;
+        } else {
+            uint32_t ad = 0;
+            for (int k = 0; k < 4; ++k) ad = ad << 8 | f.byte();
+            const uint32_t want = (uint32_t)((f.s2 + f.out % kAdlerMod) % kAdlerMod) << 16 | (f.s1 + 1) % kAdlerMod;
+            if (!f.err && ad != want) f.err = RDX_INFLATE_CHECKSUM;
+        }
+    }
+    if (lane == 0) {
+        a.out_len[i] = f.out;
+        a.err[i] = f.err;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uint64_t *d_in_len, uint64_t n,
+                          uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    KInflateArgs a{d_in, d_in_len, d_out, cap, d_out_len, d_err, format};
+    hipLaunchKernelGGL(k_inflate, dim3((uint32_t)n), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace rdx

@@ -17,6 +17,9 @@ hipError_t launch_all_strided(uint32_t dtype, uint32_t op, const KAllStrided &a,
 hipError_t launch_axis(uint32_t dtype, uint32_t op, const KAxis &a, int cus, hipStream_t s);
 hipError_t launch_map(uint32_t dtype, const KMap &a, int cus, hipStream_t s);
 hipError_t launch_unshuffle(const uint8_t *in, uint8_t *out, uint64_t len, uint64_t es, int cus, hipStream_t s);
+// k_inflate.hip: gzip / zlib streams (format = rdx_compression), one wavefront per stream
+hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uint64_t *d_in_len, uint64_t n,
+                          uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s);
 
 #define RDX_DECLARE_DTYPE(tn)                                                                                  \
     hipError_t launch_all_contig_##tn(uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s);    \

@@ -304,14 +304,15 @@ rdx_status make_plan(const rdx_request &req, uint64_t len, ExecPlan &p) {
     p.is_float = is_float_dtype(req.dtype);
     p.need_rank = p.is_float && (req.op == RDX_OP_MIN || req.op == RDX_OP_MAX);
 
-    // filter_pipeline.rs:24-32 — decompression is not on the device.
-    if (req.compression != RDX_COMPRESSION_NONE) return RDX_E_UNSUPPORTED;
+    // filter_pipeline.rs:23-25 — gzip/zlib are inflated on the device BEFORE planning (k_inflate.hip), so
+    // `len` is the decompressed length here; blosc2 is not on the device.
+    if (req.compression == RDX_COMPRESSION_BLOSC2) return RDX_E_UNSUPPORTED;
     for (uint32_t k = 0; k < req.n_filters; ++k) {
         const uint64_t es = req.filters[k].element_size;
         if (es == 0 || len % es != 0) return RDX_E_SHUFFLE_LENGTH;  // shuffle.rs:21 assert
     }
-    // app.rs:169-172
-    if (!req.has_size && (st = validate_raw_size(len, req))) return st;
+    // app.rs:169-172: validated when compressed (the raw size is only known now) or when `size` is absent
+    if ((req.compression != RDX_COMPRESSION_NONE || !req.has_size) && (st = validate_raw_size(len, req))) return st;
     // array.rs:18-27 from_bytes (alignment is moot: the chunk is copied to / lives in HBM)
     if (len % p.esz != 0) return RDX_E_FROM_BYTES;
     const uint64_t n = len / p.esz;

@@ -84,6 +84,15 @@ struct rdx_workspace {
     DevBuf<uint8_t> body;
     DevBuf<int64_t> counts;
     DevBuf<uint32_t> status;
+    // decompression (k_inflate): stream tables, the decompressed chunk of a compressed request, and a
+    // pinned readback of its length + error
+    DevBuf<const uint8_t *> zptrs;
+    DevBuf<uint64_t> zlens;
+    DevBuf<uint64_t> zout_len;
+    DevBuf<uint32_t> zerr;
+    DevBuf<uint8_t> raw;
+    std::vector<uint8_t> last_zptrs, last_zlens;
+    uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
 };
 
 struct rdx_context {
@@ -362,6 +371,70 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
     return RDX_E_INVALID_ARGUMENT;
 }
 
+thread_local uint32_t g_inflate_error = RDX_INFLATE_OK;
+
+// compression::decompress (compression.rs:18-27) of n device-resident streams into d_out (stream i at
+// d_out + i*cap), asynchronous on s.
+rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n, const uint8_t *const *h_ptrs,
+                             const uint64_t *h_lens, uint8_t *d_out, uint64_t cap, uint64_t *d_out_len,
+                             uint32_t *d_err, hipStream_t s) {
+    rdx_status st;
+    if ((st = ensure(ws, ws->zptrs, n, s))) return st;
+    if ((st = ensure(ws, ws->zlens, n, s))) return st;
+    if ((st = upload(ws, (void *)ws->zptrs.p, h_ptrs, n * sizeof(void *), ws->last_zptrs, s))) return st;
+    if ((st = upload(ws, ws->zlens.p, h_lens, n * sizeof(uint64_t), ws->last_zlens, s))) return st;
+    RDX_HIP(launch_inflate(compression, ws->zptrs.p, ws->zlens.p, n, d_out, cap, d_out_len, d_err, s));
+    return RDX_OK;
+}
+
+// A compressed request's chunk -> ws->raw (its decompressed bytes), synchronously: the operation's
+// plan depends on the decompressed length.  The capacity starts at the size the request implies
+// (shape x dtype size, else the gzip ISIZE hint, else 4x the compressed length) and grows on
+// RDX_INFLATE_OUTPUT_OVERFLOW, so a stream longer than the shape implies still decodes to its end and
+// meets validate_raw_size (app.rs:169-172) exactly like the reference.
+rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const uint8_t *d_src, uint64_t len,
+                              uint64_t size_hint, hipStream_t s, uint64_t *raw_len) {
+    g_inflate_error = RDX_INFLATE_OK;
+    if (req.compression == RDX_COMPRESSION_BLOSC2) return RDX_E_UNSUPPORTED;
+    if (req.compression != RDX_COMPRESSION_GZIP && req.compression != RDX_COMPRESSION_ZLIB)
+        return RDX_E_INVALID_ARGUMENT;
+    uint64_t cap = size_hint;
+    if (req.ndim && req.shape && req.dtype <= RDX_DTYPE_FLOAT64) {
+        uint64_t e = (req.dtype == RDX_DTYPE_INT32 || req.dtype == RDX_DTYPE_UINT32 || req.dtype == RDX_DTYPE_FLOAT32) ? 4 : 8;
+        bool ovf = false;
+        for (uint32_t k = 0; k < req.ndim; ++k) ovf |= __builtin_mul_overflow(e, req.shape[k], &e);
+        if (!ovf) cap = e;
+    }
+    if (cap == 0) cap = 4 * len + 4096;
+    rdx_status st;
+    if ((st = ensure(ws, ws->zout_len, 1, s))) return st;
+    if ((st = ensure(ws, ws->zerr, 1, s))) return st;
+    if (!ws->zback) RDX_HIP(hipHostMalloc((void **)&ws->zback, 2 * sizeof(uint64_t), hipHostMallocDefault));
+    for (;;) {
+        cap = (std::max<uint64_t>(cap, 16) + 15) / 16 * 16;
+        if ((st = ensure(ws, ws->raw, cap, s))) return st;
+        const uint8_t *ptrs[1] = {d_src};
+        const uint64_t lens[1] = {len};
+        if ((st = decompress_launch(ws, req.compression, 1, ptrs, lens, ws->raw.p, cap, ws->zout_len.p, ws->zerr.p, s)))
+            return st;
+        RDX_HIP(hipMemcpyAsync(&ws->zback[0], ws->zout_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipMemcpyAsync(&ws->zback[1], ws->zerr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipStreamSynchronize(s));
+        const uint32_t e = (uint32_t)ws->zback[1];
+        if (e == RDX_INFLATE_OUTPUT_OVERFLOW) {
+            if (cap >= (1ull << 40)) return RDX_E_OUT_OF_MEMORY;
+            cap *= 4;
+            continue;
+        }
+        if (e != RDX_INFLATE_OK) {
+            g_inflate_error = e;
+            return RDX_E_DECOMPRESSION;
+        }
+        *raw_len = ws->zback[0];
+        return RDX_OK;
+    }
+}
+
 rdx_status create_workspace(int device, rdx_workspace **out) {
     RDX_HIP(hipSetDevice(device));
     auto *ws = new (std::nothrow) rdx_workspace();
@@ -396,6 +469,12 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->body.p);
     fr(ws->counts.p);
     fr(ws->status.p);
+    fr((void *)ws->zptrs.p);
+    fr(ws->zlens.p);
+    fr(ws->zout_len.p);
+    fr(ws->zerr.p);
+    fr(ws->raw.p);
+    if (ws->zback) (void)hipHostFree(ws->zback);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
     if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
@@ -430,9 +509,30 @@ const char *rdx_status_string(rdx_status s) {
         case RDX_E_OUT_OF_MEMORY: return "out of memory";
         case RDX_E_BUFFER_TOO_SMALL: return "output buffer too small";
         case RDX_E_NO_DEVICE: return "no gfx950 device";
+        case RDX_E_DECOMPRESSION: return "decompression failed";
     }
     return "unknown status";
 }
+
+const char *rdx_inflate_error_string(uint32_t code) {
+    switch (code) {
+        case RDX_INFLATE_OK: return "ok";
+        case RDX_INFLATE_GZIP_HEADER: return "invalid gzip header";                  // compression.rs:173
+        case RDX_INFLATE_ZLIB_METHOD: return "Unknown zlib compression method";      // compression.rs:185 (+ " N")
+        case RDX_INFLATE_ZLIB_HEADER: return "invalid zlib header";
+        case RDX_INFLATE_TRUNCATED: return "unexpected end of compressed data";
+        case RDX_INFLATE_BLOCK_TYPE: return "invalid deflate block type";
+        case RDX_INFLATE_STORED_LENGTH: return "invalid stored block lengths";
+        case RDX_INFLATE_CODE_LENGTHS: return "invalid deflate code lengths";
+        case RDX_INFLATE_BAD_SYMBOL: return "invalid deflate code";
+        case RDX_INFLATE_DISTANCE: return "invalid distance too far back";
+        case RDX_INFLATE_CHECKSUM: return "checksum mismatch";
+        case RDX_INFLATE_OUTPUT_OVERFLOW: return "decompressed data larger than the output buffer";
+    }
+    return "unknown decompression error";
+}
+
+uint32_t rdx_inflate_last_error(void) { return g_inflate_error; }
 
 int rdx_device_count(void) {
     int n = 0;
@@ -565,21 +665,33 @@ rdx_status rdx_execute_device(rdx_workspace *ws, const rdx_request *req, const v
                               void *d_body, int64_t *d_counts, uint32_t *d_status, void *stream,
                               rdx_response_info *info) {
     if (!ws || !req) return RDX_E_INVALID_ARGUMENT;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint8_t *src = static_cast<const uint8_t *>(d_chunk);
+    rdx_status st;
+    if (req->compression != RDX_COMPRESSION_NONE) {  // filter_pipeline.rs:23-25, then plan on the raw size
+        if (!d_chunk && chunk_len) return RDX_E_INVALID_ARGUMENT;
+        RDX_HIP(hipSetDevice(ws->device));
+        uint64_t raw_len = 0;
+        if ((st = decompress_request(ws, *req, src, chunk_len, 0, s, &raw_len))) return st;
+        src = ws->raw.p;
+        chunk_len = raw_len;
+    }
     ExecPlan p;
-    rdx_status st = make_plan(*req, chunk_len, p);
-    if (st) return st;
+    if ((st = make_plan(*req, chunk_len, p))) return st;
     if (info) *info = p.info;
-    if ((!d_chunk && chunk_len) || (!d_body && p.info.body_bytes) || (!d_counts && p.info.n_counts))
+    if ((!src && chunk_len) || (!d_body && p.info.body_bytes) || (!d_counts && p.info.n_counts))
         return RDX_E_INVALID_ARGUMENT;
     RDX_HIP(hipSetDevice(ws->device));
-    return run_device(ws, p, static_cast<const uint8_t *>(d_chunk), nullptr, 1, chunk_len,
-                      static_cast<uint8_t *>(d_body), d_counts, d_status, static_cast<hipStream_t>(stream));
+    return run_device(ws, p, src, nullptr, 1, chunk_len, static_cast<uint8_t *>(d_body), d_counts, d_status, s);
 }
 
 rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req, uint64_t n_chunks,
                                     const void *const *h_chunk_ptrs, uint64_t chunk_len, void *d_bodies,
                                     int64_t *d_counts, uint32_t *d_status, void *stream, rdx_response_info *info) {
     if (!ws || !req || (n_chunks && !h_chunk_ptrs)) return RDX_E_INVALID_ARGUMENT;
+    // compressed chunks have per-chunk lengths: rdx_decompress_batch_device first, then this on the raw
+    // buffers
+    if (req->compression != RDX_COMPRESSION_NONE) return RDX_E_INVALID_ARGUMENT;
     ExecPlan p;
     rdx_status st = make_plan(*req, chunk_len, p);
     if (st) return st;
@@ -591,15 +703,37 @@ rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req, u
                       static_cast<uint8_t *>(d_bodies), d_counts, d_status, static_cast<hipStream_t>(stream));
 }
 
+rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, uint64_t n,
+                                       const void *const *h_in_ptrs, const uint64_t *h_in_lens, void *d_out,
+                                       uint64_t out_capacity, uint64_t *d_out_lens, uint32_t *d_errors, void *stream) {
+    if (compression == RDX_COMPRESSION_BLOSC2) return RDX_E_UNSUPPORTED;
+    if (!ws || (compression != RDX_COMPRESSION_GZIP && compression != RDX_COMPRESSION_ZLIB)) return RDX_E_INVALID_ARGUMENT;
+    if (n == 0) return RDX_OK;
+    if (!h_in_ptrs || !h_in_lens || !d_out || !d_out_lens || !d_errors || out_capacity % 16 ||
+        (uintptr_t)d_out % 16)
+        return RDX_E_INVALID_ARGUMENT;
+    for (uint64_t i = 0; i < n; ++i)
+        if (!h_in_ptrs[i] && h_in_lens[i]) return RDX_E_INVALID_ARGUMENT;
+    RDX_HIP(hipSetDevice(ws->device));
+    return decompress_launch(ws, compression, n, reinterpret_cast<const uint8_t *const *>(h_in_ptrs), h_in_lens,
+                             static_cast<uint8_t *>(d_out), out_capacity, d_out_lens, d_errors,
+                             static_cast<hipStream_t>(stream));
+}
+
 rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len, void *body,
                        uint64_t body_capacity, int64_t *counts, uint64_t counts_capacity, rdx_response_info *info) {
     if (!ctx || !req || !info || (!chunk && chunk_len)) return RDX_E_INVALID_ARGUMENT;
+    const bool compressed = req->compression != RDX_COMPRESSION_NONE;
     ExecPlan p;
-    rdx_status st = make_plan(*req, chunk_len, p);
-    if (st) return st;
-    *info = p.info;
-    if (body_capacity < p.info.body_bytes || counts_capacity < p.info.n_counts) return RDX_E_BUFFER_TOO_SMALL;
-    if ((!body && p.info.body_bytes) || (!counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
+    rdx_status st;
+    if (!compressed) {
+        if ((st = make_plan(*req, chunk_len, p))) return st;
+        *info = p.info;
+        if (body_capacity < p.info.body_bytes || counts_capacity < p.info.n_counts) return RDX_E_BUFFER_TOO_SMALL;
+        if ((!body && p.info.body_bytes) || (!counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
+    } else if (req->compression == RDX_COMPRESSION_BLOSC2) {
+        return RDX_E_UNSUPPORTED;
+    }
 
     // take a workspace (round-robin device, then any free workspace of it)
     rdx_workspace *ws = nullptr;
@@ -626,8 +760,25 @@ rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req, const void *chu
         if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
         if ((r = ensure(ws, ws->status, 1, s))) return r;
         if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
+        const uint8_t *src = ws->chunk.p;
+        uint64_t len = chunk_len;
+        if (compressed) {  // the chunk crossed PCIe compressed; inflate it in HBM, then plan on its size
+            uint64_t hint = 0;
+            if (req->compression == RDX_COMPRESSION_GZIP && chunk_len >= 18) {  // RFC 1952 ISIZE
+                const uint8_t *t = static_cast<const uint8_t *>(chunk) + chunk_len - 4;
+                hint = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+            }
+            if ((r = decompress_request(ws, *req, ws->chunk.p, chunk_len, hint, s, &len))) return r;
+            src = ws->raw.p;
+            if ((r = make_plan(*req, len, p))) return r;
+            *info = p.info;
+            if (body_capacity < p.info.body_bytes || counts_capacity < p.info.n_counts) return RDX_E_BUFFER_TOO_SMALL;
+            if ((!body && p.info.body_bytes) || (!counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
+            if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
+            if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
+        }
         RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
-        if ((r = run_device(ws, p, ws->chunk.p, nullptr, 1, chunk_len, ws->body.p, ws->counts.p, ws->status.p, s)))
+        if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
             return r;
         uint32_t status = 0;
         if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));

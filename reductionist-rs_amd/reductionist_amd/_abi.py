@@ -20,7 +20,12 @@ RDX_MAX_NDIM = 32
 # rdx_status
 OK, E_INVALID_ARGUMENT, E_REQUEST_VALIDATION, E_FROM_BYTES, E_SHAPE_INVALID, E_INCOMPATIBLE_MISSING, \
     E_SHUFFLE_LENGTH, E_NAN_UNORDERED, E_UNSUPPORTED, E_DEVICE, E_OUT_OF_MEMORY, E_BUFFER_TOO_SMALL, \
-    E_NO_DEVICE = range(13)
+    E_NO_DEVICE, E_DECOMPRESSION = range(14)
+
+# rdx_inflate_error (detail of E_DECOMPRESSION)
+INFLATE_OK, INFLATE_GZIP_HEADER, INFLATE_ZLIB_METHOD, INFLATE_ZLIB_HEADER, INFLATE_TRUNCATED, \
+    INFLATE_BLOCK_TYPE, INFLATE_STORED_LENGTH, INFLATE_CODE_LENGTHS, INFLATE_BAD_SYMBOL, INFLATE_DISTANCE, \
+    INFLATE_CHECKSUM, INFLATE_OUTPUT_OVERFLOW = range(12)
 
 OPS = {"count": 0, "max": 1, "min": 2, "select": 3, "sum": 4}
 DTYPES = {"int32": 0, "int64": 1, "uint32": 2, "uint64": 3, "float32": 4, "float64": 5}
@@ -145,6 +150,9 @@ def _declare(lib):
         "rdx_workspace_destroy": (None, [VP]),
         "rdx_execute_device": (C.c_int, [VP, req_p, VP, U64, VP, VP, VP, VP, info_p]),
         "rdx_execute_batch_device": (C.c_int, [VP, req_p, U64, P(VP), U64, VP, VP, VP, VP, info_p]),
+        "rdx_inflate_error_string": (C.c_char_p, [C.c_uint32]),
+        "rdx_inflate_last_error": (C.c_uint32, []),
+        "rdx_decompress_batch_device": (C.c_int, [VP, C.c_uint32, U64, P(VP), P(U64), VP, U64, VP, VP, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -158,7 +166,8 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_context_destroy", "rdx_validate_request", "rdx_plan", "rdx_missing_from_i64",
             "rdx_missing_from_u64", "rdx_missing_from_f64", "rdx_execute", "rdx_host_alloc", "rdx_host_free",
             "rdx_workspace_create",
-            "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device"]
+            "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
+            "rdx_inflate_last_error", "rdx_decompress_batch_device"]
 
 
 def lib():
@@ -181,3 +190,7 @@ def lib():
 
 def status_string(code: int) -> str:
     return lib().rdx_status_string(code).decode()
+
+
+def inflate_error_string(code: int) -> str:
+    return lib().rdx_inflate_error_string(code).decode()

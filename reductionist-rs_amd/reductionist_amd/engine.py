@@ -40,12 +40,19 @@ class Engine:
     def execute_raw(self, creq: _abi.CRequest, data: bytes):
         """Host chunk in, (status, info, body, counts) out — no exception on kernel-side status."""
         info = _abi.rdx_response_info()
-        st = self.lib.rdx_plan(creq.ref, len(data), C.byref(info))
-        if st != _abi.OK:
-            return st, info, b"", []
+        src = C.c_char_p(bytes(data)) if len(data) else None
+        if creq.c.compression != _abi.COMPRESSION[None]:
+            # the response size depends on the DECOMPRESSED length: a first call with no output
+            # capacity decompresses on the device and reports it (RDX_E_BUFFER_TOO_SMALL + info)
+            st = self.lib.rdx_execute(self.ctx, creq.ref, src, len(data), None, 0, None, 0, C.byref(info))
+            if st not in (_abi.OK, _abi.E_BUFFER_TOO_SMALL):
+                return st, info, b"", []
+        else:
+            st = self.lib.rdx_plan(creq.ref, len(data), C.byref(info))
+            if st != _abi.OK:
+                return st, info, b"", []
         body = (C.c_uint8 * max(1, info.body_bytes))()
         counts = (C.c_int64 * max(1, info.n_counts))()
-        src = C.c_char_p(bytes(data)) if len(data) else None
         st = self.lib.rdx_execute(self.ctx, creq.ref, src, len(data), body, info.body_bytes, counts,
                                   info.n_counts, C.byref(info))
         return st, info, bytes(body)[: info.body_bytes], [int(c) for c in counts[: info.n_counts]]
@@ -91,3 +98,15 @@ class Workspace:
                                                 C.c_void_p(d_status or 0), C.c_void_p(stream or 0),
                                                 C.byref(info)))
         return info
+
+    def decompress_batch_device(self, compression: str, d_streams: Sequence[int], lens: Sequence[int], d_out: int,
+                                out_capacity: int, d_out_lens: int, d_errors: int, stream: int | None) -> None:
+        """compression::decompress (compression.rs:18-27) of device-resident gzip/zlib streams:
+        stream i -> d_out + i*out_capacity, its length -> d_out_lens[i] (u64), rdx_inflate_error ->
+        d_errors[i] (u32).  Asynchronous on `stream`."""
+        n = len(d_streams)
+        ptrs = (C.c_void_p * max(1, n))(*d_streams)
+        ls = (C.c_uint64 * max(1, n))(*lens)
+        check(self.lib.rdx_decompress_batch_device(self.ws, _abi.COMPRESSION[compression], n, ptrs, ls,
+                                                   C.c_void_p(d_out), out_capacity, C.c_void_p(d_out_lens),
+                                                   C.c_void_p(d_errors), C.c_void_p(stream or 0)))

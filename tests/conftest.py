@@ -18,3 +18,11 @@ def engine():
     """The product engine.  No CPU fallback: constructing it without a device raises."""
     from reductionist_amd import Engine
     return Engine()
+
+
+@pytest.fixture(scope="session")
+def workspace(engine):
+    """A device-resident-path workspace (rdx_workspace) of the session engine."""
+    ws = engine.workspace(0)
+    yield ws
+    ws.close()

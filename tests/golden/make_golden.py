@@ -77,11 +77,45 @@ op("filter_pipeline_noop", "src/filter_pipeline.rs:61-67", "select", raw([1, 2, 
    ok(raw([1, 2, 3, 4]), "uint32", [1], [1]), dtype="uint32")
 op("filter_pipeline_shuffle", "src/filter_pipeline.rs:80-88", "select", raw(shuf4),
    ok(raw(one_to_8), "uint32", [2], [2]), dtype="uint32", filters=[{"id": "shuffle", "element_size": 4}])
-op("filter_pipeline_shuffle_x2 (zlib layer removed: decompression is host-side)",
-   "src/filter_pipeline.rs:104-120", "select", raw(shuf4_2), ok(raw(one_to_8), "uint32", [2], [2]),
-   dtype="uint32", filters=[{"id": "shuffle", "element_size": 4}, {"id": "shuffle", "element_size": 2}])
-op("filter_pipeline_gzip -> compression is not on the device", "src/filter_pipeline.rs:70-77", "select",
-   raw([1, 2, 3, 4]), err("E_UNSUPPORTED"), dtype="uint32", compression="gzip", size=4)
+# Compressed pipelines.  The reference compresses with flate2 Compression::fast() inside the test; any
+# valid DEFLATE encoder's stream of the same bytes must decode identically, so the streams below come
+# from CPython's zlib (level 1) and are FROZEN in kats.json as data (hex) — re-running this script
+# with another zlib may change the stream bytes, never the decoded result.
+import zlib  # noqa: E402
+
+
+def _gz(data):
+    c = zlib.compressobj(1, zlib.DEFLATED, 31)
+    return c.compress(bytes(data)) + c.flush()
+
+
+def _zl(data):
+    c = zlib.compressobj(1, zlib.DEFLATED, 15)
+    return c.compress(bytes(data)) + c.flush()
+
+
+op("filter_pipeline_gzip", "src/filter_pipeline.rs:70-77", "select", _gz([1, 2, 3, 4]).hex(),
+   ok(raw([1, 2, 3, 4]), "uint32", [1], [1]), dtype="uint32", compression="gzip", size=4)
+op("filter_pipeline_shuffle_zlib", "src/filter_pipeline.rs:91-101", "select", _zl(shuf4).hex(),
+   ok(raw(one_to_8), "uint32", [2], [2]), dtype="uint32", compression="zlib",
+   filters=[{"id": "shuffle", "element_size": 4}])
+op("filter_pipeline_shuffle_x2_zlib", "src/filter_pipeline.rs:104-120", "select", _zl(shuf4_2).hex(),
+   ok(raw(one_to_8), "uint32", [2], [2]), dtype="uint32", compression="zlib",
+   filters=[{"id": "shuffle", "element_size": 4}, {"id": "shuffle", "element_size": 2}])
+# compression.rs:136-162 decompress b"hello world": the API has no 8-bit dtype, so the 11 decoded
+# bytes are observed through validate_raw_size (11 is not a multiple of 4 -> 400) and, repeated 4
+# times (44 bytes), through Select as 11 u32 words
+op("decompress_gzip_hello_world -> raw size 11", "src/compression.rs:143-150 + src/app.rs:169-172", "count",
+   _gz(b"hello world").hex(), err("E_REQUEST_VALIDATION"), dtype="uint32", compression="gzip")
+op("decompress_zlib_hello_world_x4 (44 bytes = 11 x u32)", "src/compression.rs:152-159", "select",
+   _zl(b"hello world" * 4).hex(), ok((b"hello world" * 4).hex(), "uint32", [11], [11]), dtype="uint32",
+   compression="zlib")
+# compression.rs:166-190: b"invalid format" -> DecompressionFlate2 "invalid gzip header" /
+# DecompressionZune "Unknown zlib compression method 9" (both HTTP 400)
+op("decompress_invalid_gzip", "src/compression.rs:165-176", "count", b"invalid format".hex(),
+   {"status": "E_DECOMPRESSION", "inflate_error": "INFLATE_GZIP_HEADER"}, dtype="uint32", compression="gzip")
+op("decompress_invalid_zlib", "src/compression.rs:178-190", "count", b"invalid format".hex(),
+   {"status": "E_DECOMPRESSION", "inflate_error": "INFLATE_ZLIB_METHOD"}, dtype="uint32", compression="zlib")
 
 # ---- array.rs ----------------------------------------------------------------------------------------
 for dt, val, ref in (("uint32", 42, "216-221"), ("uint64", 2 ** 64 - 1, "224-229"), ("int32", -42, "232-237"),

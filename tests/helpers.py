@@ -15,7 +15,7 @@ GOLDEN = Path(__file__).resolve().parent / "golden" / "kats.json"
 STATUS = {"ok": _abi.OK, "E_REQUEST_VALIDATION": _abi.E_REQUEST_VALIDATION, "E_FROM_BYTES": _abi.E_FROM_BYTES,
           "E_SHAPE_INVALID": _abi.E_SHAPE_INVALID, "E_INCOMPATIBLE_MISSING": _abi.E_INCOMPATIBLE_MISSING,
           "E_SHUFFLE_LENGTH": _abi.E_SHUFFLE_LENGTH, "E_NAN_UNORDERED": _abi.E_NAN_UNORDERED,
-          "E_UNSUPPORTED": _abi.E_UNSUPPORTED}
+          "E_UNSUPPORTED": _abi.E_UNSUPPORTED, "E_DECOMPRESSION": _abi.E_DECOMPRESSION}
 
 NP = {"int32": np.int32, "int64": np.int64, "uint32": np.uint32, "uint64": np.uint64, "float32": np.float32,
       "float64": np.float64}
@@ -55,9 +55,11 @@ def product_convert(dtype, v):
         return _abi.E_INCOMPATIBLE_MISSING, b""
 
 
-def check_kat_result(kat, st, info, body, counts):
+def check_kat_result(kat, st, info, body, counts, inflate_error=None):
     exp = kat["expect"]
     assert st == STATUS[exp["status"]], (kat["name"], st, exp)
+    if "inflate_error" in exp and inflate_error is not None:
+        assert inflate_error == getattr(_abi, exp["inflate_error"]), (kat["name"], inflate_error)
     if exp["status"] != "ok":
         return
     assert body.hex() == exp["body"], (kat["name"], body.hex(), exp["body"])

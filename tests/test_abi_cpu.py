@@ -61,7 +61,7 @@ def test_plan_matches_oracle_random():
 def test_plan_error_order_matches_oracle():
     """operation<T>() raises its first error in a fixed order (app.rs:163-183)."""
     cases = [
-        ("sum", {"dtype": "int32", "compression": "zlib", "size": 8}, 8, _abi.E_UNSUPPORTED),
+        ("sum", {"dtype": "int32", "compression": "blosc2", "size": 8}, 8, _abi.E_UNSUPPORTED),
         ("sum", {"dtype": "int32", "filters": [{"id": "shuffle", "element_size": 3}]}, 8, _abi.E_SHUFFLE_LENGTH),
         ("sum", {"dtype": "int32", "filters": [{"id": "shuffle", "element_size": 0}]}, 8, _abi.E_SHUFFLE_LENGTH),
         ("sum", {"dtype": "int32"}, 6, _abi.E_REQUEST_VALIDATION),              # validate_raw_size
@@ -78,6 +78,12 @@ def test_plan_error_order_matches_oracle():
         info = _abi.rdx_response_info()
         assert ost == exp, (req, ost)
         assert lib.rdx_plan(creq.ref, n, C.byref(info)) == exp, req
+    # a compressed request is decompressed first (filter_pipeline.rs:23-25): 8 zero bytes are not a
+    # zlib stream; rdx_plan takes the DECOMPRESSED length and plans it like an uncompressed chunk
+    creq = make_request("sum", {"dtype": "int32", "compression": "zlib", "size": 8}, oracle.convert)
+    assert oracle.execute(creq, bytes(8))[0] == _abi.E_DECOMPRESSION
+    assert lib.rdx_plan(creq.ref, 8, C.byref(_abi.rdx_response_info())) == 0
+    assert lib.rdx_plan(creq.ref, 6, C.byref(_abi.rdx_response_info())) == _abi.E_REQUEST_VALIDATION
 
 
 def _random_validation_case(rng):

@@ -54,7 +54,7 @@ def assert_parity(engine, op, req, data):
 def test_reference_kats_on_device(engine, kat):
     creq = make_request(kat["op"], kat["request"], product_convert)
     st, info, body, counts = engine.execute_raw(creq, bytes.fromhex(kat["data"]))
-    check_kat_result(kat, st, info, body, counts)
+    check_kat_result(kat, st, info, body, counts, _abi.lib().rdx_inflate_last_error())
 
 
 @pytest.mark.parametrize("seed", range(8))
