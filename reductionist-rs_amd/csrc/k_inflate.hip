@@ -26,27 +26,77 @@
 namespace rdx {
 namespace {
 
-constexpr uint32_t kWin = 32768, kWinMask = kWin - 1;      // output ring = DEFLATE window
-constexpr uint32_t kInBytes = 4096, kInWords = kInBytes / 4;  // input ring
-constexpr uint32_t kStage = 2048;                             // bytes staged per refill of the ring
+#ifndef RDX_INFLATE_RING
+#define RDX_INFLATE_RING 8192
+#endif
+constexpr uint32_t kWaves = 4;                               // streams (wavefronts) per workgroup
+constexpr uint32_t kWin = RDX_INFLATE_RING, kWinMask = kWin - 1;  // LDS ring: the recent window
+constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4;  // input ring
+constexpr uint32_t kStage = 1024;                             // bytes staged per refill of the ring
 constexpr uint32_t kLitRoot = 10, kDistRoot = 8, kClRoot = 7;
-constexpr uint32_t kFlush = 4096;                             // output unit written to HBM
+constexpr uint32_t kFlush = kWin / 4;                         // output unit written to HBM
+static_assert(kFlush + 516 <= kWin, "the unflushed tail plus one copy must fit the ring");
 
+// Per-stream LDS (one per wave).  The DEFLATE window is 32 KiB but the ring keeps only the last kWin
+// bytes: a back-reference farther than that reads the already-flushed output in HBM (L2-hot).  The
+// small ring is what lets 3 workgroups x 4 waves share a CU (12 streams per CU, 3 per SIMD) instead
+// of 1 wave per CU-quarter with a 32 KiB window, so the serial decode chains of different streams
+// hide each other's LDS latency.
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t win[kWin];
     uint32_t in[kInWords];
     uint32_t lit[1u << kLitRoot];
     uint32_t dist[1u << kDistRoot];
     uint32_t cl[1u << kClRoot];
-    uint32_t crc_tab[256];
-    uint32_t x2n[32];            // x^(2^k) mod P (CRC-32 combine)
-    uint32_t lbase[29];          // base | extra << 16
-    uint32_t dbase[30];
     uint16_t lsym[288], dsym[32], clsym[20];
     uint16_t lcount[16], dcount[16], clcount[16];
     uint16_t offs[16], next[16];
     uint8_t lens[320];
 };
+
+// Read-only tables shared by the workgroup's streams.
+struct InflateShared {
+    uint32_t crc_tab[256];
+    uint32_t x2n[32];            // x^(2^k) mod P (CRC-32 combine)
+    uint32_t lbase[29];          // base | extra << 16
+    uint32_t dbase[30];
+};
+
+// The decode state is wave-uniform: values read from LDS by every lane are made scalar with
+// readfirstlane, so the bit buffer, positions and symbol dispatch live in SGPRs and branch on SCC
+// (no exec-mask juggling on the serial path).
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+    return (uint64_t)rfl((uint32_t)(x >> 32)) << 32 | rfl((uint32_t)x);
+}
+
+// Decode-table entry: value (literal byte / length or distance base) in bits 0-15, code length in
+// 16-19 (0 = code longer than the root: bit-serial walk), extra bits in 20-23, type in 24-25
+// (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol).
+constexpr uint32_t kTypeLen = 1u << 24, kTypeEob = 2u << 24, kTypeBad = 3u << 24;
+
+// Phase counters for tools/probe_inflate.hip (RDX_INFLATE_PROF); compiled out of the product.
+#ifdef RDX_INFLATE_PROF
+enum { P_LIT, P_MATCH, P_MATCH_BYTES, P_FAR, P_SLOW, P_BLOCKS, P_STAGE, P_FLUSH, P_T_COPY, P_T_FLUSH, P_T_TABLES,
+       P_T_TOTAL, P_N };
+__device__ unsigned long long g_prof[P_N];
+#define PROF_ADD(k, v) (prof[k] += (v))
+#define PROF_T0() const uint64_t _t0 = __builtin_readcyclecounter()
+#define PROF_T1(k) (prof[k] += __builtin_readcyclecounter() - _t0)
+#else
+#define PROF_ADD(k, v) ((void)0)
+#define PROF_T0() ((void)0)
+#define PROF_T1(k) ((void)0)
+#endif
+
+// LDS ordering inside ONE wavefront: its LDS instructions execute in order, so a compiler barrier is
+// all a lane needs to read what another lane of the same wave wrote (the workgroup's other waves
+// decode other streams and never touch this wave's LDS).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ---- CRC-32 (reflected 0xEDB88320) algebra, as in zlib's crc32_combine ---------------------------
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
@@ -63,7 +113,7 @@ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
 }
 
 // x^(8n) mod P
-__device__ __forceinline__ uint32_t x8n(const InflateLds &L, uint64_t n) {
+__device__ __forceinline__ uint32_t x8n(const InflateShared &L, uint64_t n) {
     uint32_t p = 1u << 31;
     uint32_t k = 3;
     while (n) {
@@ -74,7 +124,7 @@ __device__ __forceinline__ uint32_t x8n(const InflateLds &L, uint64_t n) {
     return p;
 }
 
-__device__ __forceinline__ uint32_t crc_combine(const InflateLds &L, uint32_t c1, uint32_t c2, uint64_t len2) {
+__device__ __forceinline__ uint32_t crc_combine(const InflateShared &L, uint32_t c1, uint32_t c2, uint64_t len2) {
     return multmodp(x8n(L, len2), c1) ^ c2;
 }
 
@@ -88,10 +138,12 @@ struct KInflateArgs {
     uint64_t *out_len;
     uint32_t *err;
     uint32_t format;           // RDX_COMPRESSION_GZIP / ZLIB
+    uint32_t n;                // streams
 };
 
 struct Inflater {
     InflateLds &L;
+    const InflateShared &S;
     const uint32_t lane;
     // input: the stream as dwords from its 4-byte aligned base; byte q of that aligned stream is
     // byte q - skew of the chunk
@@ -108,9 +160,13 @@ struct Inflater {
     uint32_t crc, s1, s2;
     bool gzip;
     uint32_t err;
+#ifdef RDX_INFLATE_PROF
+    uint64_t prof[P_N];
+#endif
 
     // ---- input -----------------------------------------------------------------------------------
     __device__ __forceinline__ void stage() {  // stage [start, start + kStage) with start >= pos rounded down
+        PROF_ADD(P_STAGE, 1);
         uint64_t start = pos & ~(uint64_t)(kStage - 1);
         if (start < staged) start = staged;
         const uint64_t w0 = start / 4 + (uint64_t)lane * (kStage / 4 / 64);
@@ -126,11 +182,11 @@ struct Inflater {
             L.in[w & (kInWords - 1)] = v;
         }
         staged = start + kStage;
-        __syncthreads();
+        wave_sync();
     }
     __device__ __forceinline__ uint32_t word_at(uint64_t p) const {
         const uint32_t i = (uint32_t)(p >> 2) & (kInWords - 1), sh = (uint32_t)(p & 3) * 8;
-        const uint32_t lo = L.in[i], hi = L.in[(i + 1) & (kInWords - 1)];
+        const uint32_t lo = rfl(L.in[i]), hi = rfl(L.in[(i + 1) & (kInWords - 1)]);
         return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
     }
     __device__ __forceinline__ uint32_t byte_at(uint64_t p) const {
@@ -140,7 +196,8 @@ struct Inflater {
     __device__ __forceinline__ void refill() {
         if (bc <= 32) {
             if (pos + 8 > staged) stage();
-            bb |= (uint64_t)word_at(pos) << bc;
+            const uint32_t w = (pos & 3) ? word_at(pos) : rfl(L.in[(uint32_t)(pos >> 2) & (kInWords - 1)]);
+            bb |= (uint64_t)w << bc;
             pos += 4;
             bc += 32;
             if (pos > end + 8 && !err) err = RDX_INFLATE_TRUNCATED;  // decoding the zero padding
@@ -172,15 +229,18 @@ struct Inflater {
     // ---- output ----------------------------------------------------------------------------------
     // Write [flushed, flushed + n) of the ring to HBM (n <= kFlush) and fold it into the checksum.
     __device__ __forceinline__ void flush(uint32_t n) {
-        __syncthreads();
+        constexpr uint32_t kSl = kFlush / 64;  // bytes per lane slice
+        PROF_ADD(P_FLUSH, 1);
+        PROF_T0();
+        wave_sync();
         const uint32_t base = (uint32_t)(flushed & kWinMask);
-        const uint32_t lo = lane * 64;  // this lane's 64-byte slice of the unit
-        const uint32_t cnt = lo >= n ? 0 : (n - lo < 64 ? n - lo : 64);
+        const uint32_t lo = lane * kSl;
+        const uint32_t cnt = lo >= n ? 0 : (n - lo < kSl ? n - lo : kSl);
         uint8_t *d = dst + flushed + lo;
         uint32_t c = 0, a = 0, b = 0;  // slice crc, s1, s2
-        if (cnt == 64 && ((uintptr_t)d & 15) == 0) {
+        if (cnt == kSl && ((uintptr_t)d & 15) == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (uint32_t k = 0; k < kSl / 16; ++k) {
                 const uint4 v = *reinterpret_cast<const uint4 *>(&L.win[base + lo + 16 * k]);
                 gst<uint4>(d + 16 * k, v);
             }
@@ -189,7 +249,7 @@ struct Inflater {
         }
         if (gzip) {
             c = 0xffffffffu;
-            for (uint32_t k = 0; k < cnt; ++k) c = L.crc_tab[(c ^ L.win[(base + lo + k) & kWinMask]) & 0xff] ^ (c >> 8);
+            for (uint32_t k = 0; k < cnt; ++k) c = S.crc_tab[(c ^ L.win[(base + lo + k) & kWinMask]) & 0xff] ^ (c >> 8);
             c ^= 0xffffffffu;
             // combine the 64 slice CRCs in lane order (tree; right part length = its valid bytes)
             uint32_t len = cnt;
@@ -198,12 +258,12 @@ struct Inflater {
                 const uint32_t oc = (uint32_t)__shfl_xor((int)c, m, 64);
                 const uint32_t ol = (uint32_t)__shfl_xor((int)len, m, 64);
                 if ((lane & m) == 0) {
-                    c = ol ? crc_combine(L, c, oc, ol) : c;
+                    c = ol ? crc_combine(S, c, oc, ol) : c;
                     len += ol;
                 }
             }
-            c = (uint32_t)__shfl((int)c, 0, 64);
-            crc = flushed == 0 ? c : crc_combine(L, crc, c, n);
+            c = rfl((uint32_t)__shfl((int)c, 0, 64));
+            crc = flushed == 0 ? c : crc_combine(S, crc, c, n);
         } else {
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t v = L.win[(base + lo + k) & kWinMask];
@@ -218,13 +278,18 @@ struct Inflater {
                 t1 += (uint64_t)__shfl_xor((long long)t1, m, 64);
                 t2 += (uint64_t)__shfl_xor((long long)t2, m, 64);
             }
-            t1 %= kAdlerMod;
+            t1 = rfl((uint32_t)(t1 % kAdlerMod));
+            t2 = rfl((uint32_t)(t2 % kAdlerMod));
             t2 %= kAdlerMod;
             s2 = (uint32_t)((s2 + (uint64_t)(n % kAdlerMod) * s1 + t2) % kAdlerMod);
             s1 = (uint32_t)((s1 + t1) % kAdlerMod);
         }
         flushed += n;
-        __syncthreads();
+        // the flushed bytes are read back by back-references farther than the ring (copy()): their
+        // stores must have completed in L2 before any such load issues
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_sync();
+        PROF_T1(P_T_FLUSH);
     }
     // Flushing happens at ONE place per loop (the top of the symbol loop / stored-copy loop), so the
     // flush code is inlined once there instead of behind every literal and copy; between two checks
@@ -245,18 +310,39 @@ struct Inflater {
         if (lane == 0) L.win[out & kWinMask] = (uint8_t)v;
         ++out;
     }
-    __device__ __forceinline__ void copy(uint32_t len, uint32_t dist) {
-        if (!room(len)) return;
-        __builtin_amdgcn_wave_barrier();
+    __device__ __forceinline__ void copy_at(uint64_t o, uint32_t len, uint32_t dist) {
+        PROF_ADD(P_MATCH, 1);
+        PROF_ADD(P_MATCH_BYTES, len);
+        PROF_ADD(P_FAR, dist > kWin - 258 ? 1 : 0);
+        asm volatile("" ::: "memory");  // after lane 0's literal writes (in-order LDS, same wave)
+        const uint32_t o32 = (uint32_t)o;  // ring indices need only the low bits
+        // j mod dist for overlapping copies by a float reciprocal (exact after one correction)
+        const float rd = __builtin_amdgcn_rcpf((float)dist);
         for (uint32_t j0 = 0; j0 < len; j0 += 64) {
             const uint32_t j = j0 + lane;
             if (j < len) {
-                const uint32_t m = dist >= len ? j : j % dist;
-                const uint8_t v = L.win[(uint32_t)(out - dist + m) & kWinMask];
-                L.win[(uint32_t)(out + j) & kWinMask] = v;
+                uint32_t m = j;
+                if (dist < len) {
+                    const uint32_t q = (uint32_t)((float)j * rd);
+                    int32_t r = (int32_t)(j - q * dist);
+                    r = r < 0 ? r + (int32_t)dist : (r >= (int32_t)dist ? r - (int32_t)dist : r);
+                    m = (uint32_t)r;
+                }
+                const uint32_t back = dist - m;  // source = o - back
+                // the ring holds [frontier - kWin, frontier), the frontier having advanced by the j0
+                // bytes this copy already wrote; anything older is flushed to HBM (o - flushed <
+                // kFlush + 258, j0 < 258, kWin >= kFlush + 516)
+                uint8_t v;
+                if (back + j0 <= kWin) [[likely]] v = L.win[(o32 - back) & kWinMask];
+                else v = gld<uint8_t>(dst + (o - back));
+                L.win[(o32 + j) & kWinMask] = v;
             }
         }
-        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    }
+    __device__ __forceinline__ void copy(uint32_t len, uint32_t dist) {
+        if (!room(len)) return;
+        copy_at(out, len, dist);
         out += len;
     }
 
@@ -264,8 +350,28 @@ struct Inflater {
     // Canonical code of n lengths -> root table (2^root entries: symbol | length << 16, 0 = longer
     // code) + count[] / sym[] for the bit-serial walk.  Returns 0 complete, > 0 incomplete,
     // < 0 over-subscribed; count[0] = number of unused symbols.
+    // table entry of symbol s: kind 0 = code-length code (value = s), 1 = literal/length, 2 = distance
+    __device__ __forceinline__ uint32_t entry_of(uint32_t s, uint32_t kind) const {
+        if (kind == 1) {
+            if (s < 256) return s;
+            if (s == 256) return kTypeEob;
+            if (s < 286) {
+                const uint32_t lb = S.lbase[s - 257];
+                return (lb & 0xffff) | (lb >> 16) << 20 | kTypeLen;
+            }
+            return kTypeBad;
+        }
+        if (kind == 2) {
+            if (s < 30) {
+                const uint32_t db = S.dbase[s];
+                return (db & 0xffff) | (db >> 16) << 20;
+            }
+            return kTypeBad;
+        }
+        return s;
+    }
     __device__ __forceinline__ int build(const uint8_t *lens, uint32_t n, uint32_t *tab, uint32_t root, uint16_t *count,
-                         uint16_t *sym) {
+                         uint16_t *sym, uint32_t kind) {
         uint32_t cnt[16];
 #pragma unroll
         for (int l = 0; l < 16; ++l) cnt[l] = 0;
@@ -299,7 +405,7 @@ struct Inflater {
                 L.next[l] = (uint16_t)(l ? next[l] : 0);
             }
         }
-        __syncthreads();
+        wave_sync();
         if (cnt[0] == n) return 0;  // no codes at all: complete by convention (puff)
         if (over) return -1;
         uint32_t run[16];
@@ -321,44 +427,48 @@ struct Inflater {
                 if (l <= root) {
                     const uint32_t c = L.next[l] + rank;
                     const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
-                    for (uint32_t k = r; k < (1u << root); k += 1u << l) tab[k] = s | (l << 16);
+                    const uint32_t e = entry_of(s, kind) | l << 16;
+                    for (uint32_t k = r; k < (1u << root); k += 1u << l) tab[k] = e;
                 }
             }
         }
-        __syncthreads();
+        wave_sync();
         return left;
     }
     // decode one symbol (needs >= 15 valid bits): root table, else the canonical bit-serial walk
-    __device__ __forceinline__ int decode(const uint32_t *tab, uint32_t root, const uint16_t *count, const uint16_t *sym) {
-        const uint32_t e = tab[(uint32_t)bb & ((1u << root) - 1)];
-        const uint32_t l = e >> 16;
+    __device__ __forceinline__ uint32_t decode(const uint32_t *tab, uint32_t root, const uint16_t *count,
+                                               const uint16_t *sym, uint32_t kind) {
+        const uint32_t e = rfl(tab[(uint32_t)bb & ((1u << root) - 1)]);
+        const uint32_t l = (e >> 16) & 15;
         if (l) {
             bb >>= l;
             bc -= l;
-            return (int)(e & 0xffff);
+            return e;
         }
-        int code = 0, first = 0, index = 0;
+        PROF_ADD(P_SLOW, 1);
+        int code = 0, first = 0, index = 0;  // longer than the root: canonical bit-serial walk
+#pragma unroll 1
         for (int len = 1; len < 16; ++len) {
             code |= (int)(bb & 1);
             bb >>= 1;
             --bc;
-            const int c = count[len];
-            if (code - c < first) return sym[index + (code - first)];
+            const int c = (int)rfl(count[len]);
+            if (code - c < first) return entry_of(rfl(sym[index + (code - first)]), kind);
             index += c;
             first += c;
             first <<= 1;
             code <<= 1;
         }
-        return -1;
+        return kTypeBad;
     }
 
     // ---- blocks ------------------------------------------------------------------------------------
     __device__ __forceinline__ void fixed_tables() {
         for (uint32_t s = lane; s < 288 + 30; s += 64)
             L.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
-        __syncthreads();
-        build(L.lens, 288, L.lit, kLitRoot, L.lcount, L.lsym);
-        build(L.lens + 288, 30, L.dist, kDistRoot, L.dcount, L.dsym);
+        wave_sync();
+        build(L.lens, 288, L.lit, kLitRoot, L.lcount, L.lsym, 1);
+        build(L.lens + 288, 30, L.dist, kDistRoot, L.dcount, L.dsym, 2);
     }
 
     __device__ __forceinline__ void dynamic_tables() {
@@ -385,8 +495,8 @@ struct Inflater {
             if (lane < ncode) v = lane < 10 ? (uint32_t)(v1 >> (3 * lane)) & 7 : (uint32_t)(v2 >> (3 * (lane - 10))) & 7;
             L.lens[ord] = (uint8_t)v;
         }
-        __syncthreads();
-        if (build(L.lens, 19, L.cl, kClRoot, L.clcount, L.clsym) != 0) {  // complete code required
+        wave_sync();
+        if (build(L.lens, 19, L.cl, kClRoot, L.clcount, L.clsym, 0) != 0) {  // complete code required
             err = RDX_INFLATE_CODE_LENGTHS;
             return;
         }
@@ -396,8 +506,8 @@ struct Inflater {
         bool has_eob = false;
         while (idx < total && !err) {
             refill();
-            const uint32_t e = L.cl[(uint32_t)bb & ((1u << kClRoot) - 1)];
-            const uint32_t l = e >> 16, sym = e & 0xffff;
+            const uint32_t e = rfl(L.cl[(uint32_t)bb & ((1u << kClRoot) - 1)]);
+            const uint32_t l = (e >> 16) & 15, sym = e & 0xffff;
             bb >>= l;
             bc -= l;
             if (sym < 16) {
@@ -431,55 +541,192 @@ struct Inflater {
             prev = val;
             idx += rep;
         }
-        __syncthreads();
+        wave_sync();
         if (err) return;
         if (!has_eob) {
             err = RDX_INFLATE_CODE_LENGTHS;
             return;
         }
-        int r = build(L.lens, nlen, L.lit, kLitRoot, L.lcount, L.lsym);
-        if (r < 0 || (r > 0 && nlen != (uint32_t)L.lcount[0] + L.lcount[1])) {
+        int r = build(L.lens, nlen, L.lit, kLitRoot, L.lcount, L.lsym, 1);
+        if (r < 0 || (r > 0 && nlen != rfl((uint32_t)L.lcount[0] + L.lcount[1]))) {
             err = RDX_INFLATE_CODE_LENGTHS;
             return;
         }
-        r = build(L.lens + nlen, ndist, L.dist, kDistRoot, L.dcount, L.dsym);
-        if (r < 0 || (r > 0 && ndist != (uint32_t)L.dcount[0] + L.dcount[1])) err = RDX_INFLATE_CODE_LENGTHS;
+        r = build(L.lens + nlen, ndist, L.dist, kDistRoot, L.dcount, L.dsym, 2);
+        if (r < 0 || (r > 0 && ndist != rfl((uint32_t)L.dcount[0] + L.dcount[1]))) err = RDX_INFLATE_CODE_LENGTHS;
+    }
+
+    // refill for the Huffman loop: `pos` is always 4-byte aligned there (stored() realigns it)
+    __device__ __forceinline__ void refill_fast() {
+        if (bc <= 32) {
+            if (pos + 8 > staged) [[unlikely]] {
+                stage();
+                if (pos > end + 8 && !err) err = RDX_INFLATE_TRUNCATED;  // decoding the zero padding
+            }
+            bb |= (uint64_t)rfl(L.in[(uint32_t)(pos >> 2) & (kInWords - 1)]) << bc;
+            pos += 4;
+            bc += 32;
+        }
+    }
+    // slow symbol: a code longer than the table root (bit-serial canonical walk), or no code
+    __device__ uint32_t decode_slow(const uint16_t *count, const uint16_t *sym, uint32_t kind) {
+        PROF_ADD(P_SLOW, 1);
+        int code = 0, first = 0, index = 0;
+#pragma unroll 1
+        for (int len = 1; len < 16; ++len) {
+            code |= (int)(bb & 1);
+            bb >>= 1;
+            --bc;
+            const int c = (int)rfl(count[len]);
+            if (code - c < first) return entry_of(rfl(sym[index + (code - first)]), kind);
+            index += c;
+            first += c;
+            first <<= 1;
+            code <<= 1;
+        }
+        return kTypeBad;
+    }
+
+    // The symbol loop of one Huffman block, in two tiers.  A wave issues one instruction per 4 cycles
+    // at best, so the serial decode is paid per INSTRUCTION: hot() keeps the whole state in a handful
+    // of scalar locals and handles only the common cases (literals, and matches whose codes hit the
+    // root tables, with the ring and the input known to have room); anything else (input staging,
+    // flushing, codes longer than the root, end of block, capacity, errors) leaves hot() WITHOUT
+    // consuming the symbol, and general() decodes that one symbol with every check.
+    __device__ __forceinline__ void hot() {
+        uint64_t b = bb, p = pos, o = out;
+        uint32_t c = bc;
+        const uint64_t stop_p = rfl64(staged) - 8;  // a dword refill needs p + 8 <= staged
+        const uint64_t fl = rfl64(flushed) + kFlush, cp = rfl64(cap);
+        const uint64_t lim = fl < cp ? fl : cp;
+        const uint64_t stop_o = lim > 258 ? lim - 258 : 0;  // room for one more literal or match
+        if (rfl64(o) > stop_o || rfl64(p) > stop_p + 8) return;
+        // 32-bit countdowns (SALU has no 64-bit ordered compare): input bytes left before a refill
+        // would pass `staged`, output bytes left before the ring / capacity check is due
+        const uint64_t dp = stop_p + 8 - p, dout = stop_o - o;
+        int32_t rp = (int32_t)(dp < 0x40000000u ? dp : 0x40000000u) - 8;
+        int32_t ro = (int32_t)(dout < 0x40000000u ? dout : 0x40000000u);
+        const uint32_t o_lane = lane;
+        for (;;) {
+            asm volatile("; inflate hot loop" ::: "memory");
+            b = rfl64(b);
+            c = rfl(c);
+            p = rfl64(p);
+            o = rfl64(o);
+            rp = (int32_t)rfl((uint32_t)rp);
+            ro = (int32_t)rfl((uint32_t)ro);
+            if (ro < 0) break;
+            if (c <= 32) {
+                if (rp < 0) break;
+                b |= (uint64_t)rfl(L.in[(uint32_t)(p >> 2) & (kInWords - 1)]) << c;
+                p += 4;
+                rp -= 4;
+                c += 32;
+            }
+            const uint32_t e = rfl(L.lit[(uint32_t)b & ((1u << kLitRoot) - 1)]);
+            const uint32_t l = (e >> 16) & 15;
+            if (l == 0) break;
+            const uint32_t type = e >> 24;
+            if (type == 0) {
+                PROF_ADD(P_LIT, 1);
+                b >>= l;
+                c -= l;
+                if (o_lane == 0) L.win[(uint32_t)o & kWinMask] = (uint8_t)e;
+                ++o;
+                --ro;
+                continue;
+            }
+            if (type != 1) break;
+            uint64_t b2 = b >> l;
+            uint32_t c2 = c - l;
+            const uint32_t ext = (e >> 20) & 15;
+            const uint32_t len = (e & 0xffff) + (uint32_t)(b2 & ((1u << ext) - 1));
+            b2 >>= ext;
+            c2 -= ext;
+            uint64_t p2 = p;
+            int32_t rp2 = rp;
+            if (c2 <= 32) {
+                if (rp2 < 0) break;
+                b2 |= (uint64_t)rfl(L.in[(uint32_t)(p2 >> 2) & (kInWords - 1)]) << c2;
+                p2 += 4;
+                rp2 -= 4;
+                c2 += 32;
+            }
+            const uint32_t d = rfl(L.dist[(uint32_t)b2 & ((1u << kDistRoot) - 1)]);
+            const uint32_t dl = (d >> 16) & 15;
+            if (dl == 0 || (d >> 24)) break;
+            b2 >>= dl;
+            c2 -= dl;
+            const uint32_t dext = (d >> 20) & 15;
+            const uint32_t dist = (d & 0xffff) + (uint32_t)(b2 & ((1u << dext) - 1));
+            b2 >>= dext;
+            c2 -= dext;
+            if (dist > (uint32_t)(o < 0x80000000u ? o : 0x80000000u)) break;
+            b = b2;  // commit the symbol
+            c = c2;
+            p = p2;
+            rp = rp2;
+            copy_at(o, len, dist);
+            o += len;
+            ro -= (int32_t)len;
+        }
+        bb = b;
+        bc = c;
+        pos = p;
+        out = o;
+    }
+
+    // One symbol with every check; returns true at the end of the block (or on an error).
+    __device__ __forceinline__ bool general() {
+        flush_full();
+        refill();
+        if (err) return true;
+        uint32_t e = rfl(L.lit[(uint32_t)bb & ((1u << kLitRoot) - 1)]);
+        const uint32_t l = (e >> 16) & 15;
+        if (l) {
+            bb >>= l;
+            bc -= l;
+        } else {
+            e = decode_slow(L.lcount, L.lsym, 1);
+        }
+        const uint32_t type = e & (3u << 24);
+        if (type == 0) {
+            PROF_ADD(P_LIT, 1);
+            literal(e & 0xff);
+            return err != 0;
+        }
+        if (type == kTypeEob) return true;
+        if (type != kTypeLen) {
+            err = RDX_INFLATE_BAD_SYMBOL;
+            return true;
+        }
+        const uint32_t len = (e & 0xffff) + bits((e >> 20) & 15);
+        refill();
+        uint32_t d = rfl(L.dist[(uint32_t)bb & ((1u << kDistRoot) - 1)]);
+        const uint32_t dl = (d >> 16) & 15;
+        if (dl) {
+            bb >>= dl;
+            bc -= dl;
+        } else {
+            d = decode_slow(L.dcount, L.dsym, 2);
+        }
+        if (d & (3u << 24)) {
+            err = RDX_INFLATE_BAD_SYMBOL;
+            return true;
+        }
+        const uint32_t dist = (d & 0xffff) + bits((d >> 20) & 15);
+        if (dist > out) {
+            err = RDX_INFLATE_DISTANCE;
+            return true;
+        }
+        copy(len, dist);
+        return err != 0;
     }
 
     __device__ __forceinline__ void codes() {
         while (!err) {
-            flush_full();
-            refill();
-            const int sym = decode(L.lit, kLitRoot, L.lcount, L.lsym);
-            if (sym < 256) {
-                if (sym < 0) {
-                    err = RDX_INFLATE_BAD_SYMBOL;
-                    break;
-                }
-                literal((uint32_t)sym);
-                continue;
-            }
-            if (sym == 256) break;
-            const uint32_t ls = (uint32_t)sym - 257;
-            if (ls >= 29) {
-                err = RDX_INFLATE_BAD_SYMBOL;
-                break;
-            }
-            const uint32_t le = L.lbase[ls];
-            const uint32_t len = (le & 0xffff) + bits(le >> 16);
-            refill();
-            const int ds = decode(L.dist, kDistRoot, L.dcount, L.dsym);
-            if (ds < 0 || ds >= 30) {
-                err = RDX_INFLATE_BAD_SYMBOL;
-                break;
-            }
-            const uint32_t de = L.dbase[ds];
-            const uint32_t dist = (de & 0xffff) + bits(de >> 16);
-            if (dist > out) {
-                err = RDX_INFLATE_DISTANCE;
-                break;
-            }
-            copy(len, dist);
+            hot();
+            if (general()) break;
         }
     }
 
@@ -513,6 +760,14 @@ struct Inflater {
             pos += m;
             left -= m;
         }
+        // keep `pos` 4-byte aligned (the Huffman loop refills whole dwords): move the rest of the
+        // current dword into the bit buffer
+        if (!err && (pos & 3)) {
+            const uint32_t sh = (uint32_t)(pos & 3) * 8;
+            bb = rfl(L.in[(uint32_t)(pos >> 2) & (kInWords - 1)]) >> sh;
+            bc = 32 - sh;
+            pos = (pos | 3) + 1;
+        }
     }
 
     __device__ __forceinline__ void run() {
@@ -522,16 +777,21 @@ struct Inflater {
             flush_full();
             refill();
             last = bits(1);
+            PROF_ADD(P_BLOCKS, 1);
             const uint32_t type = bits(2);
             if (type == 0) {
                 stored();
             } else if (type == 1) {
+                PROF_T0();
                 if (!fixed_ready) fixed_tables();
+                PROF_T1(P_T_TABLES);
                 fixed_ready = true;
                 codes();
             } else if (type == 2) {
                 fixed_ready = false;
+                PROF_T0();
                 dynamic_tables();
+                PROF_T1(P_T_TABLES);
                 if (!err) codes();
             } else {
                 err = RDX_INFLATE_BLOCK_TYPE;
@@ -540,48 +800,52 @@ struct Inflater {
     }
 };
 
-__global__ __launch_bounds__(64) void k_inflate(const KInflateArgs a) {
-    __shared__ InflateLds L;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t i = blockIdx.x;
-    const uint8_t *src = gld<const uint8_t *>(a.in + i);
-    const uint64_t len = gld<uint64_t>(a.in_len + i);
-    // constant tables
-    if (lane < 29) {
+__global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
+    __shared__ InflateShared S;
+    __shared__ InflateLds LW[kWaves];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // shared constant tables (once per workgroup; the only workgroup-wide barrier)
+    if (t < 29) {
         constexpr uint16_t kB[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
         uint32_t b = 0;
 #pragma unroll
         for (int k = 0; k < 29; ++k)
-            if ((uint32_t)k == lane) b = kB[k];
-        const uint32_t e = lane < 8 || lane == 28 ? 0 : (lane - 4) / 4;
-        L.lbase[lane] = b | e << 16;
-    }
-    if (lane < 30) {
-        const uint32_t e = lane < 2 ? 0 : lane / 2 - 1;
-        const uint32_t b = lane < 4 ? lane + 1 : (1u << e) * (2 + (lane & 1)) + 1;
-        L.dbase[lane] = b | e << 16;
-    }
-    for (uint32_t t = lane; t < 256; t += 64) {
-        uint32_t c = t;
-        for (int k = 0; k < 8; ++k) c = c & 1 ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        L.crc_tab[t] = c;
-    }
-    if (lane == 0) {
+            if ((uint32_t)k == t) b = kB[k];
+        const uint32_t e = t < 8 || t == 28 ? 0 : (t - 4) / 4;
+        S.lbase[t] = b | e << 16;
+    } else if (t >= 64 && t < 94) {
+        const uint32_t c = t - 64;
+        const uint32_t e = c < 2 ? 0 : c / 2 - 1;
+        const uint32_t b = c < 4 ? c + 1 : (1u << e) * (2 + (c & 1)) + 1;
+        S.dbase[c] = b | e << 16;
+    } else if (t == 128) {
         uint32_t p = 1u << 30;  // x^1
         for (int k = 0; k < 32; ++k) {
-            L.x2n[k] = p;
+            S.x2n[k] = p;
             p = multmodp(p, p);
         }
     }
+    {
+        uint32_t c = t;
+        for (int k = 0; k < 8; ++k) c = c & 1 ? 0xedb88320u ^ (c >> 1) : c >> 1;
+        S.crc_tab[t] = c;
+    }
     __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * kWaves + wave;
+    if (i >= a.n) return;
+    InflateLds &L = LW[wave];
+    // scalar: every lane reads the same descriptor, and the decode state derived from it must stay
+    // wave-uniform (SGPRs) for the serial path to compile to scalar code
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(rfl64((uint64_t)gld<const uint8_t *>(a.in + i)));
+    const uint64_t len = rfl64(gld<uint64_t>(a.in_len + i));
 
     const uint32_t skew = (uint32_t)((uintptr_t)src & 3);
-    Inflater f{L, lane};
+    Inflater f{L, S, lane};
     f.srcw = reinterpret_cast<const uint32_t *>(src - skew);
     f.end = skew + len;
     f.staged = 0;
-    f.pos = skew;
+    f.pos = 0;
     f.bb = 0;
     f.bc = 0;
     f.dst = a.out + (uint64_t)i * a.cap;
@@ -592,7 +856,15 @@ __global__ __launch_bounds__(64) void k_inflate(const KInflateArgs a) {
     f.s2 = 0;
     f.gzip = a.format == RDX_COMPRESSION_GZIP;
     f.err = 0;
+#ifdef RDX_INFLATE_PROF
+    for (int k = 0; k < P_N; ++k) f.prof[k] = 0;
+    const uint64_t t_start = __builtin_readcyclecounter();
+#endif
     f.stage();
+    if (skew) {  // refills stay 4-byte aligned: drop the bytes before the stream from the bit buffer
+        f.refill();
+        f.bits(8 * skew);
+    }
 
     if (f.gzip) {  // RFC 1952 member header (flate2 GzDecoder)
         if (len < 2 || f.need(8) != 0x1f || f.need(8) != 0x8b) {
@@ -652,6 +924,10 @@ __global__ __launch_bounds__(64) void k_inflate(const KInflateArgs a) {
     if (lane == 0) {
         a.out_len[i] = f.out;
         a.err[i] = f.err;
+#ifdef RDX_INFLATE_PROF
+        f.prof[P_T_TOTAL] = __builtin_readcyclecounter() - t_start;
+        for (int k = 0; k < P_N; ++k) atomicAdd(&g_prof[k], (unsigned long long)f.prof[k]);
+#endif
     }
 }
 
@@ -660,8 +936,8 @@ __global__ __launch_bounds__(64) void k_inflate(const KInflateArgs a) {
 hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uint64_t *d_in_len, uint64_t n,
                           uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    KInflateArgs a{d_in, d_in_len, d_out, cap, d_out_len, d_err, format};
-    hipLaunchKernelGGL(k_inflate, dim3((uint32_t)n), dim3(64), 0, s, a);
+    KInflateArgs a{d_in, d_in_len, d_out, cap, d_out_len, d_err, format, (uint32_t)n};
+    hipLaunchKernelGGL(k_inflate, dim3((uint32_t)((n + kWaves - 1) / kWaves)), dim3(64 * kWaves), 0, s, a);
     return hipGetLastError();
 }
 
