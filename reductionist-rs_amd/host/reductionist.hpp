@@ -75,14 +75,16 @@ class ActiveStorageError : public std::runtime_error {
         ShapeInvalid,           // 400
         IncompatibleMissing,    // 400
         ReferencePanic,         // the reference panics (shuffle assert, NaN order): connection drops
-        Unsupported,            // compression must be undone on the host first
+        Unsupported,            // blosc2: decompress on the host first (not on the device)
+        Decompression,          // DecompressionFlate2 / DecompressionZune: 400 (error.rs:247-249)
         Device                  // 500
     };
     ActiveStorageError(Kind k, const std::string &what, rdx_status st = RDX_OK)
         : std::runtime_error(what), kind(k), status(st) {}
     int http_status() const {
         switch (kind) {
-            case Kind::RequestDataValidation: case Kind::ShapeInvalid: case Kind::IncompatibleMissing: return 400;
+            case Kind::RequestDataValidation: case Kind::ShapeInvalid: case Kind::IncompatibleMissing:
+            case Kind::Decompression: return 400;
             default: return 500;
         }
     }
@@ -98,6 +100,8 @@ inline void check(rdx_status st) {
         case RDX_E_FROM_BYTES: throw ActiveStorageError(K::FromBytes, "failed to convert from bytes", st);
         case RDX_E_SHAPE_INVALID: throw ActiveStorageError(K::ShapeInvalid, "failed to create array from shape", st);
         case RDX_E_INCOMPATIBLE_MISSING: throw ActiveStorageError(K::IncompatibleMissing, "Incompatible value for missing", st);
+        case RDX_E_DECOMPRESSION:  // compression.rs:166-190 messages where the reference pins them
+            throw ActiveStorageError(K::Decompression, rdx_inflate_error_string(rdx_inflate_last_error()), st);
         case RDX_E_SHUFFLE_LENGTH: throw ActiveStorageError(K::ReferencePanic, "assertion `left == right` failed", st);
         case RDX_E_NAN_UNORDERED: throw ActiveStorageError(K::ReferencePanic, "unexpected undefined order error for min", st);
         case RDX_E_UNSUPPORTED: throw ActiveStorageError(K::Unsupported, "unsupported by the device engine", st);
@@ -245,13 +249,21 @@ class Engine {
 
 // src/operation.rs:53-66 — `execute(request_data, data) -> Result<Response>`; errors are thrown.
 // Unlike the reference's trait (which receives filter-decoded bytes from operation<T>()), this
-// executes the whole synchronous pipeline on the device: pass the RAW (decompressed) chunk.
+// executes the whole synchronous pipeline on the device: pass the chunk as downloaded (gzip/zlib
+// compressed or not, shuffled or not).
 template <rdx_op OP>
 struct Operation {
     static Response execute(const RequestData &rd, const std::vector<uint8_t> &data, Engine &eng = Engine::global()) {
         RequestData::Marshalled m = rd.marshal(OP);
         rdx_response_info info{};
-        check(rdx_plan(&m.req, data.size(), &info));
+        if (rd.compression) {
+            // the response size depends on the decompressed length: a call without output capacity
+            // inflates on the device and reports it (RDX_E_BUFFER_TOO_SMALL with `info` filled)
+            const rdx_status st = rdx_execute(eng.get(), &m.req, data.data(), data.size(), nullptr, 0, nullptr, 0, &info);
+            if (st != RDX_E_BUFFER_TOO_SMALL) check(st);
+        } else {
+            check(rdx_plan(&m.req, data.size(), &info));
+        }
         Response r;
         r.body.resize(info.body_bytes);
         r.count.resize(info.n_counts);

@@ -173,6 +173,20 @@ static void gpu_tests() {
     fb.dtype = DType::Uint32;
     fb.size = 3;
     EXPECT(error_kind([&] { Sum::execute(fb, {1, 2, 3}); }) == K::FromBytes);
+    // filter_pipeline.rs:70-77: a gzip chunk is inflated on the device (stream of bytes 1..8, frozen)
+    RequestData gz;
+    gz.dtype = DType::Uint32;
+    gz.compression = Compression::Gzip;
+    const std::vector<uint8_t> gzs = {0x1f, 0x8b, 0x08, 0x00, 0x00, 0x00, 0x00, 0x00, 0x04, 0x03, 0x63, 0x64, 0x62, 0x66, 0x61, 0x65, 0x63, 0xe7, 0x00, 0x00, 0xc5, 0x88, 0xca, 0x3f, 0x08, 0x00, 0x00, 0x00};
+    EXPECT(scalar<uint32_t>(Sum::execute(gz, gzs)) == 0x04030201u + 0x08070605u);
+    // compression.rs:165-176: b"invalid format" -> DecompressionFlate2 "invalid gzip header" (400)
+    const std::string bad = "invalid format";
+    try {
+        Sum::execute(gz, std::vector<uint8_t>(bad.begin(), bad.end()));
+        EXPECT(false);
+    } catch (const ActiveStorageError &e) {
+        EXPECT(e.kind == K::Decompression && e.http_status() == 400 && std::string(e.what()) == "invalid gzip header");
+    }
 }
 
 int main(int argc, char **argv) {

@@ -213,3 +213,17 @@ def test_execute_device_with_compression(torch, workspace):
         assert ost == 0 and int(status[0]) == 0
         assert body.cpu().numpy().tobytes()[:info.body_bytes] == obody
         assert counts.cpu().tolist()[:info.n_counts] == ocounts
+
+
+def test_python_mirror_with_compression(engine):
+    """The Operation mirror (reductionist_amd.operations) on a compressed request, and the error class
+    a corrupt stream raises (compression.rs:165-176 -> DecompressionFlate2, HTTP 400)."""
+    from reductionist_amd import RequestData, Sum
+    from reductionist_amd.errors import Decompression
+    vals = np.arange(1, 1001, dtype=np.uint32)
+    rd = RequestData(dtype="uint32", compression="gzip", shape=[1000])
+    resp = Sum.execute(rd, gz(vals.tobytes()), engine)
+    assert int(np.frombuffer(resp.body, np.uint32)[0]) == int(vals.sum()) and resp.count == [1000]
+    with pytest.raises(Decompression) as ei:
+        Sum.execute(RequestData(dtype="uint32", compression="gzip"), b"invalid format", engine)
+    assert str(ei.value) == "invalid gzip header" and ei.value.http_status == 400

@@ -9,7 +9,7 @@ PKG = ROOT / "reductionist-rs_amd"
 
 
 def _binary():
-    out = PKG / "build" / "test_host"
+    out = ROOT / "tests" / "cpp" / "build" / "test_host"   # built here, travels to the GPU box
     src = ROOT / "tests" / "cpp" / "test_host.cpp"
     hdr = PKG / "host" / "reductionist.hpp"
     lib = PKG / "librdx.so"
