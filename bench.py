@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-inflate", action="store_true")
     ap.add_argument("--primary-only", action="store_true", help="only the headline batched C2 loop (profiling)")
     return ap.parse_args()
 
@@ -131,6 +132,75 @@ def cpu_baseline_c4(threads, distinct=64):
     return {"value": round(C4_CHUNKS * 4 * C4_ELEMS / el / GIB, 3), "unit": "GiB/s", "cores": threads,
             "kind": "port", "sample": f"all {C4_CHUNKS} chunks ({distinct} distinct, cycled), {threads} worker "
                                       f"threads, oracle g++ -O2, {el:.2f} s"}
+
+
+def inflate_batch(torch, ws, stream, rank, world, with_cpu, n_total=1024, distinct=16, reps=3):
+    """BASELINE configs[3]'s batch shape with zlib on top: 1024 x 4 MiB N(0,1) f32 chunks, byte-shuffled,
+    zlib level 1 (distinct chunks cycled), split over ranks; one rdx_decompress_batch_device launch per
+    rep.  GB/s of decompressed output; CPU: CPython zlib (the C library) on 15 threads."""
+    import zlib
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from reductionist_amd.sharding import shard_range
+    lo, hi = shard_range(n_total, rank, world)
+    n = hi - lo
+    rng = np.random.default_rng(0x5EED2000)
+    raws, streams = [], []
+    for _ in range(distinct):
+        v = rng.standard_normal(C4_ELEMS).astype(np.float32)
+        raw = v.view(np.uint8).reshape(C4_ELEMS, 4).T.copy().tobytes()
+        c = zlib.compressobj(1, zlib.DEFLATED, 15)
+        raws.append(raw)
+        streams.append(c.compress(raw) + c.flush())
+    offs, total = [], 0
+    for s in streams:
+        offs.append(total)
+        total += (len(s) + 255) // 256 * 256
+    host = np.zeros(total, dtype=np.uint8)
+    for o, s in zip(offs, streams):
+        host[o:o + len(s)] = np.frombuffer(s, dtype=np.uint8)
+    d_in = torch.from_numpy(host).cuda()
+    raw_len = 4 * C4_ELEMS
+    d_out = torch.empty(max(1, n) * raw_len, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+    d_err = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
+    ptrs = [d_in.data_ptr() + offs[(lo + i) % distinct] for i in range(n)]
+    lens = [len(streams[(lo + i) % distinct]) for i in range(n)]
+
+    def launch():
+        ws.decompress_batch_device("zlib", ptrs, lens, d_out.data_ptr(), raw_len, d_len.data_ptr(),
+                                   d_err.data_ptr(), stream.cuda_stream)
+
+    launch()
+    torch.cuda.synchronize()
+    assert int(d_err.abs().sum()) == 0 and bool((d_len == raw_len).all())
+    assert d_out[:raw_len].cpu().numpy().tobytes() == raws[lo % distinct]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / reps
+    out = {"workload": "1024 x 4 MiB N(0,1) f32 chunks, shuffle es=4, zlib level 1 (ratio %.2f), batch split over "
+                       "ranks; one rdx_decompress_batch_device launch" % (raw_len * distinct / sum(len(s) for s in streams)),
+           "value": round(n * raw_len / t / 1e9, 2), "unit": "GB/s decompressed (this rank)", "ms_per_launch":
+           round(t * 1e3, 2), "kernel": "k_inflate", "bound": "serial decode per wavefront (DESIGN.md §9), not HBM"}
+    if with_cpu:
+        threads = max(1, min(15, (os.cpu_count() or 2) - 1))
+
+        def one(i):
+            zlib.decompress(streams[i % distinct])
+
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, range(threads)))
+            c0 = time.perf_counter()
+            list(ex.map(one, range(n_total)))
+            tz = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": round(n_total * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
+                               "kind": "library", "sample": f"CPython zlib.decompress of all {n_total} streams on a "
+                                                            f"{threads}-thread pool, {tz:.2f} s"}
+    return out
 
 
 def main():
@@ -231,7 +301,7 @@ def main():
 
     extra = {}
     if args.primary_only:
-        args.no_c4 = args.no_cpu_baseline = True
+        args.no_c4 = args.no_cpu_baseline = args.no_inflate = True
     else:
         for i in range(args.warmup):
             single_step(i)
@@ -288,6 +358,11 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             extra["c4_batch"]["cpu_baseline"] = cpu_baseline_c4(max(1, min(15, (os.cpu_count() or 2) - 1)))
 
+    # ---- decompression (extra): the filter pipeline's first stage on the device ------------
+    if not args.no_inflate:
+        extra["c4z_inflate"] = inflate_batch(torch, ws, stream, rank, world, not args.no_cpu_baseline and rank == 0
+                                             and world == 1)
+
     line = {
         "metric": "GiB/s device-resident chunk unshuffle+reduce (f32 sum), 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -300,7 +375,7 @@ def main():
                    "parallelism": f"independent chunks x{world} GPUs"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_GBS, 4), "traffic": traffic_from_profiles("c2"),
-                     "kernel": "k_all_contig<float, OP_SUM, FUSED=1, MISS=0>",
+                     "kernel": "k_all_contig<float, OP_SUM, FUSED=1, MK=0>",
                      "kernel_us_avg": round(kern_avg_s * 1e6, 3), "bytes_alg_per_launch": step_bytes,
                      "timing": "HIP events on the launch stream around the K back-to-back launches / K"},
         "extra": extra,
