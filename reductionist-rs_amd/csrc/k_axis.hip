@@ -62,14 +62,48 @@ __device__ __forceinline__ int64_t red_offset(const KView &rv, uint32_t r, int64
     return off;
 }
 
-template <typename T, int OP>
-__device__ __forceinline__ void fold_in(Red<T, OP> &r, const KMissing &miss, bool has_miss, T x, int64_t rank) {
-    if (has_miss && is_missing(miss, x)) return;
+// The reduced view's first two dims in registers, read from the kernel arguments once per lane
+// (not per load: a cold launch otherwise waits on one scalar-cache miss per dim per load, as the
+// strided all-axes kernel measured); deeper views fall back to the generic loop.
+struct RedRegs {
+    int32_t nd;
+    uint32_t c0;
+    uint64_t m0;
+    int64_t v0, v1, s0, s1, r0;
+    __device__ __forceinline__ void load(const KView &rv) {
+        nd = rv.ndim;
+        c0 = rv.count[0];
+        m0 = rv.div[0].magic;
+        v0 = rv.vstride[0];
+        s0 = rv.rstride[0];
+        v1 = rv.ndim > 1 ? rv.vstride[1] : 0;
+        s1 = rv.ndim > 1 ? rv.rstride[1] : 0;
+        r0 = rv.r0;
+    }
+};
+
+// GEN: the reduced view has more than 2 dims (generic per-dim loop); chosen at launch, so the
+// per-load offset code carries no rank branch.
+template <bool RANK, bool GEN>
+__device__ __forceinline__ int64_t red_offset(const RedRegs &g, const KView &rv, uint32_t r, int64_t &rank) {
+    if constexpr (!GEN) {  // idx1 = r / count0 (< count1 for r in range), idx0 = r % count0
+        const uint32_t q = g.nd == 2 ? udiv(r, g.m0) : 0u;
+        const uint32_t idx0 = r - q * g.c0;
+        if (RANK) rank = g.r0 + (int64_t)idx0 * g.s0 + (int64_t)q * g.s1;
+        return (int64_t)idx0 * g.v0 + (int64_t)q * g.v1;
+    } else {
+        return red_offset<RANK>(rv, r, rank);
+    }
+}
+
+template <typename T, int OP, int MK>
+__device__ __forceinline__ void fold_in(Red<T, OP> &r, const KMissing &miss, T x, int64_t rank) {
+    if (!included_mk<T, MK>(miss, x, false)) return;
     if constexpr (OP == OP_COUNT) r.cnt += 1;
     else r.add(x, [&]() { return rank; });
 }
 
-template <typename T, int OP, bool FUSED, int VW>
+template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK>
 __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
     constexpr int kU = 4;
@@ -78,7 +112,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     const uint32_t l = lane & (L - 1), g = lane / L;
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
     const uint64_t items = a.n_out * a.slices;
-    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    RedRegs rg;
+    rg.load(a.red);
     const uint64_t nrv = a.n_red / VW;  // reduced vectors per output
     // only float min/max can report an error (NaN); the host clears the status word for those
     if (!RANK && blockIdx.x == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;
@@ -97,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
             for (int u = 0; u < kU; ++u) {
                 uint64_t rv = r0 + (uint64_t)u * L;
                 if (rv >= r_hi) rv = r0;  // clamped: every load issues, the value is dropped below
-                off[u] = koff + red_offset<RANK>(a.red, (uint32_t)(rv * VW), rk[u]);
+                off[u] = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)(rv * VW), rk[u]);
             }
             Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
@@ -108,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
                 T x[VW];
                 raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) fold_in(r, a.miss, miss, x[j], rk[u] + (int64_t)j * a.red.rstride[0]);
+                for (int j = 0; j < VW; ++j) fold_in<T, OP, MK>(r, a.miss, x[j], rk[u] + (int64_t)j * rg.s0);
             }
         }
         group_reduce(r, L);
@@ -167,7 +202,7 @@ __device__ __forceinline__ void cols_combine(Red<T, OP> (&r)[VW], uint64_t *lds,
     }
 }
 
-template <typename T, int OP, bool FUSED, int VW>
+template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK>
 __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
     constexpr int kU = VW * sizeof(T) >= 16 ? 8 : 16;   // loads in flight per lane
@@ -183,7 +218,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     const uint64_t s = blockIdx.y;
     if (!RANK && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;
     const bool active = kv < nkv;
-    const bool miss = a.miss.kind != RDX_MISSING_NONE;
+    RedRegs rg;
+    rg.load(a.red);
     int64_t oi = 0, koff = 0;
     if (active) koff = kept_offset(a.kept, (uint32_t)(kv * VW), oi);
     const uint64_t r_lo = s * a.n_red / a.slices, r_hi = (s + 1) * a.n_red / a.slices;
@@ -198,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             for (int u = 0; u < kU; ++u) {
                 uint64_t rr = r0 + (uint64_t)u * step;
                 if (rr >= r_hi) rr = r0;  // clamped: every load issues, the value is dropped below
-                off[u] = koff + red_offset<RANK>(a.red, (uint32_t)rr, rk[u]);
+                off[u] = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)rr, rk[u]);
             }
             Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
@@ -209,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
                 T x[VW];
                 raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) fold_in(r[j], a.miss, miss, x[j], rk[u]);
+                for (int j = 0; j < VW; ++j) fold_in<T, OP, MK>(r[j], a.miss, x[j], rk[u]);
             }
         }
     }
@@ -272,8 +308,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     }
 }
 
-template <typename T, int OP, int VW>
-void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
+template <typename T, int OP, int VW, bool GEN, int MK>
+void launch_axis_k(const KAxis &a, int cus, hipStream_t st) {
     const dim3 block(kBlock);
     if (a.mode == 0) {
         const uint64_t waves = (a.n_out * a.slices + 64 / a.group - 1) / (64 / a.group);
@@ -281,12 +317,25 @@ void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
         const uint64_t cap = (uint64_t)cus * 16;
         if (blocks > cap) blocks = cap;
         if (blocks == 0) blocks = 1;
-        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true, 1>), dim3((uint32_t)blocks), block, 0, st, a);
-        else hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW>), dim3((uint32_t)blocks), block, 0, st, a);
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true, 1, GEN, MK>), dim3((uint32_t)blocks), block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW, GEN, MK>), dim3((uint32_t)blocks), block, 0, st, a);
     } else {
         const dim3 grid((uint32_t)((a.n_out / VW + a.group - 1) / a.group), a.slices);
-        if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((k_axis_cols<T, OP, false, VW>), grid, block, 0, st, a);
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1, GEN, MK>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_cols<T, OP, false, VW, GEN, MK>), grid, block, 0, st, a);
+    }
+}
+
+template <typename T, int OP, int VW>
+void launch_axis_vw(const KAxis &a, int cus, hipStream_t st) {
+    const bool gen = a.red.ndim > 2;
+    switch (miss_kind_of(a.miss.kind) * 2 + (gen ? 1 : 0)) {
+        case MK_NONE * 2: launch_axis_k<T, OP, VW, false, MK_NONE>(a, cus, st); break;
+        case MK_NONE * 2 + 1: launch_axis_k<T, OP, VW, true, MK_NONE>(a, cus, st); break;
+        case MK_CMP * 2: launch_axis_k<T, OP, VW, false, MK_CMP>(a, cus, st); break;
+        case MK_CMP * 2 + 1: launch_axis_k<T, OP, VW, true, MK_CMP>(a, cus, st); break;
+        case MK_ANY * 2: launch_axis_k<T, OP, VW, false, MK_ANY>(a, cus, st); break;
+        default: launch_axis_k<T, OP, VW, true, MK_ANY>(a, cus, st); break;
     }
 }
 

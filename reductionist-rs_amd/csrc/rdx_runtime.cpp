@@ -48,6 +48,7 @@ struct Tuning {
     int no_vec = env_int("RDX_NO_VEC", 0);
     int axis_rows_waves = env_int("RDX_AXIS_ROWS_WAVES_PER_CU", 16);   // sliced-rows fill target
     int axis_cols_wgs = env_int("RDX_AXIS_COLS_WGS_PER_CU", 4);        // sliced-cols fill target
+    int axis_cols_vw = env_int("RDX_AXIS_COLS_VW", 0);                 // tuning only: force the cols lane width
     int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
 };
 
@@ -310,6 +311,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 uint64_t best_wgs = 0;
                 for (uint32_t vw = vmax; vw >= 1; vw /= 2) {
                     if (!vec_ok(vw)) continue;
+                    if (tuning().axis_cols_vw && vw != (uint32_t)tuning().axis_cols_vw) continue;
                     const uint64_t nkv = a.n_out / vw;
                     uint32_t W = 64;
                     while (W > 1 && W / 2 >= nkv) W /= 2;
