@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
         if (lane == 0) {
             store_packed<T, OP, true>(a.out.partials + it * kW, r);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t *tk = a.out.tickets + o;
+            uint32_t *tk = a.out.tickets + o * kTicketStride;   // one L2 line per counter: same-line atomics serialise
             last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
             if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
-            uint32_t *tk = a.out.tickets + blockIdx.x;
+            uint32_t *tk = a.out.tickets + blockIdx.x * kTicketStride;
             const bool last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
             if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_last = last;

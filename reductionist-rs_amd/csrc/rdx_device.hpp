@@ -513,7 +513,12 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
             reinterpret_cast<T *>(out.body + chunk * out.body_stride)[0] = acc.value();
         }
         out.counts[chunk * out.counts_stride] = acc.cnt;
-        if (out.status) out.status[chunk] = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
+        if (out.status) {
+            const uint32_t e = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
+            if (!out.status_any) out.status[chunk] = e;
+            else if (e) __hip_atomic_fetch_or(out.status, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (!Red<T, OP>::kRank && chunk == 0) out.status[0] = 0;   // nothing can fail
+        }
         __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

@@ -53,6 +53,9 @@ struct KOut {
     uint64_t counts_stride;   // elements between consecutive chunks' counts (batch)
     uint64_t *partials;       // [chunk][block] x kPartialWords
     uint32_t *tickets;        // [chunk][kTicketWords] arrival counters, self-resetting
+    uint32_t status_any;      // 1: one status word for all chunks (chunks = outputs of an axis
+                              // reduction), NaN ORed in; the caller clears it when a NaN can set it
+    uint32_t pad;
 };
 
 // Reduction over ALL axes of a view whose elements form one ascending contiguous run

@@ -49,7 +49,10 @@ struct Tuning {
     int axis_rows_waves = env_int("RDX_AXIS_ROWS_WAVES_PER_CU", 16);   // sliced-rows fill target
     int axis_cols_wgs = env_int("RDX_AXIS_COLS_WGS_PER_CU", 4);        // sliced-cols fill target
     int axis_cols_vw = env_int("RDX_AXIS_COLS_VW", 0);                 // tuning only: force the cols lane width
+    int axis_fold_kib = env_int("RDX_AXIS_FOLD_KIB", 64);              // cols fold bytes per tile (x2 with >= 8 streams)
     int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
+    // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
+    int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
 };
 
 const Tuning &tuning() {
@@ -121,7 +124,8 @@ rdx_status ensure(rdx_workspace *ws, DevBuf<T> &b, size_t n, hipStream_t s, bool
     RDX_HIP(hipMalloc(&p, want * sizeof(T)));
     b.p = static_cast<T *>(p);
     b.cap = want;
-    if (zero) RDX_HIP(hipMemset(b.p, 0, want * sizeof(T)));
+    // on the work stream: a null-stream memset is not ordered before kernels on a non-blocking stream
+    if (zero) RDX_HIP(hipMemsetAsync(b.p, 0, want * sizeof(T), s));
     (void)ws;
     return RDX_OK;
 }
@@ -275,6 +279,50 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                                   (p.op == RDX_OP_MIN || p.op == RDX_OP_MAX);
             if (d_status && (can_fail || a.n_out == 0)) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
             if (a.n_out == 0) return RDX_OK;
+            // Few long contiguous rows (the reduced axes form one unit-stride run per output): each
+            // row is a chunk of the batched all-axes kernel, which streams at the contiguous read
+            // rate and folds through the sharded hand-off instead of one wave per output's slices.
+            const uint64_t rb_min = (uint64_t)tuning().axis_rowbatch_kib * 1024;
+            if (rb_min && a.mode == 0 && a.red.ndim == 1 && a.red.vstride[0] == 1 && a.n_red * p.esz >= rb_min &&
+                a.n_out <= (uint64_t)ws->cus * 4) {
+                std::vector<const uint8_t *> rows(a.n_out);
+                for (uint64_t t = 0; t < a.n_out; ++t) {
+                    int64_t off = a.kept.base_off, oi = 0;
+                    uint64_t q = t;
+                    for (int k = 0; k < a.kept.ndim; ++k) {
+                        const uint64_t idx = q % a.kept.count[k];
+                        q /= a.kept.count[k];
+                        off += (int64_t)idx * a.kept.vstride[k];
+                        oi += (int64_t)idx * a.kept.rstride[k];
+                    }
+                    rows[(uint64_t)oi] = src + off * (p.fused ? 1 : (int64_t)p.esz);
+                }
+                KAllContig c{};
+                c.off = 0;
+                c.n = a.n_red;
+                c.r0 = a.red.r0;
+                c.rs = a.red.rstride[0];
+                c.filter_semantics = 0;   // fold semantics, as k_axis.hip fold_in
+                const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
+                c.blocks_per_chunk = pick_bpc((c.n + te - 1) / te, a.n_out, ws->cus);
+                if ((st = ensure(ws, ws->ptrs, a.n_out, s))) return st;
+                if ((st = upload(ws, (void *)ws->ptrs.p, rows.data(), a.n_out * sizeof(void *), ws->last_ptrs, s)))
+                    return st;
+                if ((st = ensure(ws, ws->partials, a.n_out * c.blocks_per_chunk * kPartialWords, s))) return st;
+                if ((st = ensure(ws, ws->tickets, a.n_out * kTicketWords, s, true))) return st;
+                c.src = ksrc;
+                c.src.base = nullptr;
+                c.src.ptrs = ws->ptrs.p;
+                c.miss = miss;
+                c.out = out;
+                c.out.body_stride = p.op == RDX_OP_COUNT ? 8 : p.esz;
+                c.out.counts_stride = 1;
+                c.out.status_any = 1;
+                c.out.partials = ws->partials.p;
+                c.out.tickets = ws->tickets.p;
+                RDX_HIP(launch_all_contig(p.dtype, p.op, c, (uint32_t)a.n_out, s));
+                return RDX_OK;
+            }
             uint64_t slices = 1;
             // vw-element lanes when every stride keeps vectors aligned and inside one dim
             auto vec_ok = [&](uint32_t vw) {
@@ -303,20 +351,26 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 // Tile width W lanes x vw outputs; slices of the reduced rows fill the chip, bounded so
                 // that the last slice's fold (one workgroup, 256/W parallel slice streams) stays short:
                 // fold bytes per tile <= 64 KiB (128 KiB with >= 8 streams), <= 16 slices per stream.
+                // (A two-level fold over slice groups, measured this round, did not beat this bound.)
                 const bool frank = (p.dtype == RDX_DTYPE_FLOAT32 || p.dtype == RDX_DTYPE_FLOAT64) &&
                                    (p.op == RDX_OP_MIN || p.op == RDX_OP_MAX);
                 const uint64_t rec = 8 * ((p.op != RDX_OP_COUNT) + (p.op == RDX_OP_SUM && p.dtype == RDX_DTYPE_FLOAT64) +
                                           1 + (frank ? 3 : 0));
                 const uint64_t target = (uint64_t)ws->cus * tuning().axis_cols_wgs;      // workgroups
                 uint64_t best_wgs = 0;
-                for (uint32_t vw = vmax; vw >= 1; vw /= 2) {
+                // at most 2 outputs per lane: 4-wide f32 lanes stream as fast but double the slice
+                // records each lane publishes and folds (axis0 4096^2 f32: 20 vs 32 us, 64x1024x256
+                // axis 1: 20 vs 26 us, tools/gpu_foldkib.sh)
+                const uint32_t vtop = tuning().axis_cols_vw ? vmax : std::min<uint32_t>(vmax, 2);
+                for (uint32_t vw = vtop; vw >= 1; vw /= 2) {
                     if (!vec_ok(vw)) continue;
                     if (tuning().axis_cols_vw && vw != (uint32_t)tuning().axis_cols_vw) continue;
                     const uint64_t nkv = a.n_out / vw;
                     uint32_t W = 64;
                     while (W > 1 && W / 2 >= nkv) W /= 2;
                     const uint64_t tiles = (nkv + W - 1) / W, G = kBlock / W, R = 64 / W;
-                    const uint64_t budget = std::min<uint64_t>(65536 * std::max<uint64_t>(1, G / 4), 131072);
+                    const uint64_t fold = (uint64_t)tuning().axis_fold_kib * 1024;
+                    const uint64_t budget = std::min<uint64_t>(fold * std::max<uint64_t>(1, G / 4), 2 * fold);
                     const uint64_t smax = std::max<uint64_t>(
                         1, std::min({budget / (W * vw * rec), 16 * G, a.n_red / (16 * R)}));
                     const uint64_t sl = std::max<uint64_t>(1, std::min((target + tiles - 1) / tiles, smax));
@@ -332,12 +386,12 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             }
             slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, 65535));
             a.slices = (uint32_t)slices;
-            if (slices > 1) {   // partial records + one self-resetting arrival counter per output / tile
+            if (slices > 1) {   // partial records + a self-resetting arrival counter (own L2 line) per output / tile
                 const uint64_t tiles = (a.n_out / a.vec + a.group - 1) / a.group;
                 const uint64_t recs = a.mode == 0 ? a.n_out : tiles * a.group * a.vec;
                 if ((st = ensure(ws, ws->partials, recs * slices * kPartialWords, s))) return st;
-                if ((st = ensure(ws, ws->tickets, std::max<uint64_t>(a.mode == 0 ? a.n_out : tiles, kTicketWords), s,
-                                 true)))
+                if ((st = ensure(ws, ws->tickets, std::max<uint64_t>((a.mode == 0 ? a.n_out : tiles) * kTicketStride, kTicketWords),
+                                 s, true)))
                     return st;
                 out.partials = ws->partials.p;
                 out.tickets = ws->tickets.p;

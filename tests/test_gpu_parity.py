@@ -162,6 +162,8 @@ def test_nan_raises_like_reference_panic(engine):
     ([64, 512, 96], 1, "uint64", "count"),    # cols over a middle axis, missing filter
     ([8, 4096, 3], 1, "float32", "max"),      # odd inner width, scalar lanes
     ([40000, 2], 0, "int64", "sum"),          # 2 outputs
+    ([50001, 6], 0, "float32", "max"),        # 1-lane tile, ragged slices
+    ([30000, 64], 0, "int32", "sum"),         # 16-B lanes, many slices per tile
 ])
 def test_cols_tilings(engine, shape, axis, dtype, op):
     """Column-mode tile shapes (k_axis_cols): W lanes x VW outputs, several rows per wave access,
@@ -177,6 +179,43 @@ def test_cols_tilings(engine, shape, axis, dtype, op):
         v[rng.integers(0, n, 50)] = 0.0
         v[rng.integers(0, n, 50)] = -0.0           # ±0 ties across slices
     assert_parity(engine, op, req, v.tobytes())
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_row_batch(engine, case):
+    """Few long contiguous rows (>= 64 KiB reduced per output) go to the batched all-axes kernel,
+    one chunk per output (rdx_runtime.cpp, Mode::Axis): selections on the kept and reduced dims,
+    reversed reduced axis, F order, shuffle + big-endian, missing data, ±0 ties, NaN."""
+    dtype, op, shape, sel, axis, order, extra = [
+        ("float32", "sum", [6, 40000], None, 1, "C", {}),
+        ("float64", "max", [5, 16411], None, 1, "C", {}),                         # unaligned rows
+        ("float32", "min", [7, 30001], [[1, 7, 2], [3, 29990, 1]], 1, "C", {}),    # strided kept, offset rows
+        ("int32", "max", [4, 50000], [[0, 4, 1], [49999, 10, -1]], 1, "C", {}),    # reversed reduced axis
+        ("int64", "sum", [20000, 3], None, 0, "F", {}),
+        ("uint32", "count", [3, 70000], None, 1, "C", {"missing": {"valid_min": 40}}),
+        ("float32", "max", [4, 65536], None, 1, "C", {"byte_order": "big",
+                                                     "filters": [{"id": "shuffle", "element_size": 4}]}),
+        ("uint64", "min", [2, 3, 20000], None, 2, "C", {"missing": {"missing_values": [7, 9]}}),
+        ("float64", "min", [3, 9000], None, 1, "C", {}),                          # NaN -> status
+        ("float32", "select", [4, 40000], None, 1, "C", {}),
+    ][case]
+    rng = np.random.default_rng(100 + case)
+    n = int(np.prod(shape))
+    v = rng.integers(-100, 100, n).astype(NP[dtype]) if not dtype.startswith("u") else \
+        rng.integers(0, 100, n).astype(NP[dtype])
+    if dtype.startswith("float") and op in ("min", "max"):
+        v[rng.integers(0, n, 200)] = 0.0
+        v[rng.integers(0, n, 200)] = -0.0
+        if case == 8:
+            v[n // 2 + 17] = np.nan
+    req = {"dtype": dtype, "shape": shape, "axis": axis, "order": order, **extra}
+    if sel:
+        req["selection"] = sel
+    raw = v.astype(NP[dtype]).tobytes()
+    if req.get("byte_order") == "big":
+        raw = v.astype(np.dtype(NP[dtype]).newbyteorder(">")).tobytes()
+    data = encode_filters(raw, req.get("filters"), oracle.shuffle)
+    assert_parity(engine, op, req, data)
 
 
 def test_long_missing_values_list(engine):
