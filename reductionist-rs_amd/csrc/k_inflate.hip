@@ -69,11 +69,18 @@ __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_re
 __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
     return (uint64_t)rfl((uint32_t)(x >> 32)) << 32 | rfl((uint32_t)x);
 }
+// LDS byte address of a __shared__ object (the address operand of ds_* instructions)
+template <class P>
+__device__ __forceinline__ uint32_t lds_addr(P *p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void *)p;
+}
 
 // Decode-table entry: value (literal byte / length or distance base) in bits 0-15, code length in
 // 16-19 (0 = code longer than the root: bit-serial walk), extra bits in 20-23, type in 24-25
-// (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol).
-constexpr uint32_t kTypeLen = 1u << 24, kTypeEob = 2u << 24, kTypeBad = 3u << 24;
+// (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol).  A literal/length root entry
+// may hold TWO literals whose codes together fit the root: bytes in bits 0-7 and 8-15, the summed
+// length in 16-19, kPair (bit 20; literals have no extra bits) set.
+constexpr uint32_t kTypeLen = 1u << 24, kTypeEob = 2u << 24, kTypeBad = 3u << 24, kPair = 1u << 20;
 
 // Phase counters for tools/probe_inflate.hip (RDX_INFLATE_PROF); compiled out of the product.
 #ifdef RDX_INFLATE_PROF
@@ -433,35 +440,32 @@ struct Inflater {
             }
         }
         wave_sync();
+        if (kind == 1 && root == kLitRoot) {
+            // literal pairs: where a root entry is a literal of l1 bits and the next 10 - l1 bits
+            // start a literal code of l2 <= 10 - l1 bits (the entry at index >> l1 decodes it: its
+            // missing high bits are past that code), one lookup yields both
+            constexpr uint32_t kPer = (1u << kLitRoot) / 64;
+            uint32_t ent[kPer];
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint32_t i = k * 64 + lane;
+                uint32_t e1 = tab[i];
+                const uint32_t l1 = (e1 >> 16) & 15;
+                if (l1 && (e1 >> 24) == 0) {
+                    const uint32_t e2 = tab[i >> l1];
+                    const uint32_t l2 = (e2 >> 16) & 15;
+                    if (l2 && (e2 >> 24) == 0 && l1 + l2 <= kLitRoot)
+                        e1 = (e1 & 0xff) | (e2 & 0xff) << 8 | (l1 + l2) << 16 | kPair;
+                }
+                ent[k] = e1;
+            }
+            wave_sync();
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) tab[k * 64 + lane] = ent[k];
+            wave_sync();
+        }
         return left;
     }
-    // decode one symbol (needs >= 15 valid bits): root table, else the canonical bit-serial walk
-    __device__ __forceinline__ uint32_t decode(const uint32_t *tab, uint32_t root, const uint16_t *count,
-                                               const uint16_t *sym, uint32_t kind) {
-        const uint32_t e = rfl(tab[(uint32_t)bb & ((1u << root) - 1)]);
-        const uint32_t l = (e >> 16) & 15;
-        if (l) {
-            bb >>= l;
-            bc -= l;
-            return e;
-        }
-        PROF_ADD(P_SLOW, 1);
-        int code = 0, first = 0, index = 0;  // longer than the root: canonical bit-serial walk
-#pragma unroll 1
-        for (int len = 1; len < 16; ++len) {
-            code |= (int)(bb & 1);
-            bb >>= 1;
-            --bc;
-            const int c = (int)rfl(count[len]);
-            if (code - c < first) return entry_of(rfl(sym[index + (code - first)]), kind);
-            index += c;
-            first += c;
-            first <<= 1;
-            code <<= 1;
-        }
-        return kTypeBad;
-    }
-
     // ---- blocks ------------------------------------------------------------------------------------
     __device__ __forceinline__ void fixed_tables() {
         for (uint32_t s = lane; s < 288 + 30; s += 64)
@@ -587,6 +591,82 @@ struct Inflater {
         return kTypeBad;
     }
 
+    // The literal run of hot(), in GCN assembly: the compiler's version of this loop carried ~47
+    // instructions per literal (phi copies between SGPRs, a spilled exec mask for lane 0's store);
+    // this one ~30 per root-table entry, and an entry may hold two literals (build()).  State: the
+    // bit buffer pinned to s[80:81], valid bits c, input position p / output position o (low 32
+    // bits), countdowns rp / ro; scratch s82-s84.  Per iteration: refill from the input ring when
+    // c <= 32 (stop at rp < 0), look the next 10 bits up in the literal/length table, and while the
+    // entry is a literal (pair), store it to the window ring (lane j writes byte j; exec = the
+    // literal count) and consume it.  Leaves with why = 1 at a limit (ro < 0, or a refill due with
+    // rp < 0), or why = 0 and the entry e of a non-literal symbol, not consumed, refill done.
+    __device__ __forceinline__ void literal_run(uint64_t &b, uint32_t &c, uint32_t &p32, uint32_t &o32, int32_t &rp,
+                                                int32_t &ro, uint32_t &e, uint32_t &why, uint32_t v_in, uint32_t v_lit,
+                                                uint32_t v_win, uint32_t v_lane, uint32_t v_sh) {
+        static_assert(kWinMask == 0x1fff && kInWords * 4 == 0x800 && kLitRoot == 10, "masks hard-coded below");
+        uint32_t va, vv, t0, t1, t2;
+        uint64_t sav;
+        asm volatile(
+            "1:\n"
+            "  s_cmp_lt_i32 %[ro], 0\n"
+            "  s_cbranch_scc1 8f\n"
+            "  s_cmp_gt_u32 %[c], 32\n"
+            "  s_cbranch_scc1 2f\n"
+            "  s_cmp_lt_i32 %[rp], 0\n"
+            "  s_cbranch_scc1 8f\n"
+            "  s_and_b32 s82, %[p], 0x7fc\n"
+            "  v_add_u32 %[va], s82, %[vin]\n"
+            "  ds_read_b32 %[vv], %[va]\n"
+            "  s_waitcnt lgkmcnt(0)\n"
+            "  v_readfirstlane_b32 s82, %[vv]\n"
+            "  s_mov_b32 s83, 0\n"
+            "  s_lshl_b64 s[82:83], s[82:83], %[c]\n"
+            "  s_or_b64 s[80:81], s[80:81], s[82:83]\n"
+            "  s_add_u32 %[p], %[p], 4\n"
+            "  s_sub_i32 %[rp], %[rp], 4\n"
+            "  s_add_u32 %[c], %[c], 32\n"
+            "2:\n"
+            "  s_and_b32 s82, s80, 0x3ff\n"
+            "  v_lshl_add_u32 %[va], s82, 2, %[vlit]\n"
+            "  ds_read_b32 %[vv], %[va]\n"
+            "  v_add_u32 %[va], %[o], %[vlane]\n"
+            "  v_and_b32 %[va], 0x1fff, %[va]\n"
+            "  v_add_u32 %[va], %[va], %[vwin]\n"
+            "  s_waitcnt lgkmcnt(0)\n"
+            "  v_readfirstlane_b32 %[e], %[vv]\n"
+            "  s_bfe_u32 s82, %[e], 0x40010\n"
+            "  s_cmp_eq_u32 s82, 0\n"
+            "  s_cbranch_scc1 9f\n"
+            "  s_cmp_gt_u32 %[e], 0xffffff\n"
+            "  s_cbranch_scc1 9f\n"
+            "  s_bfe_u32 s83, %[e], 0x10014\n"
+            "  s_add_u32 s83, s83, 1\n"
+            "  s_bfm_b32 s84, s83, 0\n"
+            "  v_lshrrev_b32 %[vv], %[vsh], %[e]\n"
+            "  s_mov_b64 %[sav], exec\n"
+            "  s_mov_b32 exec_lo, s84\n"
+            "  s_mov_b32 exec_hi, 0\n"
+            "  ds_write_b8 %[va], %[vv]\n"
+            "  s_mov_b64 exec, %[sav]\n"
+            "  s_lshr_b64 s[80:81], s[80:81], s82\n"
+            "  s_sub_u32 %[c], %[c], s82\n"
+            "  s_add_u32 %[o], %[o], s83\n"
+            "  s_sub_i32 %[ro], %[ro], s83\n"
+            "  s_branch 1b\n"
+            "8:\n"
+            "  s_mov_b32 %[why], 1\n"
+            "  s_branch 10f\n"
+            "9:\n"
+            "  s_mov_b32 %[why], 0\n"
+            "10:\n"
+            "  s_waitcnt lgkmcnt(0)\n"
+            : [b] "+{s[80:81]}"(b), [c] "+s"(c), [p] "+s"(p32), [o] "+s"(o32), [rp] "+s"(rp), [ro] "+s"(ro),
+              [e] "=&s"(e), [why] "=&s"(why), [sav] "=&s"(sav), [va] "=&v"(va), [vv] "=&v"(vv), [t0] "={s82}"(t0),
+              [t1] "={s83}"(t1), [t2] "={s84}"(t2)
+            : [vin] "v"(v_in), [vlit] "v"(v_lit), [vwin] "v"(v_win), [vlane] "v"(v_lane), [vsh] "v"(v_sh)
+            : "memory", "scc");
+    }
+
     // The symbol loop of one Huffman block, in two tiers.  A wave issues one instruction per 4 cycles
     // at best, so the serial decode is paid per INSTRUCTION: hot() keeps the whole state in a handful
     // of scalar locals and handles only the common cases (literals, and matches whose codes hit the
@@ -594,8 +674,10 @@ struct Inflater {
     // flushing, codes longer than the root, end of block, capacity, errors) leaves hot() WITHOUT
     // consuming the symbol, and general() decodes that one symbol with every check.
     __device__ __forceinline__ void hot() {
-        uint64_t b = bb, p = pos, o = out;
-        uint32_t c = bc;
+        // loop-carried state uniform from the start: phis of SGPR values stay in SGPRs (re-reading
+        // them with readfirstlane at the loop head instead makes the compiler carry VGPR copies)
+        uint64_t b = rfl64(bb), p = rfl64(pos), o = rfl64(out);
+        uint32_t c = rfl(bc);
         const uint64_t stop_p = rfl64(staged) - 8;  // a dword refill needs p + 8 <= staged
         const uint64_t fl = rfl64(flushed) + kFlush, cp = rfl64(cap);
         const uint64_t lim = fl < cp ? fl : cp;
@@ -604,38 +686,24 @@ struct Inflater {
         // 32-bit countdowns (SALU has no 64-bit ordered compare): input bytes left before a refill
         // would pass `staged`, output bytes left before the ring / capacity check is due
         const uint64_t dp = stop_p + 8 - p, dout = stop_o - o;
-        int32_t rp = (int32_t)(dp < 0x40000000u ? dp : 0x40000000u) - 8;
-        int32_t ro = (int32_t)(dout < 0x40000000u ? dout : 0x40000000u);
-        const uint32_t o_lane = lane;
+        int32_t rp = (int32_t)rfl((uint32_t)((int32_t)(dp < 0x40000000u ? dp : 0x40000000u) - 8));
+        int32_t ro = (int32_t)rfl((uint32_t)(dout < 0x40000000u ? dout : 0x40000000u));
+        const uint32_t v_in = lds_addr(L.in), v_lit = lds_addr(L.lit), v_win = lds_addr(L.win);
+        const uint32_t v_lane = lane, v_sh = lane * 8;
         for (;;) {
             asm volatile("; inflate hot loop" ::: "memory");
-            b = rfl64(b);
-            c = rfl(c);
-            p = rfl64(p);
-            o = rfl64(o);
-            rp = (int32_t)rfl((uint32_t)rp);
-            ro = (int32_t)rfl((uint32_t)ro);
-            if (ro < 0) break;
-            if (c <= 32) {
-                if (rp < 0) break;
-                b |= (uint64_t)rfl(L.in[(uint32_t)(p >> 2) & (kInWords - 1)]) << c;
-                p += 4;
-                rp -= 4;
-                c += 32;
-            }
-            const uint32_t e = rfl(L.lit[(uint32_t)b & ((1u << kLitRoot) - 1)]);
+            // literals, hand-scheduled (literal_run below); ring / input positions travel as their low
+            // 32 bits (all the ring masks need), advanced here by what the run consumed
+            uint32_t p32 = (uint32_t)p, o32 = (uint32_t)o, e, why;
+            const uint32_t p0 = p32, o0 = o32;
+            literal_run(b, c, p32, o32, rp, ro, e, why, v_in, v_lit, v_win, v_lane, v_sh);
+            p += p32 - p0;
+            o += o32 - o0;
+            PROF_ADD(P_LIT, o32 - o0);
+            if (why) break;
             const uint32_t l = (e >> 16) & 15;
             if (l == 0) break;
             const uint32_t type = e >> 24;
-            if (type == 0) {
-                PROF_ADD(P_LIT, 1);
-                b >>= l;
-                c -= l;
-                if (o_lane == 0) L.win[(uint32_t)o & kWinMask] = (uint8_t)e;
-                ++o;
-                --ro;
-                continue;
-            }
             if (type != 1) break;
             uint64_t b2 = b >> l;
             uint32_t c2 = c - l;
@@ -693,6 +761,7 @@ struct Inflater {
         if (type == 0) {
             PROF_ADD(P_LIT, 1);
             literal(e & 0xff);
+            if (e & kPair) literal((e >> 8) & 0xff);
             return err != 0;
         }
         if (type == kTypeEob) return true;
