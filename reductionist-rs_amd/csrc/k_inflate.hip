@@ -77,15 +77,16 @@ __device__ __forceinline__ uint32_t lds_addr(P *p) {
 
 // Decode-table entry: value (literal byte / length or distance base) in bits 0-15, code length in
 // 16-19 (0 = code longer than the root: bit-serial walk), extra bits in 20-23, type in 24-25
-// (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol).  A literal/length root entry
-// may hold TWO literals whose codes together fit the root: bytes in bits 0-7 and 8-15, the summed
-// length in 16-19, kPair (bit 20; literals have no extra bits) set.
-constexpr uint32_t kTypeLen = 1u << 24, kTypeEob = 2u << 24, kTypeBad = 3u << 24, kPair = 1u << 20;
+// (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol).  Literals have no extra bits:
+// their bits 20-21 hold the literal count instead, 1, or 2 for a literal/length root entry holding
+// TWO literals whose codes together fit the root (bytes in bits 0-7 and 8-15, the summed length in
+// 16-19).
+constexpr uint32_t kTypeLen = 1u << 24, kTypeEob = 2u << 24, kTypeBad = 3u << 24, kOneLit = 1u << 20, kPair = 2u << 20;
 
 // Phase counters for tools/probe_inflate.hip (RDX_INFLATE_PROF); compiled out of the product.
 #ifdef RDX_INFLATE_PROF
 enum { P_LIT, P_MATCH, P_MATCH_BYTES, P_FAR, P_SLOW, P_BLOCKS, P_STAGE, P_FLUSH, P_T_COPY, P_T_FLUSH, P_T_TABLES,
-       P_T_TOTAL, P_N };
+       P_T_STORED, P_T_GENERAL, P_T_TOTAL, P_N };
 __device__ unsigned long long g_prof[P_N];
 #define PROF_ADD(k, v) (prof[k] += (v))
 #define PROF_T0() const uint64_t _t0 = __builtin_readcyclecounter()
@@ -157,6 +158,8 @@ struct Inflater {
     const uint32_t *srcw;
     uint64_t end;     // skew + length: first byte past the stream (aligned-stream coordinates)
     uint64_t staged;  // aligned-stream bytes [.., staged) are in the ring
+    uint64_t pf_start;             // the unit whose words are in flight into pf (~0: none)
+    uint32_t pf[kStage / 4 / 64];  // this lane's words of that unit
     uint64_t pos;     // next byte to move into the bit buffer
     uint64_t bb;      // bit buffer (LSB first)
     uint32_t bc;      // valid bits in bb
@@ -172,23 +175,34 @@ struct Inflater {
 #endif
 
     // ---- input -----------------------------------------------------------------------------------
-    __device__ __forceinline__ void stage() {  // stage [start, start + kStage) with start >= pos rounded down
-        PROF_ADD(P_STAGE, 1);
-        uint64_t start = pos & ~(uint64_t)(kStage - 1);
-        if (start < staged) start = staged;
+    // One kStage unit of the input as this lane's words (lane-contiguous), bytes past the stream zeroed.
+    __device__ __forceinline__ void load_unit(uint64_t start, uint32_t (&v)[kStage / 4 / 64]) const {
         const uint64_t w0 = start / 4 + (uint64_t)lane * (kStage / 4 / 64);
 #pragma unroll
         for (int k = 0; k < (int)(kStage / 4 / 64); ++k) {
             const uint64_t w = w0 + k;
-            uint32_t v = 0;
+            v[k] = 0;
             if (w * 4 < end) {
-                v = gld<uint32_t>(srcw + w);
+                v[k] = gld<uint32_t>(srcw + w);
                 const uint64_t valid = end - w * 4;  // zero the bytes past the stream
-                if (valid < 4) v &= (1u << (8 * valid)) - 1;
+                if (valid < 4) v[k] &= (1u << (8 * valid)) - 1;
             }
-            L.in[w & (kInWords - 1)] = v;
         }
+    }
+    // Stage [start, start + kStage) with start >= pos rounded down into the input ring, then start
+    // loading the unit after it: the next stage finds it in registers instead of waiting a full
+    // memory round trip (1-2 us per KiB of input otherwise, a third of the decode time at ratio 1).
+    __device__ __forceinline__ void stage() {
+        PROF_ADD(P_STAGE, 1);
+        uint64_t start = pos & ~(uint64_t)(kStage - 1);
+        if (start < staged) start = staged;
+        if (start != pf_start) load_unit(start, pf);
+        const uint32_t i0 = (uint32_t)(start / 4 + (uint64_t)lane * (kStage / 4 / 64));
+#pragma unroll
+        for (int k = 0; k < (int)(kStage / 4 / 64); ++k) L.in[(i0 + k) & (kInWords - 1)] = pf[k];
         staged = start + kStage;
+        pf_start = staged;
+        load_unit(pf_start, pf);
         wave_sync();
     }
     __device__ __forceinline__ uint32_t word_at(uint64_t p) const {
@@ -298,10 +312,11 @@ struct Inflater {
         wave_sync();
         PROF_T1(P_T_FLUSH);
     }
-    // Flushing happens at ONE place per loop (the top of the symbol loop / stored-copy loop), so the
-    // flush code is inlined once there instead of behind every literal and copy; between two checks
-    // at most one copy (<= 258 bytes) is added, so the unflushed tail stays < kFlush + 258 bytes and
-    // never reaches ring slots that still hold unflushed output.
+    // Flushing happens at ONE place per loop (general() / the stored-copy loop), so the flush code is
+    // inlined once there instead of behind every literal and copy.  The unflushed tail stays below
+    // kWin: hot() stops at kWin - 258 (one match of room), general() and stored() add at most one
+    // copy (<= 258 bytes) after a flush_full(); so no write reaches a ring slot still unflushed, and
+    // a source farther back than the ring is always already in HBM.
     __device__ __forceinline__ void flush_full() {
         while (out - flushed >= kFlush) flush(kFlush);
     }
@@ -337,8 +352,8 @@ struct Inflater {
                 }
                 const uint32_t back = dist - m;  // source = o - back
                 // the ring holds [frontier - kWin, frontier), the frontier having advanced by the j0
-                // bytes this copy already wrote; anything older is flushed to HBM (o - flushed <
-                // kFlush + 258, j0 < 258, kWin >= kFlush + 516)
+                // bytes this copy already wrote; anything older is flushed to HBM (o - flushed <=
+                // kWin - 258 and j0 <= 256, flush_full())
                 uint8_t v;
                 if (back + j0 <= kWin) [[likely]] v = L.win[(o32 - back) & kWinMask];
                 else v = gld<uint8_t>(dst + (o - back));
@@ -360,7 +375,7 @@ struct Inflater {
     // table entry of symbol s: kind 0 = code-length code (value = s), 1 = literal/length, 2 = distance
     __device__ __forceinline__ uint32_t entry_of(uint32_t s, uint32_t kind) const {
         if (kind == 1) {
-            if (s < 256) return s;
+            if (s < 256) return s | kOneLit;
             if (s == 256) return kTypeEob;
             if (s < 286) {
                 const uint32_t lb = S.lbase[s - 257];
@@ -591,41 +606,69 @@ struct Inflater {
         return kTypeBad;
     }
 
-    // The literal run of hot(), in GCN assembly: the compiler's version of this loop carried ~47
-    // instructions per literal (phi copies between SGPRs, a spilled exec mask for lane 0's store);
-    // this one ~30 per root-table entry, and an entry may hold two literals (build()).  State: the
-    // bit buffer pinned to s[80:81], valid bits c, input position p / output position o (low 32
-    // bits), countdowns rp / ro; scratch s82-s84.  Per iteration: refill from the input ring when
-    // c <= 32 (stop at rp < 0), look the next 10 bits up in the literal/length table, and while the
-    // entry is a literal (pair), store it to the window ring (lane j writes byte j; exec = the
-    // literal count) and consume it.  Leaves with why = 1 at a limit (ro < 0, or a refill due with
-    // rp < 0), or why = 0 and the entry e of a non-literal symbol, not consumed, refill done.
-    __device__ __forceinline__ void literal_run(uint64_t &b, uint32_t &c, uint32_t &p32, uint32_t &o32, int32_t &rp,
-                                                int32_t &ro, uint32_t &e, uint32_t &why, uint32_t v_in, uint32_t v_lit,
-                                                uint32_t v_win, uint32_t v_lane, uint32_t v_sh) {
-        static_assert(kWinMask == 0x1fff && kInWords * 4 == 0x800 && kLitRoot == 10, "masks hard-coded below");
-        uint32_t va, vv, t0, t1, t2;
-        uint64_t sav;
+    // The symbol loop of hot() in GCN assembly.  The compiler's version carried ~47 instructions per
+    // literal (phi copies between SGPRs, a spilled exec mask for lane 0's store) and a match went
+    // through ~1000 cycles of mixed scalar/vector code; here a literal (pair) is ~30 instructions
+    // and a near match ~45 plus its two LDS round trips.  State: the bit buffer pinned to s[80:81]
+    // (s[82:83] scratch), valid bits c (>= 33 at the loop top), input / output positions p / o as
+    // their low 32 bits (all the ring masks need), countdowns rp / ro (as in hot()).  Per symbol:
+    // look the next 10 bits up in the literal/length root table; a literal (pair) is stored to the
+    // window ring (lane j writes byte j, exec = the count); a length whose distance code hits the
+    // distance root table and whose source lies in the ring (dist <= kWin - 258) is copied ring to
+    // ring, 64 bytes per step (source o - dist + (j mod dist), always written history).  Leaves with
+    // why = 1 at a limit (ro < 0, or a refill due with rp < 0), why = 0 at a symbol for general()
+    // (long code, end of block, invalid, or a distance past the output start), nothing consumed;
+    // why = 2 after consuming a far match (len, dist) for copy_at() to take from HBM.
+    __device__ __forceinline__ void symbol_run(uint64_t &b, uint32_t &c, uint32_t &p32, uint32_t &o32, int32_t &rp,
+                                               int32_t &ro, uint32_t &why, uint32_t &len, uint32_t &dist,
+                                               uint32_t o_small, uint32_t v_in, uint32_t v_lit, uint32_t v_dst,
+                                               uint32_t v_win, uint32_t v_lane, uint32_t v_sh) {
+        static_assert(kWinMask == 0x1fff && kInWords * 4 == 0x800 && kLitRoot == 10 && kDistRoot == 8 &&
+                          kWin - 258 == 0x1efe,
+                      "masks hard-coded below");
+#define RDX_REFILL                             \
+    "  s_and_b32 s82, %[p], 0x7fc\n"           \
+    "  v_add_u32 %[vv], s82, %[vin]\n"         \
+    "  ds_read_b32 %[vv], %[vv]\n"             \
+    "  s_waitcnt lgkmcnt(0)\n"                 \
+    "  v_readfirstlane_b32 s82, %[vv]\n"       \
+    "  s_mov_b32 s83, 0\n"                     \
+    "  s_lshl_b64 s[82:83], s[82:83], %[c]\n"  \
+    "  s_or_b64 s[80:81], s[80:81], s[82:83]\n" \
+    "  s_add_u32 %[p], %[p], 4\n"              \
+    "  s_sub_i32 %[rp], %[rp], 4\n"            \
+    "  s_add_u32 %[c], %[c], 32\n"
+#define RDX_COPY_STEP(L)                        \
+    "  v_and_b32 %[vs], 0x1fff, %[vs]\n"        \
+    "  v_add_u32 %[vs], %[vs], %[vwin]\n"       \
+    "  v_add_u32 %[va], %[o], %[vj]\n"          \
+    "  v_and_b32 %[va], 0x1fff, %[va]\n"        \
+    "  v_add_u32 %[va], %[va], %[vwin]\n"       \
+    "  s_sub_u32 %[w], %[len], %[j]\n"          \
+    "  s_mov_b64 s[82:83], -1\n"                \
+    "  s_cmp_lt_u32 %[w], 64\n"                 \
+    "  s_cbranch_scc0 " L "f\n"                 \
+    "  s_bfm_b64 s[82:83], %[w], 0\n"           \
+    L ":\n"                                     \
+    "  s_mov_b64 exec, s[82:83]\n"              \
+    "  ds_read_u8 %[vv], %[vs]\n"               \
+    "  s_waitcnt lgkmcnt(0)\n"                  \
+    "  ds_write_b8 %[va], %[vv]\n"              \
+    "  s_mov_b64 exec, %[sav]\n"                \
+    "  s_add_u32 %[j], %[j], 64\n"              \
+    "  s_cmp_lt_u32 %[j], %[len]\n"
+        uint64_t sav, bs;
+        uint32_t t0, t1, e, u, w, j, od, rs, va, vv, vj, vq, vs, vr;
         asm volatile(
+            "  s_mov_b64 %[sav], exec\n"
+            "  s_cmp_gt_u32 %[c], 32\n"
+            "  s_cbranch_scc1 1f\n"
+            "  s_cmp_lt_i32 %[rp], 0\n"
+            "  s_cbranch_scc1 80f\n"
+            RDX_REFILL
             "1:\n"
             "  s_cmp_lt_i32 %[ro], 0\n"
-            "  s_cbranch_scc1 8f\n"
-            "  s_cmp_gt_u32 %[c], 32\n"
-            "  s_cbranch_scc1 2f\n"
-            "  s_cmp_lt_i32 %[rp], 0\n"
-            "  s_cbranch_scc1 8f\n"
-            "  s_and_b32 s82, %[p], 0x7fc\n"
-            "  v_add_u32 %[va], s82, %[vin]\n"
-            "  ds_read_b32 %[vv], %[va]\n"
-            "  s_waitcnt lgkmcnt(0)\n"
-            "  v_readfirstlane_b32 s82, %[vv]\n"
-            "  s_mov_b32 s83, 0\n"
-            "  s_lshl_b64 s[82:83], s[82:83], %[c]\n"
-            "  s_or_b64 s[80:81], s[80:81], s[82:83]\n"
-            "  s_add_u32 %[p], %[p], 4\n"
-            "  s_sub_i32 %[rp], %[rp], 4\n"
-            "  s_add_u32 %[c], %[c], 32\n"
-            "2:\n"
+            "  s_cbranch_scc1 80f\n"
             "  s_and_b32 s82, s80, 0x3ff\n"
             "  v_lshl_add_u32 %[va], s82, 2, %[vlit]\n"
             "  ds_read_b32 %[vv], %[va]\n"
@@ -634,37 +677,150 @@ struct Inflater {
             "  v_add_u32 %[va], %[va], %[vwin]\n"
             "  s_waitcnt lgkmcnt(0)\n"
             "  v_readfirstlane_b32 %[e], %[vv]\n"
-            "  s_bfe_u32 s82, %[e], 0x40010\n"
-            "  s_cmp_eq_u32 s82, 0\n"
-            "  s_cbranch_scc1 9f\n"
-            "  s_cmp_gt_u32 %[e], 0xffffff\n"
-            "  s_cbranch_scc1 9f\n"
-            "  s_bfe_u32 s83, %[e], 0x10014\n"
-            "  s_add_u32 s83, s83, 1\n"
-            "  s_bfm_b32 s84, s83, 0\n"
+            "  s_bfe_u32 %[u], %[e], 0x40010\n"
+            "  s_sub_u32 %[w], %[e], 0x10000\n"
+            "  s_cmp_lt_u32 %[w], 0xff0000\n"
+            "  s_cbranch_scc0 20f\n"
+            // literal (pair)
+            "  s_bfe_u32 %[w], %[e], 0x20014\n"
             "  v_lshrrev_b32 %[vv], %[vsh], %[e]\n"
-            "  s_mov_b64 %[sav], exec\n"
-            "  s_mov_b32 exec_lo, s84\n"
-            "  s_mov_b32 exec_hi, 0\n"
+            "  s_bfm_b64 s[82:83], %[w], 0\n"
+            "  s_mov_b64 exec, s[82:83]\n"
             "  ds_write_b8 %[va], %[vv]\n"
             "  s_mov_b64 exec, %[sav]\n"
-            "  s_lshr_b64 s[80:81], s[80:81], s82\n"
-            "  s_sub_u32 %[c], %[c], s82\n"
-            "  s_add_u32 %[o], %[o], s83\n"
-            "  s_sub_i32 %[ro], %[ro], s83\n"
+            "  s_lshr_b64 s[80:81], s[80:81], %[u]\n"
+            "  s_sub_u32 %[c], %[c], %[u]\n"
+            "  s_add_u32 %[o], %[o], %[w]\n"
+            "  s_sub_i32 %[ro], %[ro], %[w]\n"
+            "  s_cmp_gt_u32 %[c], 32\n"
+            "  s_cbranch_scc1 1b\n"
+            "  s_cmp_lt_i32 %[rp], 0\n"
+            "  s_cbranch_scc1 80f\n"
+            RDX_REFILL
             "  s_branch 1b\n"
-            "8:\n"
-            "  s_mov_b32 %[why], 1\n"
-            "  s_branch 10f\n"
-            "9:\n"
-            "  s_mov_b32 %[why], 0\n"
-            "10:\n"
+            // length symbol: base + extra bits
+            "20:\n"
+            "  s_cmp_eq_u32 %[u], 0\n"
+            "  s_cbranch_scc1 81f\n"
+            "  s_lshr_b32 %[w], %[e], 24\n"
+            "  s_cmp_lg_u32 %[w], 1\n"
+            "  s_cbranch_scc1 81f\n"
+            "  s_mov_b64 %[bs], s[80:81]\n"
+            "  s_mov_b32 %[od], %[c]\n"
+            "  s_mov_b32 %[j], %[p]\n"
+            "  s_mov_b32 %[rs], %[rp]\n"
+            "  s_lshr_b64 s[80:81], s[80:81], %[u]\n"
+            "  s_sub_u32 %[c], %[c], %[u]\n"
+            "  s_bfe_u32 %[u], %[e], 0x40014\n"
+            "  s_bfm_b32 %[w], %[u], 0\n"
+            "  s_and_b32 %[w], s80, %[w]\n"
+            "  s_and_b32 %[len], %[e], 0xffff\n"
+            "  s_add_u32 %[len], %[len], %[w]\n"
+            "  s_lshr_b64 s[80:81], s[80:81], %[u]\n"
+            "  s_sub_u32 %[c], %[c], %[u]\n"
+            "  s_cmp_gt_u32 %[c], 32\n"
+            "  s_cbranch_scc1 21f\n"
+            "  s_cmp_lt_i32 %[rp], 0\n"
+            "  s_cbranch_scc1 82f\n"
+            RDX_REFILL
+            // distance: root table + extra bits
+            "21:\n"
+            "  s_and_b32 %[w], s80, 0xff\n"
+            "  v_lshl_add_u32 %[va], %[w], 2, %[vdst]\n"
+            "  ds_read_b32 %[vv], %[va]\n"
             "  s_waitcnt lgkmcnt(0)\n"
-            : [b] "+{s[80:81]}"(b), [c] "+s"(c), [p] "+s"(p32), [o] "+s"(o32), [rp] "+s"(rp), [ro] "+s"(ro),
-              [e] "=&s"(e), [why] "=&s"(why), [sav] "=&s"(sav), [va] "=&v"(va), [vv] "=&v"(vv), [t0] "={s82}"(t0),
-              [t1] "={s83}"(t1), [t2] "={s84}"(t2)
-            : [vin] "v"(v_in), [vlit] "v"(v_lit), [vwin] "v"(v_win), [vlane] "v"(v_lane), [vsh] "v"(v_sh)
-            : "memory", "scc");
+            "  v_readfirstlane_b32 %[e], %[vv]\n"
+            "  s_bfe_u32 %[u], %[e], 0x40010\n"
+            "  s_cmp_eq_u32 %[u], 0\n"
+            "  s_cbranch_scc1 83f\n"
+            "  s_cmp_gt_u32 %[e], 0xffffff\n"
+            "  s_cbranch_scc1 83f\n"
+            "  s_lshr_b64 s[80:81], s[80:81], %[u]\n"
+            "  s_sub_u32 %[c], %[c], %[u]\n"
+            "  s_bfe_u32 %[u], %[e], 0x40014\n"
+            "  s_bfm_b32 %[w], %[u], 0\n"
+            "  s_and_b32 %[w], s80, %[w]\n"
+            "  s_and_b32 %[dist], %[e], 0xffff\n"
+            "  s_add_u32 %[dist], %[dist], %[w]\n"
+            "  s_lshr_b64 s[80:81], s[80:81], %[u]\n"
+            "  s_sub_u32 %[c], %[c], %[u]\n"
+            "  s_cmp_eq_u32 %[osm], 0\n"
+            "  s_cbranch_scc1 22f\n"
+            "  s_cmp_gt_u32 %[dist], %[o]\n"
+            "  s_cbranch_scc1 83f\n"
+            "22:\n"
+            "  s_cmp_gt_u32 %[dist], 0x1efe\n"
+            "  s_cbranch_scc1 84f\n"
+            // near copy, ring to ring
+            "  s_sub_u32 %[od], %[o], %[dist]\n"
+            "  s_mov_b32 %[j], 0\n"
+            "  s_cmp_lt_u32 %[dist], %[len]\n"
+            "  s_cbranch_scc1 40f\n"
+            "30:\n"  // source o - dist + j
+            "  v_add_u32 %[vj], %[j], %[vlane]\n"
+            "  v_add_u32 %[vs], %[od], %[vj]\n"
+            RDX_COPY_STEP("31")
+            "  s_cbranch_scc1 30b\n"
+            "  s_branch 50f\n"
+            "40:\n"  // overlapping (dist < len): source o - dist + (j mod dist), float reciprocal + correction
+            "  v_cvt_f32_u32 %[vr], %[dist]\n"
+            "  v_rcp_f32 %[vr], %[vr]\n"
+            "41:\n"
+            "  v_add_u32 %[vj], %[j], %[vlane]\n"
+            "  v_cvt_f32_u32 %[vq], %[vj]\n"
+            "  v_mul_f32 %[vq], %[vq], %[vr]\n"
+            "  v_cvt_u32_f32 %[vq], %[vq]\n"
+            "  v_mul_lo_u32 %[vq], %[vq], %[dist]\n"
+            "  v_sub_u32 %[vq], %[vj], %[vq]\n"
+            "  v_add_u32 %[vs], %[dist], %[vq]\n"
+            "  v_cmp_gt_i32 vcc, 0, %[vq]\n"
+            "  v_cndmask_b32 %[vq], %[vq], %[vs], vcc\n"
+            "  v_subrev_u32 %[vs], %[dist], %[vq]\n"
+            "  v_cmp_le_u32 vcc, %[dist], %[vq]\n"
+            "  v_cndmask_b32 %[vq], %[vq], %[vs], vcc\n"
+            "  v_add_u32 %[vs], %[od], %[vq]\n"
+            RDX_COPY_STEP("42")
+            "  s_cbranch_scc1 41b\n"
+            "50:\n"
+            "  s_add_u32 %[o], %[o], %[len]\n"
+            "  s_sub_i32 %[ro], %[ro], %[len]\n"
+            "  s_cmp_gt_u32 %[c], 32\n"
+            "  s_cbranch_scc1 1b\n"
+            "  s_cmp_lt_i32 %[rp], 0\n"
+            "  s_cbranch_scc1 80f\n"
+            RDX_REFILL
+            "  s_branch 1b\n"
+            "80:\n"
+            "  s_mov_b32 %[why], 1\n"
+            "  s_branch 90f\n"
+            "81:\n"
+            "  s_mov_b32 %[why], 0\n"
+            "  s_branch 90f\n"
+            "82:\n"
+            "  s_mov_b32 %[why], 1\n"
+            "  s_branch 85f\n"
+            "83:\n"
+            "  s_mov_b32 %[why], 0\n"
+            "85:\n"  // nothing consumed: restore the state before the length symbol
+            "  s_mov_b64 s[80:81], %[bs]\n"
+            "  s_mov_b32 %[c], %[od]\n"
+            "  s_mov_b32 %[p], %[j]\n"
+            "  s_mov_b32 %[rp], %[rs]\n"
+            "  s_branch 90f\n"
+            "84:\n"
+            "  s_mov_b32 %[why], 2\n"
+            "90:\n"
+            "  s_waitcnt lgkmcnt(0)\n"
+            : [b] "+{s[80:81]}"(b), [t0] "={s82}"(t0), [t1] "={s83}"(t1), [c] "+s"(c), [p] "+s"(p32), [o] "+s"(o32),
+              [rp] "+s"(rp), [ro] "+s"(ro), [why] "=&s"(why), [len] "=&s"(len), [dist] "=&s"(dist),
+              [sav] "=&s"(sav), [bs] "=&s"(bs), [e] "=&s"(e), [u] "=&s"(u), [w] "=&s"(w), [j] "=&s"(j),
+              [od] "=&s"(od), [rs] "=&s"(rs), [va] "=&v"(va), [vv] "=&v"(vv),
+              [vj] "=&v"(vj), [vq] "=&v"(vq), [vs] "=&v"(vs), [vr] "=&v"(vr)
+            : [osm] "s"(o_small), [vin] "v"(v_in), [vlit] "v"(v_lit), [vdst] "v"(v_dst), [vwin] "v"(v_win),
+              [vlane] "v"(v_lane), [vsh] "v"(v_sh)
+            : "memory", "scc", "vcc");
+#undef RDX_REFILL
+#undef RDX_COPY_STEP
     }
 
     // The symbol loop of one Huffman block, in two tiers.  A wave issues one instruction per 4 cycles
@@ -679,7 +835,9 @@ struct Inflater {
         uint64_t b = rfl64(bb), p = rfl64(pos), o = rfl64(out);
         uint32_t c = rfl(bc);
         const uint64_t stop_p = rfl64(staged) - 8;  // a dword refill needs p + 8 <= staged
-        const uint64_t fl = rfl64(flushed) + kFlush, cp = rfl64(cap);
+        // the unflushed tail may grow to the whole ring less one match: hot() leaves (and general()
+        // flushes every complete unit) once per ~3 units, not at every symbol past the first unit
+        const uint64_t fl = rfl64(flushed) + kWin, cp = rfl64(cap);
         const uint64_t lim = fl < cp ? fl : cp;
         const uint64_t stop_o = lim > 258 ? lim - 258 : 0;  // room for one more literal or match
         if (rfl64(o) > stop_o || rfl64(p) > stop_p + 8) return;
@@ -688,55 +846,30 @@ struct Inflater {
         const uint64_t dp = stop_p + 8 - p, dout = stop_o - o;
         int32_t rp = (int32_t)rfl((uint32_t)((int32_t)(dp < 0x40000000u ? dp : 0x40000000u) - 8));
         int32_t ro = (int32_t)rfl((uint32_t)(dout < 0x40000000u ? dout : 0x40000000u));
-        const uint32_t v_in = lds_addr(L.in), v_lit = lds_addr(L.lit), v_win = lds_addr(L.win);
-        const uint32_t v_lane = lane, v_sh = lane * 8;
+        const uint32_t v_in = lds_addr(L.in), v_lit = lds_addr(L.lit), v_dst = lds_addr(L.dist);
+        const uint32_t v_win = lds_addr(L.win), v_lane = lane, v_sh = lane * 8;
         for (;;) {
             asm volatile("; inflate hot loop" ::: "memory");
-            // literals, hand-scheduled (literal_run below); ring / input positions travel as their low
-            // 32 bits (all the ring masks need), advanced here by what the run consumed
-            uint32_t p32 = (uint32_t)p, o32 = (uint32_t)o, e, why;
-            const uint32_t p0 = p32, o0 = o32;
-            literal_run(b, c, p32, o32, rp, ro, e, why, v_in, v_lit, v_win, v_lane, v_sh);
+            // positions travel through the asm as their low 32 bits, advanced here by what it consumed
+            uint32_t p32 = (uint32_t)p, o32 = (uint32_t)o, why, len, dist;
+            const uint32_t p0 = p32, o0 = o32, o_small = rfl((uint32_t)(o >> 31) == 0 ? 1u : 0u);
+            symbol_run(b, c, p32, o32, rp, ro, why, len, dist, o_small, v_in, v_lit, v_dst, v_win, v_lane, v_sh);
             p += p32 - p0;
             o += o32 - o0;
             PROF_ADD(P_LIT, o32 - o0);
-            if (why) break;
-            const uint32_t l = (e >> 16) & 15;
-            if (l == 0) break;
-            const uint32_t type = e >> 24;
-            if (type != 1) break;
-            uint64_t b2 = b >> l;
-            uint32_t c2 = c - l;
-            const uint32_t ext = (e >> 20) & 15;
-            const uint32_t len = (e & 0xffff) + (uint32_t)(b2 & ((1u << ext) - 1));
-            b2 >>= ext;
-            c2 -= ext;
-            uint64_t p2 = p;
-            int32_t rp2 = rp;
-            if (c2 <= 32) {
-                if (rp2 < 0) break;
-                b2 |= (uint64_t)rfl(L.in[(uint32_t)(p2 >> 2) & (kInWords - 1)]) << c2;
-                p2 += 4;
-                rp2 -= 4;
-                c2 += 32;
-            }
-            const uint32_t d = rfl(L.dist[(uint32_t)b2 & ((1u << kDistRoot) - 1)]);
-            const uint32_t dl = (d >> 16) & 15;
-            if (dl == 0 || (d >> 24)) break;
-            b2 >>= dl;
-            c2 -= dl;
-            const uint32_t dext = (d >> 20) & 15;
-            const uint32_t dist = (d & 0xffff) + (uint32_t)(b2 & ((1u << dext) - 1));
-            b2 >>= dext;
-            c2 -= dext;
-            if (dist > (uint32_t)(o < 0x80000000u ? o : 0x80000000u)) break;
-            b = b2;  // commit the symbol
-            c = c2;
-            p = p2;
-            rp = rp2;
-            copy_at(o, len, dist);
-            o += len;
-            ro -= (int32_t)len;
+            if (why != 2) break;
+            len = rfl(len);
+            dist = rfl(dist);
+            PROF_T0();
+            copy_at(o, len, dist);   // a source past the ring: from the flushed output in HBM
+            PROF_T1(P_T_COPY);
+            // past copy_at's lane-dependent code the compiler no longer proves the loop state uniform
+            o = rfl64(o + len);
+            ro = (int32_t)rfl((uint32_t)(ro - (int32_t)len));
+            b = rfl64(b);
+            p = rfl64(p);
+            c = rfl(c);
+            rp = (int32_t)rfl((uint32_t)rp);
         }
         bb = b;
         bc = c;
@@ -795,7 +928,10 @@ struct Inflater {
     __device__ __forceinline__ void codes() {
         while (!err) {
             hot();
-            if (general()) break;
+            PROF_T0();
+            const bool end = general();
+            PROF_T1(P_T_GENERAL);
+            if (end) break;
         }
     }
 
@@ -849,7 +985,9 @@ struct Inflater {
             PROF_ADD(P_BLOCKS, 1);
             const uint32_t type = bits(2);
             if (type == 0) {
+                PROF_T0();
                 stored();
+                PROF_T1(P_T_STORED);
             } else if (type == 1) {
                 PROF_T0();
                 if (!fixed_ready) fixed_tables();
@@ -914,6 +1052,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
     f.srcw = reinterpret_cast<const uint32_t *>(src - skew);
     f.end = skew + len;
     f.staged = 0;
+    f.pf_start = ~0ull;
     f.pos = 0;
     f.bb = 0;
     f.bc = 0;

@@ -114,11 +114,13 @@ int main(int argc, char **argv) {
            p[rdx::P_LIT] * per, p[rdx::P_MATCH] * per, (double)p[rdx::P_MATCH_BYTES] / std::max(1ull, p[rdx::P_MATCH]),
            p[rdx::P_FAR] * per, p[rdx::P_SLOW] * per, p[rdx::P_BLOCKS] * per, p[rdx::P_STAGE] * per, p[rdx::P_FLUSH] * per);
     const double tot = (double)p[rdx::P_T_TOTAL];
-    printf("cycles per stream %.3g: copy %.1f%%  flush %.1f%%  tables %.1f%%  rest (symbol decode, literals) %.1f%%\n",
+    const double named = (double)p[rdx::P_T_COPY] + p[rdx::P_T_FLUSH] + p[rdx::P_T_TABLES] + p[rdx::P_T_STORED] +
+                         p[rdx::P_T_GENERAL];
+    printf("cycles per stream %.3g: far copies %.1f%%  flush %.1f%%  tables %.1f%%  stored blocks %.1f%%  general() %.1f%%  "
+           "rest (hot loop) %.1f%%\n",
            tot * per, 100 * p[rdx::P_T_COPY] / tot, 100 * p[rdx::P_T_FLUSH] / tot, 100 * p[rdx::P_T_TABLES] / tot,
-           100 * (tot - p[rdx::P_T_COPY] - p[rdx::P_T_FLUSH] - p[rdx::P_T_TABLES]) / tot);
-    printf("cycles per literal+match symbol (rest): %.1f; per match (copy only): %.1f; per flush: %.0f\n",
-           (tot - p[rdx::P_T_COPY] - p[rdx::P_T_FLUSH] - p[rdx::P_T_TABLES]) / (p[rdx::P_LIT] + p[rdx::P_MATCH]),
-           (double)p[rdx::P_T_COPY] / std::max(1ull, p[rdx::P_MATCH]), (double)p[rdx::P_T_FLUSH] / std::max(1ull, p[rdx::P_FLUSH]));
+           100 * p[rdx::P_T_STORED] / tot, 100 * p[rdx::P_T_GENERAL] / tot, 100 * (tot - named) / tot);
+    printf("cycles per far copy: %.0f; per flush: %.0f\n", (double)p[rdx::P_T_COPY] / std::max(1ull, p[rdx::P_FAR]),
+           (double)p[rdx::P_T_FLUSH] / std::max(1ull, p[rdx::P_FLUSH]));
     return 0;
 }
