@@ -17,8 +17,9 @@
 //     up to 64 bytes per step, one byte per lane (src = out - dist + (j mod dist) keeps every source
 //     in already-written history, so overlapping matches need no serial byte loop), and full 4 KiB
 //     units are flushed to HBM with 16-byte stores;
-//   * the CRC-32 / Adler-32 of each flushed unit is computed by all lanes over 64-byte slices and
-//     combined (GF(2) polynomial shift for CRC-32, weighted sums for Adler-32).
+//   * the CRC-32 / Adler-32 of each flushed unit is computed by all lanes over 32-byte slices and
+//     combined (CRC-32: each slice CRC shifted past the bytes after it by one GF(2) multiplication
+//     and XOR-reduced, the running CRC folded into lane 0's slice; Adler-32: weighted sums).
 // LDS ≈ 44 KiB per wave (one wave per workgroup): 3 streams resident per CU, 768 chip-wide.
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
@@ -29,7 +30,10 @@ namespace {
 #ifndef RDX_INFLATE_RING
 #define RDX_INFLATE_RING 8192
 #endif
-constexpr uint32_t kWaves = 4;                               // streams (wavefronts) per workgroup
+#ifndef RDX_INFLATE_WAVES
+#define RDX_INFLATE_WAVES 4
+#endif
+constexpr uint32_t kWaves = RDX_INFLATE_WAVES;               // streams (wavefronts) per workgroup
 constexpr uint32_t kWin = RDX_INFLATE_RING, kWinMask = kWin - 1;  // LDS ring: the recent window
 constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4;  // input ring
 constexpr uint32_t kStage = 1024;                             // bytes staged per refill of the ring
@@ -56,7 +60,8 @@ struct __attribute__((aligned(16))) InflateLds {
 
 // Read-only tables shared by the workgroup's streams.
 struct InflateShared {
-    uint32_t crc_tab[256];
+    uint32_t crc_tab[4][256];    // slicing-by-4 CRC-32 tables (crc_tab[0] = the byte table)
+    uint32_t x_after[64];        // x^(8 * 32 * (63 - l)) mod P: shifts lane l's slice CRC to the unit end
     uint32_t x2n[32];            // x^(2^k) mod P (CRC-32 combine)
     uint32_t lbase[29];          // base | extra << 16
     uint32_t dbase[30];
@@ -120,6 +125,17 @@ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
     return p;
 }
 
+// a(x) * b(x) mod P for a lane-varying a: all 32 terms, no data-dependent branches
+__device__ __forceinline__ uint32_t mulp(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+        p ^= (a >> i) & 1 ? b : 0u;
+        b = (b >> 1) ^ (b & 1 ? 0xedb88320u : 0u);
+    }
+    return p;
+}
+
 // x^(8n) mod P
 __device__ __forceinline__ uint32_t x8n(const InflateShared &L, uint64_t n) {
     uint32_t p = 1u << 31;
@@ -130,10 +146,6 @@ __device__ __forceinline__ uint32_t x8n(const InflateShared &L, uint64_t n) {
         ++k;
     }
     return p;
-}
-
-__device__ __forceinline__ uint32_t crc_combine(const InflateShared &L, uint32_t c1, uint32_t c2, uint64_t len2) {
-    return multmodp(x8n(L, len2), c1) ^ c2;
 }
 
 constexpr uint32_t kAdlerMod = 65521;
@@ -269,22 +281,29 @@ struct Inflater {
             for (uint32_t k = 0; k < cnt; ++k) d[k] = L.win[(base + lo + k) & kWinMask];
         }
         if (gzip) {
-            c = 0xffffffffu;
-            for (uint32_t k = 0; k < cnt; ++k) c = S.crc_tab[(c ^ L.win[(base + lo + k) & kWinMask]) & 0xff] ^ (c >> 8);
-            c ^= 0xffffffffu;
-            // combine the 64 slice CRCs in lane order (tree; right part length = its valid bytes)
-            uint32_t len = cnt;
+            // CRC-32 is linear: crc(state, unit) = XOR over lanes of lane l's slice CRC shifted past the
+            // bytes after it (x^(8 * after) mod P), with the running state folded into lane 0's start.
+            // `crc` is the raw register (no final inversion).  Full slices: slicing-by-4 over dwords
+            // and a per-lane constant shift; a short final unit: bytes and a computed shift.
+            c = lane == 0 ? crc : 0u;
+            uint32_t xa;
+            if (cnt == kSl) {
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(&L.win[base + lo]);
 #pragma unroll
-            for (int m = 1; m < 64; m <<= 1) {
-                const uint32_t oc = (uint32_t)__shfl_xor((int)c, m, 64);
-                const uint32_t ol = (uint32_t)__shfl_xor((int)len, m, 64);
-                if ((lane & m) == 0) {
-                    c = ol ? crc_combine(S, c, oc, ol) : c;
-                    len += ol;
+                for (uint32_t k = 0; k < kSl / 4; ++k) {
+                    c ^= w[k];
+                    c = S.crc_tab[3][c & 0xff] ^ S.crc_tab[2][(c >> 8) & 0xff] ^ S.crc_tab[1][(c >> 16) & 0xff] ^
+                        S.crc_tab[0][c >> 24];
                 }
+                xa = n == kFlush ? S.x_after[lane] : x8n(S, n - (lo + cnt));
+            } else {
+                for (uint32_t k = 0; k < cnt; ++k) c = S.crc_tab[0][(c ^ L.win[(base + lo + k) & kWinMask]) & 0xff] ^ (c >> 8);
+                xa = x8n(S, lo + cnt < n ? n - (lo + cnt) : 0);
             }
-            c = rfl((uint32_t)__shfl((int)c, 0, 64));
-            crc = flushed == 0 ? c : crc_combine(S, crc, c, n);
+            c = mulp(xa, c);
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) c ^= (uint32_t)__shfl_xor((int)c, m, 64);
+            crc = rfl(c);
         } else {
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t v = L.win[(base + lo + k) & kWinMask];
@@ -623,9 +642,7 @@ struct Inflater {
                                                int32_t &ro, uint32_t &why, uint32_t &len, uint32_t &dist,
                                                uint32_t o_small, uint32_t v_in, uint32_t v_lit, uint32_t v_dst,
                                                uint32_t v_win, uint32_t v_lane, uint32_t v_sh) {
-        static_assert(kWinMask == 0x1fff && kInWords * 4 == 0x800 && kLitRoot == 10 && kDistRoot == 8 &&
-                          kWin - 258 == 0x1efe,
-                      "masks hard-coded below");
+        static_assert(kInWords * 4 == 0x800 && kLitRoot == 10 && kDistRoot == 8, "masks hard-coded below");
 #define RDX_REFILL                             \
     "  s_and_b32 s82, %[p], 0x7fc\n"           \
     "  v_add_u32 %[vv], s82, %[vin]\n"         \
@@ -639,10 +656,10 @@ struct Inflater {
     "  s_sub_i32 %[rp], %[rp], 4\n"            \
     "  s_add_u32 %[c], %[c], 32\n"
 #define RDX_COPY_STEP(L)                        \
-    "  v_and_b32 %[vs], 0x1fff, %[vs]\n"        \
+    "  v_and_b32 %[vs], %[wm], %[vs]\n"        \
     "  v_add_u32 %[vs], %[vs], %[vwin]\n"       \
     "  v_add_u32 %[va], %[o], %[vj]\n"          \
-    "  v_and_b32 %[va], 0x1fff, %[va]\n"        \
+    "  v_and_b32 %[va], %[wm], %[va]\n"        \
     "  v_add_u32 %[va], %[va], %[vwin]\n"       \
     "  s_sub_u32 %[w], %[len], %[j]\n"          \
     "  s_mov_b64 s[82:83], -1\n"                \
@@ -673,7 +690,7 @@ struct Inflater {
             "  v_lshl_add_u32 %[va], s82, 2, %[vlit]\n"
             "  ds_read_b32 %[vv], %[va]\n"
             "  v_add_u32 %[va], %[o], %[vlane]\n"
-            "  v_and_b32 %[va], 0x1fff, %[va]\n"
+            "  v_and_b32 %[va], %[wm], %[va]\n"
             "  v_add_u32 %[va], %[va], %[vwin]\n"
             "  s_waitcnt lgkmcnt(0)\n"
             "  v_readfirstlane_b32 %[e], %[vv]\n"
@@ -749,7 +766,7 @@ struct Inflater {
             "  s_cmp_gt_u32 %[dist], %[o]\n"
             "  s_cbranch_scc1 83f\n"
             "22:\n"
-            "  s_cmp_gt_u32 %[dist], 0x1efe\n"
+            "  s_cmp_gt_u32 %[dist], %[near]\n"
             "  s_cbranch_scc1 84f\n"
             // near copy, ring to ring
             "  s_sub_u32 %[od], %[o], %[dist]\n"
@@ -817,7 +834,7 @@ struct Inflater {
               [od] "=&s"(od), [rs] "=&s"(rs), [va] "=&v"(va), [vv] "=&v"(vv),
               [vj] "=&v"(vj), [vq] "=&v"(vq), [vs] "=&v"(vs), [vr] "=&v"(vr)
             : [osm] "s"(o_small), [vin] "v"(v_in), [vlit] "v"(v_lit), [vdst] "v"(v_dst), [vwin] "v"(v_win),
-              [vlane] "v"(v_lane), [vsh] "v"(v_sh)
+              [vlane] "v"(v_lane), [vsh] "v"(v_sh), [wm] "n"(kWinMask), [near] "n"(kWin - 258)
             : "memory", "scc", "vcc");
 #undef RDX_REFILL
 #undef RDX_COPY_STEP
@@ -1036,7 +1053,16 @@ __global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
     {
         uint32_t c = t;
         for (int k = 0; k < 8; ++k) c = c & 1 ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        S.crc_tab[t] = c;
+        S.crc_tab[0][t] = c;
+    }
+    __syncthreads();
+    {   // slicing tables (each from the byte table) and the per-lane unit shifts (from x2n)
+        uint32_t c = S.crc_tab[0][t];
+        for (int k = 1; k < 4; ++k) {
+            c = (c >> 8) ^ S.crc_tab[0][c & 0xff];
+            S.crc_tab[k][t] = c;
+        }
+        if (t < 64) S.x_after[t] = x8n(S, (kFlush / 64) * (63 - t));
     }
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * kWaves + wave;
@@ -1059,7 +1085,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
     f.dst = a.out + (uint64_t)i * a.cap;
     f.cap = a.cap;
     f.out = f.flushed = 0;
-    f.crc = 0;
+    f.crc = 0xffffffffu;  // raw CRC-32 register
     f.s1 = 0;
     f.s2 = 0;
     f.gzip = a.format == RDX_COMPRESSION_GZIP;
@@ -1121,7 +1147,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
             uint32_t crc = 0, isize = 0;
             for (int k = 0; k < 4; ++k) crc |= f.byte() << (8 * k);
             for (int k = 0; k < 4; ++k) isize |= f.byte() << (8 * k);
-            if (!f.err && (crc != f.crc || isize != (uint32_t)f.out)) f.err = RDX_INFLATE_CHECKSUM;
+            if (!f.err && (crc != ~f.crc || isize != (uint32_t)f.out)) f.err = RDX_INFLATE_CHECKSUM;
         } else {
             uint32_t ad = 0;
             for (int k = 0; k < 4; ++k) ad = ad << 8 | f.byte();
