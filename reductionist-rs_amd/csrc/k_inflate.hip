@@ -39,7 +39,7 @@ constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4;  // input ring
 constexpr uint32_t kStage = 1024;                             // bytes staged per refill of the ring
 constexpr uint32_t kLitRoot = 10, kDistRoot = 8, kClRoot = 7;
 constexpr uint32_t kFlush = kWin / 4;                         // output unit written to HBM
-static_assert(kFlush + 516 <= kWin, "the unflushed tail plus one copy must fit the ring");
+static_assert(kFlush + 516 <= kWin, "the unflushed tail plus one copy (or stored step) must fit the ring");
 
 // Per-stream LDS (one per wave).  The DEFLATE window is 32 KiB but the ring keeps only the last kWin
 // bytes: a back-reference farther than that reads the already-flushed output in HBM (L2-hot).  The
@@ -966,17 +966,24 @@ struct Inflater {
             literal(bits(8));
             --left;
         }
-        // the rest straight from the input ring, 64 bytes per step
+        // the rest straight from the input ring, 256 bytes per step (4 per lane; the unflushed tail
+        // stays below kFlush + 256 <= kWin - 258, the input ring keeps >= 1 KiB ahead of pos)
+        constexpr uint32_t kStep = 256;
         while (left && !err) {
             flush_full();
-            if (pos + 64 > staged) stage();
-            const uint32_t m = left < 64 ? left : 64;
+            if (pos + kStep > staged) stage();
+            const uint32_t m = left < kStep ? left : kStep;
             if (pos + m > end) {
                 err = RDX_INFLATE_TRUNCATED;
                 break;
             }
             if (!room(m)) break;
-            if (lane < m) L.win[(uint32_t)(out + lane) & kWinMask] = (uint8_t)byte_at(pos + lane);
+            uint32_t v[kStep / 64];
+#pragma unroll
+            for (uint32_t k = 0; k < kStep / 64; ++k) v[k] = byte_at(pos + lane + 64 * k);
+#pragma unroll
+            for (uint32_t k = 0; k < kStep / 64; ++k)
+                if (lane + 64 * k < m) L.win[(uint32_t)(out + lane + 64 * k) & kWinMask] = (uint8_t)v[k];
             __builtin_amdgcn_wave_barrier();
             out += m;
             pos += m;
