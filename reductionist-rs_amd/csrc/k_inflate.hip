@@ -6,21 +6,21 @@
 // A DEFLATE stream is one serial bit stream (block boundaries and symbol positions are only known
 // after decoding everything before them), so the device parallelism is ACROSS streams: one
 // wavefront per compressed chunk, a batch of chunks per launch.  Inside a wave:
-//   * the symbol decode is wave-uniform serial code: every lane holds the same 64-bit bit buffer and
-//     walks the same symbols (no divergence; the SIMD executes it once per wave);
-//   * the compressed bytes are staged 2 KiB at a time into an LDS ring by all 64 lanes (one global
-//     load round trip per 2 KiB of input, not per refill);
-//   * Huffman codes decode through LDS root tables (10 bits literal/length, 8 bits distance; the
-//     rare longer codes by the canonical bit-serial walk), rebuilt per block by all lanes with
-//     ballot/popcount ranking instead of zlib's serial table construction;
-//   * the output goes through a 32 KiB LDS ring that IS the DEFLATE window: a back-reference copies
+//   * the symbol decode is wave-uniform serial code (GCN assembly, symbol_run): every lane holds
+//     the same bit buffer and walks the same symbols in SGPRs (no divergence);
+//   * the compressed bytes are staged 1 KiB at a time into a 2 KiB LDS input ring by all 64 lanes,
+//     the next unit's loads in flight while the current one decodes;
+//   * Huffman codes decode through LDS root tables (10 bits literal/length, with literal pairs; 8 bits
+//     distance; the rare longer codes by the canonical bit-serial walk), rebuilt per block by all
+//     lanes with ballot/popcount ranking instead of zlib's serial table construction;
+//   * the output goes through an 8 KiB LDS ring holding the recent window: a back-reference copies
 //     up to 64 bytes per step, one byte per lane (src = out - dist + (j mod dist) keeps every source
-//     in already-written history, so overlapping matches need no serial byte loop), and full 4 KiB
-//     units are flushed to HBM with 16-byte stores;
+//     in already-written history, so overlapping matches need no serial byte loop); sources farther
+//     back read the output already flushed to HBM; full 2 KiB units are flushed with 16-byte stores;
 //   * the CRC-32 / Adler-32 of each flushed unit is computed by all lanes over 32-byte slices and
 //     combined (CRC-32: each slice CRC shifted past the bytes after it by one GF(2) multiplication
 //     and XOR-reduced, the running CRC folded into lane 0's slice; Adler-32: weighted sums).
-// LDS ≈ 44 KiB per wave (one wave per workgroup): 3 streams resident per CU, 768 chip-wide.
+// LDS ≈ 17 KiB per wave, 4 waves (streams) per workgroup: 8 streams resident per CU.
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
 
