@@ -645,10 +645,10 @@ struct Inflater {
         static_assert(kInWords * 4 == 0x800 && kLitRoot == 10 && kDistRoot == 8, "masks hard-coded below");
 #define RDX_REFILL                             \
     "  s_and_b32 s82, %[p], 0x7fc\n"           \
-    "  v_add_u32 %[vv], s82, %[vin]\n"         \
-    "  ds_read_b32 %[vv], %[vv]\n"             \
+    "  v_add_u32 %[vr], s82, %[vin]\n"         \
+    "  ds_read_b32 %[vr], %[vr]\n"             \
     "  s_waitcnt lgkmcnt(0)\n"                 \
-    "  v_readfirstlane_b32 s82, %[vv]\n"       \
+    "  v_readfirstlane_b32 s82, %[vr]\n"       \
     "  s_mov_b32 s83, 0\n"                     \
     "  s_lshl_b64 s[82:83], s[82:83], %[c]\n"  \
     "  s_or_b64 s[80:81], s[80:81], s[82:83]\n" \
@@ -668,14 +668,14 @@ struct Inflater {
     "  s_bfm_b64 s[82:83], %[w], 0\n"           \
     L ":\n"                                     \
     "  s_mov_b64 exec, s[82:83]\n"              \
-    "  ds_read_u8 %[vv], %[vs]\n"               \
+    "  ds_read_u8 %[vd], %[vs]\n"               \
     "  s_waitcnt lgkmcnt(0)\n"                  \
-    "  ds_write_b8 %[va], %[vv]\n"              \
+    "  ds_write_b8 %[va], %[vd]\n"              \
     "  s_mov_b64 exec, %[sav]\n"                \
     "  s_add_u32 %[j], %[j], 64\n"              \
     "  s_cmp_lt_u32 %[j], %[len]\n"
         uint64_t sav, bs;
-        uint32_t t0, t1, e, u, w, j, od, rs, va, vv, vj, vq, vs, vr;
+        uint32_t t0, t1, e, u, w, j, od, rs, va, vv, vj, vq, vs, vr, vd;
         asm volatile(
             "  s_mov_b64 %[sav], exec\n"
             "  s_cmp_gt_u32 %[c], 32\n"
@@ -683,38 +683,45 @@ struct Inflater {
             "  s_cmp_lt_i32 %[rp], 0\n"
             "  s_cbranch_scc1 80f\n"
             RDX_REFILL
-            "1:\n"
+            "1:\n"  // loop top (c >= 33): look the next symbol up
             "  s_cmp_lt_i32 %[ro], 0\n"
             "  s_cbranch_scc1 80f\n"
             "  s_and_b32 s82, s80, 0x3ff\n"
             "  v_lshl_add_u32 %[va], s82, 2, %[vlit]\n"
             "  ds_read_b32 %[vv], %[va]\n"
-            "  v_add_u32 %[va], %[o], %[vlane]\n"
-            "  v_and_b32 %[va], %[wm], %[va]\n"
-            "  v_add_u32 %[va], %[va], %[vwin]\n"
+            "3:\n"  // the lookup of the symbol at the head of the bit buffer is in flight (c >= 33)
             "  s_waitcnt lgkmcnt(0)\n"
             "  v_readfirstlane_b32 %[e], %[vv]\n"
             "  s_bfe_u32 %[u], %[e], 0x40010\n"
             "  s_sub_u32 %[w], %[e], 0x10000\n"
             "  s_cmp_lt_u32 %[w], 0xff0000\n"
             "  s_cbranch_scc0 20f\n"
-            // literal (pair)
+            // literal (pair): consume it and issue the next lookup first (>= 23 valid bits remain), then
+            // store it and refill while that lookup is in flight
             "  s_bfe_u32 %[w], %[e], 0x20014\n"
-            "  v_lshrrev_b32 %[vv], %[vsh], %[e]\n"
-            "  s_bfm_b64 s[82:83], %[w], 0\n"
-            "  s_mov_b64 exec, s[82:83]\n"
-            "  ds_write_b8 %[va], %[vv]\n"
-            "  s_mov_b64 exec, %[sav]\n"
             "  s_lshr_b64 s[80:81], s[80:81], %[u]\n"
             "  s_sub_u32 %[c], %[c], %[u]\n"
+            "  s_and_b32 s82, s80, 0x3ff\n"
+            "  v_lshl_add_u32 %[va], s82, 2, %[vlit]\n"
+            "  ds_read_b32 %[vv], %[va]\n"
+            "  v_add_u32 %[va], %[o], %[vlane]\n"
+            "  v_and_b32 %[va], %[wm], %[va]\n"
+            "  v_add_u32 %[va], %[va], %[vwin]\n"
+            "  v_lshrrev_b32 %[vj], %[vsh], %[e]\n"
+            "  s_bfm_b64 s[82:83], %[w], 0\n"
+            "  s_mov_b64 exec, s[82:83]\n"
+            "  ds_write_b8 %[va], %[vj]\n"
+            "  s_mov_b64 exec, %[sav]\n"
             "  s_add_u32 %[o], %[o], %[w]\n"
             "  s_sub_i32 %[ro], %[ro], %[w]\n"
+            "  s_cmp_lt_i32 %[ro], 0\n"
+            "  s_cbranch_scc1 80f\n"
             "  s_cmp_gt_u32 %[c], 32\n"
-            "  s_cbranch_scc1 1b\n"
+            "  s_cbranch_scc1 3b\n"
             "  s_cmp_lt_i32 %[rp], 0\n"
             "  s_cbranch_scc1 80f\n"
             RDX_REFILL
-            "  s_branch 1b\n"
+            "  s_branch 3b\n"
             // length symbol: base + extra bits
             "20:\n"
             "  s_cmp_eq_u32 %[u], 0\n"
@@ -768,9 +775,13 @@ struct Inflater {
             "22:\n"
             "  s_cmp_gt_u32 %[dist], %[near]\n"
             "  s_cbranch_scc1 84f\n"
-            // near copy, ring to ring
+            // near copy, ring to ring, with the next symbol's lookup in flight meanwhile (>= 12 valid
+            // bits remain after the distance)
             "  s_sub_u32 %[od], %[o], %[dist]\n"
             "  s_mov_b32 %[j], 0\n"
+            "  s_and_b32 s82, s80, 0x3ff\n"
+            "  v_lshl_add_u32 %[va], s82, 2, %[vlit]\n"
+            "  ds_read_b32 %[vv], %[va]\n"
             "  s_cmp_lt_u32 %[dist], %[len]\n"
             "  s_cbranch_scc1 40f\n"
             "30:\n"  // source o - dist + j
@@ -801,12 +812,14 @@ struct Inflater {
             "50:\n"
             "  s_add_u32 %[o], %[o], %[len]\n"
             "  s_sub_i32 %[ro], %[ro], %[len]\n"
+            "  s_cmp_lt_i32 %[ro], 0\n"
+            "  s_cbranch_scc1 80f\n"
             "  s_cmp_gt_u32 %[c], 32\n"
-            "  s_cbranch_scc1 1b\n"
+            "  s_cbranch_scc1 3b\n"
             "  s_cmp_lt_i32 %[rp], 0\n"
             "  s_cbranch_scc1 80f\n"
             RDX_REFILL
-            "  s_branch 1b\n"
+            "  s_branch 3b\n"
             "80:\n"
             "  s_mov_b32 %[why], 1\n"
             "  s_branch 90f\n"
@@ -832,7 +845,7 @@ struct Inflater {
               [rp] "+s"(rp), [ro] "+s"(ro), [why] "=&s"(why), [len] "=&s"(len), [dist] "=&s"(dist),
               [sav] "=&s"(sav), [bs] "=&s"(bs), [e] "=&s"(e), [u] "=&s"(u), [w] "=&s"(w), [j] "=&s"(j),
               [od] "=&s"(od), [rs] "=&s"(rs), [va] "=&v"(va), [vv] "=&v"(vv),
-              [vj] "=&v"(vj), [vq] "=&v"(vq), [vs] "=&v"(vs), [vr] "=&v"(vr)
+              [vj] "=&v"(vj), [vq] "=&v"(vq), [vs] "=&v"(vs), [vr] "=&v"(vr), [vd] "=&v"(vd)
             : [osm] "s"(o_small), [vin] "v"(v_in), [vlit] "v"(v_lit), [vdst] "v"(v_dst), [vwin] "v"(v_win),
               [vlane] "v"(v_lane), [vsh] "v"(v_sh), [wm] "n"(kWinMask), [near] "n"(kWin - 258)
             : "memory", "scc", "vcc");
