@@ -20,34 +20,28 @@
 //   * the CRC-32 / Adler-32 of each flushed unit is computed by all lanes over 32-byte slices and
 //     combined (CRC-32: each slice CRC shifted past the bytes after it by one GF(2) multiplication
 //     and XOR-reduced, the running CRC folded into lane 0's slice; Adler-32: weighted sums).
-// LDS ≈ 17 KiB per wave, 4 waves (streams) per workgroup: 8 streams resident per CU.
+// LDS per wave ≈ ring + 8.5 KiB; ring and streams per workgroup chosen per launch (InflateLds).
+#include <cstdlib>
+
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
 
 namespace rdx {
 namespace {
 
-#ifndef RDX_INFLATE_RING
-#define RDX_INFLATE_RING 8192
-#endif
-#ifndef RDX_INFLATE_WAVES
-#define RDX_INFLATE_WAVES 4
-#endif
-constexpr uint32_t kWaves = RDX_INFLATE_WAVES;               // streams (wavefronts) per workgroup
-constexpr uint32_t kWin = RDX_INFLATE_RING, kWinMask = kWin - 1;  // LDS ring: the recent window
 constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4;  // input ring
 constexpr uint32_t kStage = 1024;                             // bytes staged per refill of the ring
 constexpr uint32_t kLitRoot = 10, kDistRoot = 8, kClRoot = 7;
-constexpr uint32_t kFlush = kWin / 4;                         // output unit written to HBM
-static_assert(kFlush + 516 <= kWin, "the unflushed tail plus one copy (or stored step) must fit the ring");
 
-// Per-stream LDS (one per wave).  The DEFLATE window is 32 KiB but the ring keeps only the last kWin
-// bytes: a back-reference farther than that reads the already-flushed output in HBM (L2-hot).  The
-// small ring is what lets 3 workgroups x 4 waves share a CU (12 streams per CU, 3 per SIMD) instead
-// of 1 wave per CU-quarter with a 32 KiB window, so the serial decode chains of different streams
-// hide each other's LDS latency.
+// Per-stream LDS (one per wave).  The DEFLATE window is 32 KiB; the ring keeps the last RING bytes and
+// a back-reference farther than that reads the already-flushed output in HBM (L2-hot).  The ring size
+// trades residency against far copies, so it is picked per launch from the batch size
+// (launch_inflate): a 32 KiB ring (the whole window, never a far copy) and 2 streams per workgroup up
+// to 512 streams, 16 KiB x 4 up to 1024 (one wave per SIMD), 8 KiB x 4 beyond (two per SIMD, whose
+// serial decode chains hide each other's LDS latency).
+template <uint32_t RING>
 struct __attribute__((aligned(16))) InflateLds {
-    uint8_t win[kWin];
+    uint8_t win[RING];
     uint32_t in[kInWords];
     uint32_t lit[1u << kLitRoot];
     uint32_t dist[1u << kDistRoot];
@@ -161,8 +155,12 @@ struct KInflateArgs {
     uint32_t n;                // streams
 };
 
+template <uint32_t RING>
 struct Inflater {
-    InflateLds &L;
+    static constexpr uint32_t kWin = RING, kWinMask = RING - 1;  // LDS ring: the recent window
+    static constexpr uint32_t kFlush = RING / 4;                  // output unit written to HBM
+    static_assert(kFlush + 516 <= kWin, "the unflushed tail plus one copy (or stored step) must fit the ring");
+    InflateLds<RING> &L;
     const InflateShared &S;
     const uint32_t lane;
     // input: the stream as dwords from its 4-byte aligned base; byte q of that aligned stream is
@@ -1044,11 +1042,13 @@ struct Inflater {
     }
 };
 
-__global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
+template <uint32_t RING, uint32_t WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
+    constexpr uint32_t kThreads = 64 * WAVES;
     __shared__ InflateShared S;
-    __shared__ InflateLds LW[kWaves];
+    __shared__ InflateLds<RING> LW[WAVES];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    // shared constant tables (once per workgroup; the only workgroup-wide barrier)
+    // shared constant tables (once per workgroup; the only workgroup-wide barriers)
     if (t < 29) {
         constexpr uint16_t kB[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -1058,43 +1058,44 @@ __global__ __launch_bounds__(64 * kWaves) void k_inflate(const KInflateArgs a) {
             if ((uint32_t)k == t) b = kB[k];
         const uint32_t e = t < 8 || t == 28 ? 0 : (t - 4) / 4;
         S.lbase[t] = b | e << 16;
-    } else if (t >= 64 && t < 94) {
-        const uint32_t c = t - 64;
+    } else if (t >= 32 && t < 62) {
+        const uint32_t c = t - 32;
         const uint32_t e = c < 2 ? 0 : c / 2 - 1;
         const uint32_t b = c < 4 ? c + 1 : (1u << e) * (2 + (c & 1)) + 1;
         S.dbase[c] = b | e << 16;
-    } else if (t == 128) {
+    } else if (t == 63) {
         uint32_t p = 1u << 30;  // x^1
         for (int k = 0; k < 32; ++k) {
             S.x2n[k] = p;
             p = multmodp(p, p);
         }
     }
-    {
-        uint32_t c = t;
+    for (uint32_t q = t; q < 256; q += kThreads) {
+        uint32_t c = q;
         for (int k = 0; k < 8; ++k) c = c & 1 ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        S.crc_tab[0][t] = c;
+        S.crc_tab[0][q] = c;
     }
     __syncthreads();
-    {   // slicing tables (each from the byte table) and the per-lane unit shifts (from x2n)
-        uint32_t c = S.crc_tab[0][t];
+    // slicing tables (each from the byte table) and the per-lane unit shifts (from x2n)
+    for (uint32_t q = t; q < 256; q += kThreads) {
+        uint32_t c = S.crc_tab[0][q];
         for (int k = 1; k < 4; ++k) {
             c = (c >> 8) ^ S.crc_tab[0][c & 0xff];
-            S.crc_tab[k][t] = c;
+            S.crc_tab[k][q] = c;
         }
-        if (t < 64) S.x_after[t] = x8n(S, (kFlush / 64) * (63 - t));
     }
+    if (t < 64) S.x_after[t] = x8n(S, (Inflater<RING>::kFlush / 64) * (63 - t));
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * kWaves + wave;
+    const uint64_t i = (uint64_t)blockIdx.x * WAVES + wave;
     if (i >= a.n) return;
-    InflateLds &L = LW[wave];
+    InflateLds<RING> &L = LW[wave];
     // scalar: every lane reads the same descriptor, and the decode state derived from it must stay
     // wave-uniform (SGPRs) for the serial path to compile to scalar code
     const uint8_t *src = reinterpret_cast<const uint8_t *>(rfl64((uint64_t)gld<const uint8_t *>(a.in + i)));
     const uint64_t len = rfl64(gld<uint64_t>(a.in_len + i));
 
     const uint32_t skew = (uint32_t)((uintptr_t)src & 3);
-    Inflater f{L, S, lane};
+    Inflater<RING> f{L, S, lane};
     f.srcw = reinterpret_cast<const uint32_t *>(src - skew);
     f.end = skew + len;
     f.staged = 0;
@@ -1191,7 +1192,19 @@ hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uin
                           uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s) {
     if (n == 0) return hipSuccess;
     KInflateArgs a{d_in, d_in_len, d_out, cap, d_out_len, d_err, format, (uint32_t)n};
-    hipLaunchKernelGGL(k_inflate, dim3((uint32_t)((n + kWaves - 1) / kWaves)), dim3(64 * kWaves), 0, s, a);
+    // ring size from the batch size (InflateLds); RDX_INFLATE_RING=8192/16384/32768 forces one (tuning)
+    static const int force = [] {
+        const char *v = std::getenv("RDX_INFLATE_RING");
+        return v ? std::atoi(v) : 0;
+    }();
+    const uint32_t ring = force ? (uint32_t)force : n <= 512 ? 32768u : n <= 1024 ? 16384u : 8192u;
+    if (ring == 32768u) {
+        hipLaunchKernelGGL((k_inflate<32768, 2>), dim3((uint32_t)((n + 1) / 2)), dim3(128), 0, s, a);
+    } else if (ring == 16384u) {
+        hipLaunchKernelGGL((k_inflate<16384, 4>), dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((k_inflate<8192, 4>), dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 
