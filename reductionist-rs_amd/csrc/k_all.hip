@@ -318,12 +318,7 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
             }
         }
     }
-#ifdef RDX_X_NOFIN      // timing experiments only (wrong results)
-    block_reduce(r);
-    if (threadIdx.x == 0) store_packed<T, OP, false>(a.out.partials + (uint64_t)blockIdx.x * kPartialWords, r);
-#else
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
-#endif
 }
 
 template <typename T, int OP, int UNR>

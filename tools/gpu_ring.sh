@@ -1,4 +1,6 @@
-# Inflate ring size x waves per workgroup (probe_inflate builds), field and noise, 1024 and 2048 streams.
+# Inflate ring size x waves per workgroup, field and noise, 1024 and 2048 streams.  Measured with
+# per-variant probe_inflate builds before the ring became a per-launch choice (RDX_INFLATE_RING forces
+# one now: see tools/gpu_ringsel.sh); kept as the record of that sweep.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/ring.log
