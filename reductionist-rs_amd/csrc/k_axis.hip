@@ -263,6 +263,13 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     // contiguous slice ranges, then the same lane + LDS combine.
     const uint64_t tile_rec = (uint64_t)W * VW;
     uint64_t *P = a.out.partials + (uint64_t)blockIdx.x * a.slices * tile_rec * kW;
+    if (a.fold_sep) {   // k_axis_cols_fold reads the records after this launch: plain stores
+        if (wave == 0 && lane < W) {
+#pragma unroll
+            for (int j = 0; j < VW; ++j) store_packed<T, OP, false>(P + ((uint64_t)s * tile_rec + c * VW + j) * kW, r[j]);
+        }
+        return;
+    }
     if (wave == 0) {
         if (lane < W) {
 #pragma unroll
@@ -308,6 +315,47 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     }
 }
 
+// The fold of sliced column reductions as its own launch (fold_sep), parallel across outputs instead of
+// one workgroup per tile: a wave per output (WG = false; its lanes take contiguous slice ranges, the
+// wave butterfly merges them) or, for few outputs with many slices, a workgroup per output (WG = true,
+// 256 slice ranges, block combine), so a tall narrow reduction folds in one or two round trips.
+template <typename T, int OP, int VW, bool WG>
+__global__ __launch_bounds__(kBlock) void k_axis_cols_fold(const KAxis a) {
+    constexpr int kW = packed_words<T, OP>();
+    constexpr uint32_t kLanes = WG ? kBlock : 64;
+    const uint32_t lane = WG ? threadIdx.x : threadIdx.x & 63;
+    const uint32_t W = a.group;
+    const uint64_t tile_rec = (uint64_t)W * VW;
+    const uint64_t nkv = a.n_out / VW;
+    const uint64_t q = WG ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t x = q / tile_rec, cj = q - x * tile_rec;                        // tile, c * VW + j
+    const uint64_t kv = x * W + cj / VW;
+    const uint32_t j = (uint32_t)(cj % VW);
+    if (kv >= nkv) return;   // uniform over the wave (WG: over the workgroup)
+    const uint64_t *P = a.out.partials + x * a.slices * tile_rec * kW + cj * kW;
+    const uint32_t s_lo = (uint32_t)((uint64_t)lane * a.slices / kLanes);
+    const uint32_t s_hi = (uint32_t)((uint64_t)(lane + 1) * a.slices / kLanes);
+    Red<T, OP> r;
+    r.init();
+    for (uint32_t s0 = s_lo; s0 < s_hi; s0 += 4) {
+        Red<T, OP> p[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            if (s0 + u < s_hi) load_packed<T, OP, false>(P + (uint64_t)(s0 + u) * tile_rec * kW, p[u]);
+            else p[u].init();
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) r.merge(p[u]);
+    }
+    if constexpr (WG) block_reduce(r);
+    else wave_reduce(r);
+    if (lane == 0) {
+        int64_t oi;
+        kept_offset(a.kept, (uint32_t)(kv * VW), oi);
+        write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r);
+    }
+}
+
 template <typename T, int OP, int VW, bool GEN, int MK>
 void launch_axis_k(const KAxis &a, int cus, hipStream_t st) {
     const dim3 block(kBlock);
@@ -323,6 +371,18 @@ void launch_axis_k(const KAxis &a, int cus, hipStream_t st) {
         const dim3 grid((uint32_t)((a.n_out / VW + a.group - 1) / a.group), a.slices);
         if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1, GEN, MK>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((k_axis_cols<T, OP, false, VW, GEN, MK>), grid, block, 0, st, a);
+        if (a.slices > 1 && a.fold_sep && a.probe == 0) {
+            const uint64_t cols = (uint64_t)grid.x * a.group * (a.src.fused ? 1 : VW);   // record columns
+            const bool wg = cols * 4 <= (uint64_t)cus * 4 && a.slices >= 256;   // few outputs, long folds
+            const dim3 fgrid((uint32_t)(wg ? cols : (cols + kBlock / 64 - 1) / (kBlock / 64)));
+            if (a.src.fused) {
+                if (wg) hipLaunchKernelGGL((k_axis_cols_fold<T, OP, 1, true>), fgrid, block, 0, st, a);
+                else hipLaunchKernelGGL((k_axis_cols_fold<T, OP, 1, false>), fgrid, block, 0, st, a);
+            } else {
+                if (wg) hipLaunchKernelGGL((k_axis_cols_fold<T, OP, VW, true>), fgrid, block, 0, st, a);
+                else hipLaunchKernelGGL((k_axis_cols_fold<T, OP, VW, false>), fgrid, block, 0, st, a);
+            }
+        }
     }
 }
 

@@ -114,7 +114,8 @@ struct KAxis {
     uint32_t vec;    // elements per 16-byte lane load (1 = scalar)
     uint32_t group;  // rows mode: lanes per output (power of two <= 64); 64/group outputs per wave
     uint32_t probe;  // tuning probe only (RDX_AXIS_PROBE): 1 = skip the slice fold, 2 = stop after streaming
-    uint32_t pad;
+    uint32_t fold_sep;  // cols, slices > 1: 0 = the tile's last slice folds (arrival counters); 1 = every
+                        // slice only publishes and k_axis_cols_fold folds (a wave per output) next
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

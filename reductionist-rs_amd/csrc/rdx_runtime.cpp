@@ -50,6 +50,7 @@ struct Tuning {
     int axis_cols_wgs = env_int("RDX_AXIS_COLS_WGS_PER_CU", 4);        // sliced-cols fill target
     int axis_cols_vw = env_int("RDX_AXIS_COLS_VW", 0);                 // tuning only: force the cols lane width
     int axis_fold_kib = env_int("RDX_AXIS_FOLD_KIB", 64);              // cols fold bytes per tile (x2 with >= 8 streams)
+    int axis_fold_sep = env_int("RDX_AXIS_FOLD_SEP", -1);              // cols fold launch: -1 auto, 0 off, 1 on
     int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
@@ -338,6 +339,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             const uint32_t vmax = 16 / p.esz;
             a.group = 64;
             a.probe = (uint32_t)tuning().axis_probe;
+            a.fold_sep = 0;
             if (a.mode == 0) {
                 a.vec = vec_ok(vmax) ? vmax : 1;
                 const uint64_t target = (uint64_t)ws->cus * tuning().axis_rows_waves;     // waves
@@ -373,13 +375,23 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                     const uint64_t budget = std::min<uint64_t>(fold * std::max<uint64_t>(1, G / 4), 2 * fold);
                     const uint64_t smax = std::max<uint64_t>(
                         1, std::min({budget / (W * vw * rec), 16 * G, a.n_red / (16 * R)}));
-                    const uint64_t sl = std::max<uint64_t>(1, std::min((target + tiles - 1) / tiles, smax));
+                    uint64_t sl = std::max<uint64_t>(1, std::min((target + tiles - 1) / tiles, smax));
+                    // few tiles whose fold budget leaves the chip underfilled (tall, narrow): more slices
+                    // and the separate fold launch (k_axis_cols_fold, parallel across outputs)
+                    bool sep = tuning().axis_fold_sep == 1;
+                    if (tuning().axis_fold_sep < 0 && tiles * sl * 2 < target) sep = true;
+                    if (sep) {
+                        const uint64_t target2 = (uint64_t)ws->cus * 8;
+                        sl = std::max<uint64_t>(1, std::min<uint64_t>({(target2 + tiles - 1) / tiles,
+                                                                       a.n_red / (16 * R), 4096}));
+                    }
                     const uint64_t wgs = tiles * sl;
                     if (wgs > best_wgs) {
                         best_wgs = wgs;
                         a.vec = vw;
                         a.group = W;
                         slices = sl;
+                        a.fold_sep = sep ? 1u : 0u;
                     }
                     if (wgs * 2 >= target) break;   // the widest lanes that fill the chip
                 }
