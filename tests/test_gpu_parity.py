@@ -181,7 +181,7 @@ def test_cols_tilings(engine, shape, axis, dtype, op):
     assert_parity(engine, op, req, v.tobytes())
 
 
-@pytest.mark.parametrize("case", range(10))
+@pytest.mark.parametrize("case", range(12))
 def test_row_batch(engine, case):
     """Few long contiguous rows (>= 64 KiB reduced per output) go to the batched all-axes kernel,
     one chunk per output (rdx_runtime.cpp, Mode::Axis): selections on the kept and reduced dims,
@@ -198,6 +198,10 @@ def test_row_batch(engine, case):
         ("uint64", "min", [2, 3, 20000], None, 2, "C", {"missing": {"missing_values": [7, 9]}}),
         ("float64", "min", [3, 9000], None, 1, "C", {}),                          # NaN -> status
         ("float32", "select", [4, 40000], None, 1, "C", {}),
+        ("float32", "sum", [3, 20001], None, 1, "C", {"byte_order": "big",               # unaligned fused rows
+                                                      "filters": [{"id": "shuffle", "element_size": 4}]}),
+        ("int64", "max", [5, 9001], [[0, 5, 2], [1, 9000, 1]], 1, "C",
+         {"filters": [{"id": "shuffle", "element_size": 8}], "missing": {"valid_max": 90}}),
     ][case]
     rng = np.random.default_rng(100 + case)
     n = int(np.prod(shape))
