@@ -13,6 +13,8 @@ Ranks (one per GPU, torchrun) each process their own chunks: weak scaling, no da
 
 Also reported (extra.c4_batch): BASELINE configs[3] — a batch of 1024 independent 4 MiB shuffled f32
 chunks summed by one launch per step, the batch split across ranks (strong scaling of that batch).
+extra.f64_64mib / extra.f64_4mib: the north_star's f64 legs — 8 x 64 MiB and 128 x 4 MiB f64 chunks
+per GPU (big-endian, shuffle element_size 8, sum), one batched launch per step (weak scaling).
 
 Roofline: bytes_alg per launch = n_elements * 4 B read (unshuffle / byte swap add no algorithmic
 bytes; the 16 B result is negligible) / average kernel duration from HIP events recorded on the
@@ -52,6 +54,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-inflate", action="store_true")
+    ap.add_argument("--no-f64", action="store_true")
     ap.add_argument("--primary-only", action="store_true", help="only the headline batched C2 loop (profiling)")
     return ap.parse_args()
 
@@ -61,6 +64,53 @@ def shuffled_be_f32(torch, vals):
     (src/filters/shuffle.rs:124-135 encoder), laid out (…, 4*n) uint8 contiguous."""
     b = vals.contiguous().view(torch.uint8).reshape(*vals.shape, 4).flip(-1)       # big-endian
     return b.transpose(-1, -2).contiguous().reshape(*vals.shape[:-1], 4 * vals.shape[-1])
+
+
+def f64_batch(torch, ws, stream, g, rank, barrier, max_over_ranks, world, elems, n_chunks, steps):
+    """n_chunks independent HBM-resident f64 chunks (big-endian, shuffle element_size 8, sum) per rank,
+    one rdx_execute_batch_device launch per step; results checked against an f64 sum of the values
+    (f64 chunks are summed Neumaier-compensated)."""
+    g.manual_seed(0x5EED2000 + rank)
+    vals = torch.rand(n_chunks, elems, device="cuda", generator=g, dtype=torch.float64)
+    exact = vals.sum(dim=1).cpu()
+    b = vals.view(torch.uint8).reshape(n_chunks, elems, 8).flip(-1)            # big-endian
+    chunks = b.transpose(-1, -2).contiguous().reshape(n_chunks, 8 * elems)     # shuffle es=8
+    del vals, b
+    bodies = torch.zeros(n_chunks, dtype=torch.float64, device="cuda")
+    counts = torch.zeros(n_chunks, dtype=torch.int64, device="cuda")
+    status = torch.zeros(n_chunks, dtype=torch.int32, device="cuda")
+    from reductionist_amd import _abi
+    creq = _abi.CRequest("sum", "float64", byte_order="big", filters=[{"id": "shuffle", "element_size": 8}])
+    ptrs = [chunks[i].data_ptr() for i in range(n_chunks)]
+
+    def launch():
+        ws.execute_batch_device(creq, ptrs, 8 * elems, bodies.data_ptr(), counts.data_ptr(), status.data_ptr(),
+                                stream.cuda_stream)
+
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0 and bool((counts.cpu() == elems).all())
+    assert bool(((bodies.cpu() - exact).abs() <= exact.abs() * 2.0 ** -44).all()), (bodies.cpu(), exact)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    el = max_over_ranks(t1 - t0)
+    k = e0.elapsed_time(e1) / 1e3 / steps
+    step_bytes = n_chunks * 8 * elems
+    return {"workload": f"{n_chunks} x {8 * elems >> 20} MiB f64 chunks per GPU, big-endian, shuffle es=8, sum; "
+                        "one batched launch per step",
+            "value": round(steps * step_bytes * world / el / GIB, 2), "unit": "GiB/s", "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 5), "kernel_us_avg": round(k * 1e6, 3),
+            "roofline_frac": round(step_bytes / k / 1e9 / PEAK_GBS, 4)}
 
 
 def traffic_from_profiles(tag):
@@ -301,7 +351,7 @@ def main():
 
     extra = {}
     if args.primary_only:
-        args.no_c4 = args.no_cpu_baseline = args.no_inflate = True
+        args.no_c4 = args.no_cpu_baseline = args.no_inflate = args.no_f64 = True
     else:
         for i in range(max(args.warmup, N_BUF)):   # every chunk at least once, whatever --warmup is
             single_step(i)
@@ -357,6 +407,13 @@ def main():
         del c4
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             extra["c4_batch"]["cpu_baseline"] = cpu_baseline_c4(max(1, min(15, (os.cpu_count() or 2) - 1)))
+
+    # ---- f64 chunks (extra): north_star's "4 MiB and 64 MiB f32/f64 chunks", f64 legs --------------------
+    if not args.no_f64:
+        extra["f64_64mib"] = f64_batch(torch, ws, stream, g, rank, barrier, max_over_ranks, world,
+                                       elems=8 * 1024 * 1024, n_chunks=N_BUF, steps=max(10, args.steps // 4))
+        extra["f64_4mib"] = f64_batch(torch, ws, stream, g, rank, barrier, max_over_ranks, world,
+                                      elems=512 * 1024, n_chunks=128, steps=max(10, args.steps // 4))
 
     # ---- decompression (extra): the filter pipeline's first stage on the device ------------
     if not args.no_inflate:
