@@ -7,7 +7,9 @@ byte-shuffled (element_size 4), each reduced with `sum` (its own result + count)
 fused unshuffle + byte-swap + f64-accumulated sum kernel over those 8 independent chunks through the
 engine's batch entry point (rdx_execute_batch_device), so every step streams 512 MiB from HBM and the
 per-launch ramp/finalisation (~6 us, profiles/) is paid once per 8 chunks.  extra.c2_single_chunk
-reports the same chunks at one chunk per launch (rdx_execute_device).
+reports the same chunks at one chunk per launch (rdx_execute_device); extra.c2_concurrent_requests
+issues those single-chunk calls round-robin over 4 HIP streams (one workspace each), as concurrent
+server requests would be (RDX_BENCH_STREAMS overrides the 4).
 Ranks (one per GPU, torchrun) each process their own chunks: weak scaling, no data-path collective
 (the control-plane barrier / max-time reduction uses gloo).
 
@@ -362,6 +364,42 @@ def main():
         "value": round(args.steps * C2_BYTES * world / el1 / GIB, 2), "unit": "GiB/s",
         "ms_per_step": round(el1 / args.steps * 1e3, 5), "kernel_us_avg": round(k1 * 1e6, 3),
         "roofline_frac": round(C2_BYTES / k1 / 1e9 / PEAK_GBS, 4)}
+
+        # concurrent single-chunk requests, the way a server runs them (one request per worker thread,
+        # app.rs:123-153): one workspace + HIP stream per in-flight request, chunks round-robin, so one
+        # launch's ramp / hand-off tail overlaps the next launch's streaming
+        n_st = int(os.environ.get("RDX_BENCH_STREAMS", "4"))
+        sts = [torch.cuda.Stream() for _ in range(n_st)]
+        wss = [eng.workspace(device) for _ in range(n_st)]
+        conc_args = [(wss[i % n_st].ws,) + single_args[i][1:-2] + (C.c_void_p(sts[i % n_st].cuda_stream),
+                                                                   single_args[i][-1]) for i in range(N_BUF)]
+
+        def conc_step(i):
+            st = lib.rdx_execute_device(*conc_args[i % N_BUF])
+            if st:
+                raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
+
+        for i in range(max(args.warmup, N_BUF)):
+            conc_step(i)
+        check_results()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            conc_step(i)
+        torch.cuda.synchronize()
+        elc = max_over_ranks(time.perf_counter() - t0)
+        barrier()
+        check_results()
+        extra["c2_concurrent_requests"] = {
+            "workload": f"the same 64 MiB chunks, one chunk per rdx_execute_device call, {n_st} streams / "
+                        "workspaces round-robin (concurrent requests)",
+            "value": round(args.steps * C2_BYTES * world / elc / GIB, 2), "unit": "GiB/s",
+            "us_per_request": round(elc / args.steps * 1e6, 3),
+            "roofline_frac": round(args.steps * C2_BYTES / elc / 1e9 / PEAK_GBS, 4),
+            "timing": "host wall clock around the K calls, synchronize on both sides"}
+        for w in wss:
+            w.close()
 
     # ---- C4 (extra): 1024 x 4 MiB chunks, one batched launch per step ----------------------------------
     if not args.no_c4:
