@@ -49,6 +49,53 @@ def dev_time(creq, bufs, nbytes, out_bytes, k=50):
 
 
 HOST = {}
+
+
+def conc_time(creq, bufs, nbytes, n_th=4, k=4000):
+    """Concurrent requests the way the server issues them (one request per worker thread,
+    src/app.rs:123-153): n_th host threads, each with its own workspace, HIP stream and output
+    buffers, issue k/n_th single-chunk rdx_execute_device calls over the rotating buffers (ctypes
+    releases the GIL).  Returns wall seconds per request, synchronize on both sides."""
+    import threading
+    info = _abi.rdx_response_info()
+    assert lib.rdx_plan(creq.ref, nbytes, C.byref(info)) == 0
+    per = []
+    for t in range(n_th):
+        w = eng.workspace(0)
+        st = torch.cuda.Stream()
+        body = torch.empty(max(16, info.body_bytes), dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(max(1, info.n_counts), dtype=torch.int64, device="cuda")
+        status = torch.zeros(4, dtype=torch.int32, device="cuda")
+        per.append((w, st, body, counts, status))
+    errs = []
+
+    def worker(t, n):
+        w, st, body, counts, status = per[t]
+        inf = _abi.rdx_response_info()
+        args = [(w.ws, creq.ref, C.c_void_p(b.data_ptr()), nbytes, C.c_void_p(body.data_ptr()),
+                 C.c_void_p(counts.data_ptr()), C.c_void_p(status.data_ptr()), C.c_void_p(st.cuda_stream),
+                 C.byref(inf)) for b in bufs]
+        for i in range(n):
+            r = lib.rdx_execute_device(*args[(i * n_th + t) % len(args)])
+            if r:
+                errs.append(r)
+                return
+
+    for t in range(n_th):   # warm-up: every thread's path once
+        worker(t, 3)
+    torch.cuda.synchronize()
+    ths = [threading.Thread(target=worker, args=(t, k // n_th)) for t in range(n_th)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    assert not errs and all(int(p[4].abs().sum()) == 0 for p in per)
+    for p in per:
+        p[0].close()
+    return el / (k // n_th * n_th)
 NO_CPU = "--no-cpu" in sys.argv   # profiling runs: skip the oracle timings
 
 
@@ -100,6 +147,10 @@ for op, miss in (("min", ("missing_value", -9999.0)), ("max", ("missing_value", 
     tc = cpu_time(creq, v.tobytes())
     report(f"c3_{op}_{miss[0]}", t, n_sel * 8 + 16, 128 ** 3 * 8, n_selected=n_sel,
            cpu_oracle_us=round(tc * 1e6, 1), gpu_over_cpu=round(tc / t, 1))
+    if op == "min":
+        tcc = conc_time(creq, c3, 128 ** 3 * 8)
+        report(f"c3_{op}_{miss[0]}_concurrent4", tcc, n_sel * 8 + 16, 128 ** 3 * 8, n_selected=n_sel,
+               note="4 host threads x (workspace, stream), wall clock per request")
 # C3 as a batch: 20 independent 16 MiB chunks per launch (rdx_execute_batch_device), min
 creqb = _abi.CRequest("min", "float64", shape=[128, 128, 128], selection=sel, missing_kind="missing_value",
                       missing_values=np.float64(-9999.0).tobytes(), n_missing=1)
@@ -132,6 +183,10 @@ for seed, real in ((0x5EED0001, False), (0x5EED0002, True)):
     t = dev_time(creq1, bufs, 4 << 20, 4)
     report("c1_sum_4MiB_" + ("real" if real else "int"), t, 4 << 20, 4 << 20, cpu_oracle_us=round(tc * 1e6, 1),
            cpu_oracle_GiBs=round((4 << 20) / tc / 2 ** 30, 3), gpu_over_cpu=round(tc / t, 1))
+    if real:
+        tcc = conc_time(creq1, bufs, 4 << 20)
+        report("c1_sum_4MiB_real_concurrent4", tcc, 4 << 20, 4 << 20,
+               note="4 host threads x (workspace, stream), wall clock per request")
     del bufs
 
 # ---- axis reductions ---------------------------------------------------------------------------------
@@ -170,6 +225,9 @@ host5 = c5[0].cpu().numpy().tobytes()
 tc = cpu_time(creq5, host5, seconds=3.0)
 report("c5_select_device", t, (128 << 20) * 2, 256 << 20, note="128 MiB read + 128 MiB written",
        cpu_oracle_us=round(tc * 1e6, 1), gpu_over_cpu=round(tc / t, 1))
+tcc = conc_time(creq5, c5, 256 << 20, k=400)
+report("c5_select_device_concurrent4", tcc, (128 << 20) * 2, 256 << 20,
+       note="4 host threads x (workspace, stream, 128 MiB body), wall clock per request")
 
 # host-inclusive C5: host chunk in (pageable), 128 MiB body out (pageable) through rdx_execute
 del c5
