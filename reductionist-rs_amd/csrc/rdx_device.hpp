@@ -274,14 +274,23 @@ struct Red {
         } else if constexpr (OP == OP_MAX || OP == OP_MIN) {
             if constexpr (kFloat) {
                 nan |= (x != x);
-                if (x == T(0)) {
-                    const int64_t r = rank();
-                    if (__builtin_signbit(x)) zn = OP == OP_MAX ? max(zn, r) : min(zn, r);
-                    else zp = OP == OP_MAX ? max(zp, r) : min(zp, r);
+                // ±0 fold-order ranks behind a wave-uniform branch: without it the compiler
+                // if-converts the zero case and every element pays a 64-bit rank and two selects.
+                if (__builtin_amdgcn_ballot_w64(x == T(0))) {
+                    if (x == T(0)) {
+                        const int64_t r = rank();
+                        if (__builtin_signbit(x)) zn = OP == OP_MAX ? max(zn, r) : min(zn, r);
+                        else zp = OP == OP_MAX ? max(zp, r) : min(zp, r);
+                    }
                 }
+                // order-free value fold: a NaN operand leaves v unchanged (and sets the error flag);
+                // a zero's sign is decided from the ranks in value()
+                if constexpr (OP == OP_MAX) v = __builtin_fmax(v, x);
+                else v = __builtin_fmin(v, x);
+            } else {
+                if constexpr (OP == OP_MAX) v = x > v ? x : v;
+                else v = x < v ? x : v;
             }
-            if constexpr (OP == OP_MAX) v = x > v ? x : v;
-            else v = x < v ? x : v;
         }
     }
 

@@ -379,7 +379,9 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                     // few tiles whose fold budget leaves the chip underfilled (tall, narrow): more slices
                     // and the separate fold launch (k_axis_cols_fold, parallel across outputs)
                     bool sep = tuning().axis_fold_sep == 1;
-                    if (tuning().axis_fold_sep < 0 && tiles * sl * 2 < target) sep = true;
+                    // (below a quarter of the target: at 3/8, [4096,4096] f32 axis-0 max, the in-kernel
+                    // fold measured 25.7 us vs 33.9 us with the fold launch, tools/gpu_colsmax.sh)
+                    if (tuning().axis_fold_sep < 0 && tiles * sl * 4 < target) sep = true;
                     if (sep) {
                         const uint64_t target2 = (uint64_t)ws->cus * 8;
                         sl = std::max<uint64_t>(1, std::min<uint64_t>({(target2 + tiles - 1) / tiles,

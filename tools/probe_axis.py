@@ -27,9 +27,18 @@ CONFIGS = (("axis1_f32_4096x4096_sum", "float32", [4096, 4096], 1, "sum"),
            ("axis2_i32_256x256x256_count_missing", "int32", [256, 256, 256], 2, "count"),
            ("axis0_f64_65536x32_min", "float64", [65536, 32], 0, "min"),
            ("axis1_f32_16x1048576_sum", "float32", [16, 1 << 20], 1, "sum"))
+if "--minmax" in sys.argv:   # sum vs max vs min on the same shapes (float ±0 rank bookkeeping cost)
+    CONFIGS = tuple((f"{nm}_{op}", dt, sh, ax, op) + tuple(rest)
+                    for nm, dt, sh, ax, *rest in (("axis1_f32_4096x4096", "float32", [4096, 4096], 1),
+                                                  ("axis0_f32_4096x4096", "float32", [4096, 4096], 0),
+                                                  ("all_f32_256cube_sel_stride2", "float32", [256, 256, 256], None,
+                                                   [[0, 256, 1], [32, 224, 1], [0, 256, 2]]),
+                                                  ("all_f64_128cube_sel", "float64", [128, 128, 128], None,
+                                                   [[8, 120, 1], [0, 128, 2], [16, 112, 1]]))
+                    for op in ("sum", "max", "min"))
 ra = np.random.default_rng(7)
 COLS_ONLY = ("axis0_f32_4096x4096_sum", "axis1_f32_64x1024x256_sum", "axis0_f64_65536x32_min")
-for name, dtype, shape, axis, op in CONFIGS:
+for name, dtype, shape, axis, op, *sel in CONFIGS:
     if "--cols" in sys.argv and name not in COLS_ONLY:
         continue
     n = int(np.prod(shape))
@@ -37,7 +46,8 @@ for name, dtype, shape, axis, op in CONFIGS:
     mk, mv, nm = (None, b"", 0)
     if op == "count":
         mk, mv, nm = "valid_min", np.int32(0).tobytes(), 1
-    creq = _abi.CRequest(op, dtype, shape=shape, axis=axis, missing_kind=mk, missing_values=mv, n_missing=nm)
+    creq = _abi.CRequest(op, dtype, shape=shape, axis=axis, missing_kind=mk, missing_values=mv, n_missing=nm,
+                         selection=sel[0] if sel else None)
     info = _abi.rdx_response_info()
     assert lib.rdx_plan(creq.ref, vals.nbytes, C.byref(info)) == 0
     reps = max(2, (320 << 20) // vals.nbytes + 1)
