@@ -137,6 +137,29 @@ def test_pm0_tie_rule(engine):
                 assert_parity(engine, op, req, v.tobytes())
 
 
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+@pytest.mark.parametrize("per", [3, 4, 5, 7])
+def test_minmax_long_contiguous_ranges(engine, dtype, per):
+    """Float min/max over whole chunks long enough that every workgroup of k_all_contig folds `per`
+    4096-element tiles (the software-pipelined loop's even/odd exits and its single-tile remainder),
+    plus a ragged tail; ±0 planted everywhere incl. the last tile, so the value is a zero whose sign
+    comes from the fold-order ranks (min_by keeps the FIRST equal, max_by the LAST); plain, and
+    byte-shuffled + big-endian (the fused path)."""
+    rng = np.random.default_rng(100 * per + (dtype == "float64"))
+    n = 4096 * 256 * per + int(rng.integers(1, 4096))
+    base = (np.abs(rng.standard_normal(n)) + 1.0).astype(NP[dtype])
+    pos = np.concatenate([rng.integers(0, n, 48), rng.integers(n - 5000, n, 16)])
+    zeros = np.where(rng.random(pos.size) < 0.5, -0.0, 0.0).astype(NP[dtype])
+    es = np.dtype(NP[dtype]).itemsize
+    for op, sign in (("min", 1.0), ("max", -1.0)):
+        v = (base * sign).astype(NP[dtype])
+        v[pos] = zeros
+        for req in ({"dtype": dtype},
+                    {"dtype": dtype, "byte_order": "big", "filters": [{"id": "shuffle", "element_size": es}]}):
+            raw = v.astype(v.dtype.newbyteorder(">")).tobytes() if req.get("byte_order") == "big" else v.tobytes()
+            assert_parity(engine, op, req, encode_filters(raw, req.get("filters"), oracle.shuffle))
+
+
 def test_nan_raises_like_reference_panic(engine):
     for dtype in ("float32", "float64"):
         v = np.arange(4096, dtype=NP[dtype])
