@@ -396,22 +396,25 @@ __device__ __forceinline__ constexpr int packed_words() {
 }
 
 // AGENT = agent-scope (sc1) accesses for the cross-workgroup hand-off.
+// Word k of the record at P[k * stride]: stride 1 = one record per kW consecutive words; a record
+// array laid out word-major (stride = record count) makes a wave's per-lane stores / loads of one
+// word coalesced.
 template <typename T, int OP, bool AGENT>
-__device__ __forceinline__ void store_packed(uint64_t *P, const Red<T, OP> &r) {
+__device__ __forceinline__ void store_packed(uint64_t *P, const Red<T, OP> &r, uint64_t stride = 1) {
     uint64_t w[kPartialWords];
     r.to_words(w);
     int k = 0;
 #pragma unroll
     for (int i = 0; i < kPartialWords; ++i) {
         if (!word_used<T, OP>(i)) continue;
-        if constexpr (AGENT) __hip_atomic_store(P + k, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else P[k] = w[i];
+        if constexpr (AGENT) __hip_atomic_store(P + k * stride, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else P[k * stride] = w[i];
         ++k;
     }
 }
 
 template <typename T, int OP, bool AGENT>
-__device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r) {
+__device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r, uint64_t stride = 1) {
     Red<T, OP> id;
     id.init();
     uint64_t w[kPartialWords];
@@ -420,8 +423,8 @@ __device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r) {
 #pragma unroll
     for (int i = 0; i < kPartialWords; ++i) {
         if (!word_used<T, OP>(i)) continue;
-        if constexpr (AGENT) w[i] = __hip_atomic_load(P + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else w[i] = P[k];
+        if constexpr (AGENT) w[i] = __hip_atomic_load(P + k * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else w[i] = P[k * stride];
         ++k;
     }
     r.from_words(w);
