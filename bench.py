@@ -1,33 +1,46 @@
 #!/usr/bin/env python3
-"""bench.py — GiB/s of device-resident chunk unshuffle+reduce (f32 sum) on MI355X.
+"""bench.py — GiB/s of device-resident chunk unshuffle+reduce (f32 sum) on 1/2/4/8 MI355X.
 
-Workload (BASELINE.json configs[1], "c2"): 64 MiB chunks of 16 Mi f32 values stored big-endian and
-byte-shuffled (element_size 4), each reduced with `sum` (its own result + count).  8 distinct chunks
-(512 MiB > the 256 MiB Infinity Cache) are resident in HBM before timing; one step = one launch of the
-fused unshuffle + byte-swap + f64-accumulated sum kernel over those 8 independent chunks through the
-engine's batch entry point (rdx_execute_batch_device), so every step streams 512 MiB from HBM and the
-per-launch ramp/finalisation (~6 us, profiles/) is paid once per 8 chunks.  extra.c2_single_chunk
-reports the same chunks at one chunk per launch (rdx_execute_device); extra.c2_concurrent_requests
-issues those single-chunk calls round-robin over 4 HIP streams (one workspace each), as concurrent
-server requests would be (RDX_BENCH_STREAMS overrides the 4).
-Ranks (one per GPU, torchrun) each process their own chunks: weak scaling, no data-path collective
-(the control-plane barrier / max-time reduction uses gloo).
+Headline workload (BASELINE.json configs[1], "c2"): 64 MiB chunks of 16 Mi f32 values stored big-endian
+and byte-shuffled (element_size 4), each reduced with `sum` (its own result + count).  8 distinct chunks
+per GPU (512 MiB > the 256 MiB Infinity Cache) are resident in HBM before timing; one step = one launch
+of the fused unshuffle + byte-swap + f64-accumulated sum kernel over those 8 independent chunks through
+the engine's batch entry point (rdx_execute_batch_device).
 
-Also reported (extra.c4_batch): BASELINE configs[3] — a batch of 1024 independent 4 MiB shuffled f32
-chunks summed by one launch per step, the batch split across ranks (strong scaling of that batch).
-extra.f64_64mib / extra.f64_4mib: the north_star's f64 legs — 8 x 64 MiB and 128 x 4 MiB f64 chunks
-per GPU (big-endian, shuffle element_size 8, sum), one batched launch per step (weak scaling).
+Multi-GPU: one process per GPU, each owning its own chunks (weak scaling, no data-path
+collective; the control-plane barrier and max-over-ranks timing use gloo on the host).  Under torchrun
+the ranks come from the environment; `python bench.py --gpus N` outside torchrun starts N ranks itself
+(a child torchrun, from this parent, which makes no GPU call) and fails loudly when fewer than N GPUs are
+visible.  Every rank uses its own device (LOCAL_RANK); the line reports the distinct devices used.
 
-Roofline: bytes_alg per launch = n_elements * 4 B read (unshuffle / byte swap add no algorithmic
-bytes; the 16 B result is negligible) / average kernel duration from HIP events recorded on the
-launch stream around every step of the timed region; peak = 8.0 TB/s HBM3E (MI355X_MICROARCH.md).
-`traffic` comes from a rocprofv3 PMC pass (profiles/*_pmc.json) when one is committed.
-cpu_baseline: the oracle (CPU restatement of the reference's sequential path) on 1 host core.
+extra (every number DESIGN.md quotes comes from here):
+  c2_single_chunk        the same chunks, one chunk per launch (rdx_execute_device)
+  c2_concurrent_requests one chunk per rdx_execute_device call over 4 HIP streams / workspaces; the
+                         calls are queued behind a gate so the device time is measured (HIP events on
+                         every stream), not the host's issue rate
+  c4_batch               BASELINE configs[3]: 1024 x 4 MiB shuffled f32 chunks, one launch, split over
+                         ranks (strong scaling of that batch)
+  f64_64mib / f64_4mib   the north_star's f64 legs (shuffle es=8, big-endian, sum)
+  c4z_inflate            the batch compressed with zlib, decompressed on the device
+  configs                (N=1) device-resident C1, C3 (min / max / valid_range) and C5 select launches
+  mixed_requests         (N=1) 20 mixed C1/C3 requests in ONE heterogeneous launch (rdx_execute_multi_device)
+  host_inclusive         (N=1) C2 / C3 / C5 through rdx_execute from pageable and pinned host memory,
+                         next to the raw PCIe copy time of the same bytes
+  cpu_baselines          (N=1) the oracle (CPU restatement of the reference path) on host cores: C1 with
+                         and without the per-iteration clone of benches/operations.rs:63, C3, C5; CPU
+                         model, affinity and cgroup quota
+
+Roofline: bytes_alg per launch = n_elements * 4 B read (unshuffle / byte swap add no algorithmic bytes;
+the 16 B result is negligible) / average kernel duration from HIP events recorded on the launch stream
+around every step of the timed region; peak = 8.0 TB/s HBM3E (MI355X_MICROARCH.md).  `traffic` comes
+from a rocprofv3 PMC pass (profiles/c2_pmc.json) when one is committed.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -44,6 +57,9 @@ C2_BYTES = C2_ELEMS * 4
 N_BUF = 8
 C4_CHUNKS = 1024
 C4_ELEMS = 1024 * 1024
+C3_SEL = [[8, 120, 1], [0, 128, 2], [16, 112, 1]]
+C3_NSEL = 112 * 64 * 96
+C5_SEL = [[0, 512, 1], [64, 192, 1], [0, 256, 1]]
 
 
 def parse():
@@ -57,62 +73,38 @@ def parse():
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-inflate", action="store_true")
     ap.add_argument("--no-f64", action="store_true")
+    ap.add_argument("--no-configs", action="store_true")
+    ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--primary-only", action="store_true", help="only the headline batched C2 loop (profiling)")
     return ap.parse_args()
 
 
+# ---- N ranks without an external launcher ----------------------------------------------------------------
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` outside torchrun: N per-GPU ranks as a child torchrun (this process makes no GPU
+    call: torch.cuda.device_count() does not initialise HIP on this image)."""
+    import torch
+    n_dev = torch.cuda.device_count()
+    if args.gpus > n_dev and os.environ.get("RDX_BENCH_OVERSUBSCRIBE") != "1":
+        print(f"bench.py: --gpus {args.gpus} requested but only {n_dev} GPU(s) are visible; refusing to "
+              "report a multi-GPU number from fewer devices (RDX_BENCH_OVERSUBSCRIBE=1 rehearses the N-rank "
+              "code path on shared devices and reports the distinct devices used)", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ---- helpers ------------------------------------------------------------------------------------------------
 def shuffled_be_f32(torch, vals):
     """values (…, n) f32 on device -> big-endian bytes, byte-shuffled with element_size 4
     (src/filters/shuffle.rs:124-135 encoder), laid out (…, 4*n) uint8 contiguous."""
     b = vals.contiguous().view(torch.uint8).reshape(*vals.shape, 4).flip(-1)       # big-endian
     return b.transpose(-1, -2).contiguous().reshape(*vals.shape[:-1], 4 * vals.shape[-1])
-
-
-def f64_batch(torch, ws, stream, g, rank, barrier, max_over_ranks, world, elems, n_chunks, steps):
-    """n_chunks independent HBM-resident f64 chunks (big-endian, shuffle element_size 8, sum) per rank,
-    one rdx_execute_batch_device launch per step; results checked against an f64 sum of the values
-    (f64 chunks are summed Neumaier-compensated, DESIGN.md §3)."""
-    g.manual_seed(0x5EED2000 + rank)
-    vals = torch.rand(n_chunks, elems, device="cuda", generator=g, dtype=torch.float64)
-    exact = vals.sum(dim=1).cpu()
-    b = vals.view(torch.uint8).reshape(n_chunks, elems, 8).flip(-1)            # big-endian
-    chunks = b.transpose(-1, -2).contiguous().reshape(n_chunks, 8 * elems)     # shuffle es=8
-    del vals, b
-    bodies = torch.zeros(n_chunks, dtype=torch.float64, device="cuda")
-    counts = torch.zeros(n_chunks, dtype=torch.int64, device="cuda")
-    status = torch.zeros(n_chunks, dtype=torch.int32, device="cuda")
-    from reductionist_amd import _abi
-    creq = _abi.CRequest("sum", "float64", byte_order="big", filters=[{"id": "shuffle", "element_size": 8}])
-    ptrs = [chunks[i].data_ptr() for i in range(n_chunks)]
-
-    def launch():
-        ws.execute_batch_device(creq, ptrs, 8 * elems, bodies.data_ptr(), counts.data_ptr(), status.data_ptr(),
-                                stream.cuda_stream)
-
-    for _ in range(3):
-        launch()
-    torch.cuda.synchronize()
-    assert int(status.abs().sum()) == 0 and bool((counts.cpu() == elems).all())
-    assert bool(((bodies.cpu() - exact).abs() <= exact.abs() * 2.0 ** -44).all()), (bodies.cpu(), exact)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(steps):
-        launch()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    el = max_over_ranks(t1 - t0)
-    k = e0.elapsed_time(e1) / 1e3 / steps
-    step_bytes = n_chunks * 8 * elems
-    return {"workload": f"{n_chunks} x {8 * elems >> 20} MiB f64 chunks per GPU, big-endian, shuffle es=8, sum; "
-                        "one batched launch per step",
-            "value": round(steps * step_bytes * world / el / GIB, 2), "unit": "GiB/s", "steps": steps,
-            "ms_per_step": round(el / steps * 1e3, 5), "kernel_us_avg": round(k * 1e6, 3),
-            "roofline_frac": round(step_bytes / k / 1e9 / PEAK_GBS, 4)}
 
 
 def traffic_from_profiles(tag):
@@ -125,37 +117,608 @@ def traffic_from_profiles(tag):
     return None
 
 
-def cpu_baseline(seconds):
-    """Oracle on the host: unshuffle + byte swap + sequential f32 fold of one 64 MiB chunk."""
+def cpu_info():
+    """CPU model, the threads this process may run on, and the cgroup CPU quota (the GPU box gives each
+    one-GPU job a share of a large host: nproc shows the whole machine)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = round(q / per, 2) if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def pool_threads():
+    """Worker threads for the multi-chunk CPU baseline: the reference's default thread_limit is
+    num_cpus - 1 (src/app_state.rs:22), capped by the CPUs this job may actually use (affinity, cgroup
+    quota, OMP_NUM_THREADS as the box's stated share)."""
+    info = cpu_info()
+    n = (info["affinity_cpus"] or 2) - 1
+    if info["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(info["cgroup_cpu_quota"]) - 1))
+    if info["omp_num_threads"]:
+        try:
+            n = min(n, max(1, int(info["omp_num_threads"]) - 1))
+        except ValueError:
+            pass
+    return max(1, n)
+
+
+class Ctx:
+    """Per-rank state shared by the legs."""
+
+    def __init__(self, torch, dist, args, world, rank, device):
+        from reductionist_amd import Engine, _abi
+        self.torch, self.dist, self.args = torch, dist, args
+        self.world, self.rank, self.device = world, rank, device
+        self.abi = _abi
+        self.eng = Engine([device])
+        self.ws = self.eng.workspace(device)
+        self.lib = _abi.lib()
+        self.stream = torch.cuda.current_stream()
+        self.sh = C.c_void_p(self.stream.cuda_stream)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def events(self):
+        return (self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True))
+
+    def timed(self, step, n):
+        """n back-to-back launches on one stream, bracketed by barrier + synchronize; HIP events on the
+        launch stream around the same region give the average launch duration (gaps included)."""
+        torch = self.torch
+        ev0, ev1 = self.events()
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(self.stream)
+        for i in range(n):
+            step(i)
+        ev1.record(self.stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        self.barrier()
+        return self.max_over_ranks(t1 - t0), ev0.elapsed_time(ev1) / 1e3 / n
+
+    def dev_time(self, step, n, warm=3):
+        """Device time per launch: HIP events around n back-to-back launches on the launch stream."""
+        for i in range(warm):
+            step(i)
+        self.torch.cuda.synchronize()
+        e0, e1 = self.events()
+        e0.record(self.stream)
+        for i in range(n):
+            step(i)
+        e1.record(self.stream)
+        self.torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / n
+
+    def gate(self, streams, hold_s=0.02):
+        """Hold `streams` behind a device-side sleep so that the host can queue every call before the
+        device starts on them; returns the event that opens the gate (timing starts there)."""
+        torch = self.torch
+        gs = torch.cuda.Stream()
+        with torch.cuda.stream(gs):
+            torch.cuda._sleep(int(hold_s * self.sleep_rate()))
+        opened = torch.cuda.Event(enable_timing=True)
+        opened.record(gs)
+        for s in streams:
+            s.wait_event(opened)
+        return opened
+
+    _rate = None
+
+    def sleep_rate(self):
+        """torch.cuda._sleep cycles per second on this device (measured once)."""
+        if Ctx._rate is None:
+            torch = self.torch
+            e0, e1 = self.events()
+            e0.record(self.stream)
+            torch.cuda._sleep(1_000_000)
+            e1.record(self.stream)
+            torch.cuda.synchronize()
+            Ctx._rate = 1_000_000 / max(1e-6, e0.elapsed_time(e1) / 1e3)
+        return Ctx._rate
+
+
+# ---- legs ---------------------------------------------------------------------------------------------------
+def leg_c2(cx):
+    """Headline: 8 x 64 MiB HBM-resident chunks per GPU, one batched launch per step; plus the single-chunk
+    and concurrent-request legs over the same chunks."""
+    torch, args, lib, _abi = cx.torch, cx.args, cx.lib, cx.abi
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0004 + cx.rank)
+    vals = torch.rand(N_BUF, C2_ELEMS, device="cuda", generator=g, dtype=torch.float32)
+    chunks = shuffled_be_f32(torch, vals)
+    exact = vals.double().sum(dim=1).cpu()
+    del vals
+    bodies = torch.zeros(N_BUF, dtype=torch.float32, device="cuda")
+    counts = torch.zeros(N_BUF, dtype=torch.int64, device="cuda")
+    status = torch.zeros(N_BUF, dtype=torch.int32, device="cuda")
+    creq = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
+    info = _abi.rdx_response_info()
+    ptrs = (C.c_void_p * N_BUF)(*[chunks[i].data_ptr() for i in range(N_BUF)])
+    batch_args = (cx.ws.ws, creq.ref, N_BUF, ptrs, C2_BYTES, C.c_void_p(bodies.data_ptr()),
+                  C.c_void_p(counts.data_ptr()), C.c_void_p(status.data_ptr()), cx.sh, C.byref(info))
+    single_args = [(cx.ws.ws, creq.ref, C.c_void_p(chunks[i].data_ptr()), C2_BYTES, C.c_void_p(bodies[i:].data_ptr()),
+                    C.c_void_p(counts[i:].data_ptr()), C.c_void_p(status[i:].data_ptr()), cx.sh, C.byref(info))
+                   for i in range(N_BUF)]
+
+    def check_results():
+        torch.cuda.synchronize()
+        got = bodies.double().cpu()
+        assert int(status.abs().sum()) == 0 and bool((counts.cpu() == C2_ELEMS).all()), (status.cpu(), counts.cpu())
+        tol = exact.abs() * 2.0 ** -23 + 1e-3
+        assert bool(((got - exact).abs() <= tol).all()), (got, exact)
+        bodies.zero_()
+        counts.zero_()
+        torch.cuda.synchronize()
+
+    def batch_step(i):
+        st = lib.rdx_execute_batch_device(*batch_args)
+        if st:
+            raise RuntimeError(f"rdx_execute_batch_device failed: {_abi.status_string(st)}")
+
+    def single_step(i):
+        st = lib.rdx_execute_device(*single_args[i % N_BUF])
+        if st:
+            raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
+
+    for i in range(max(args.warmup, 1)):   # (at least one launch, so the check below has results)
+        batch_step(i)
+    check_results()                       # what we time is correct: every chunk vs an f64 sum
+    elapsed, kern_avg_s = cx.timed(batch_step, args.steps)
+    check_results()
+    step_bytes = N_BUF * C2_BYTES
+    out = {"value": args.steps * step_bytes * cx.world / elapsed / GIB, "elapsed": elapsed,
+           "kern_avg_s": kern_avg_s, "step_bytes": step_bytes, "extra": {}}
+    if args.primary_only:
+        return out
+    extra = out["extra"]
+    for i in range(max(args.warmup, N_BUF)):   # every chunk at least once, whatever --warmup is
+        single_step(i)
+    check_results()
+    el1, k1 = cx.timed(single_step, args.steps)
+    check_results()
+    extra["c2_single_chunk"] = {
+        "workload": "the same 64 MiB chunks, one chunk per launch (rdx_execute_device), one stream",
+        "value": round(args.steps * C2_BYTES * cx.world / el1 / GIB, 2), "unit": "GiB/s",
+        "ms_per_step": round(el1 / args.steps * 1e3, 5), "kernel_us_avg": round(k1 * 1e6, 3),
+        "roofline_frac": round(C2_BYTES / k1 / 1e9 / PEAK_GBS, 4)}
+
+    # concurrent single-chunk requests, the way a server runs them (one request per worker thread,
+    # app.rs:123-153): one workspace + HIP stream per in-flight request, chunks round-robin, so one
+    # launch's ramp / hand-off tail overlaps the next launch's streaming.  The calls are queued behind a
+    # device-side gate and timed with events on every stream (K fixed, independent of --steps).
+    n_st = int(os.environ.get("RDX_BENCH_STREAMS", "4"))
+    k_conc = max(args.steps, 400)
+    sts = [torch.cuda.Stream() for _ in range(n_st)]
+    wss = [cx.eng.workspace(cx.device) for _ in range(n_st)]
+    conc_args = [(wss[i % n_st].ws,) + single_args[i][1:-2] + (C.c_void_p(sts[i % n_st].cuda_stream),
+                                                               single_args[i][-1]) for i in range(N_BUF)]
+
+    def conc_step(i):
+        st = lib.rdx_execute_device(*conc_args[i % N_BUF])
+        if st:
+            raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
+
+    for s in sts:   # the zeroing in check_results() ran on the launch stream
+        s.wait_stream(cx.stream)
+    for i in range(max(args.warmup, N_BUF)):
+        conc_step(i)
+    check_results()
+    for s in sts:
+        s.wait_stream(cx.stream)
+    cx.barrier()
+    torch.cuda.synchronize()
+    opened = cx.gate(sts, hold_s=0.01 + k_conc * 15e-6)
+    for i in range(k_conc):
+        conc_step(i)
+    ends = []
+    for s in sts:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(s)
+        ends.append(e)
+    torch.cuda.synchronize()
+    dev_s = max(opened.elapsed_time(e) for e in ends) / 1e3
+    elc = cx.max_over_ranks(dev_s)
+    cx.barrier()
+    check_results()
+    extra["c2_concurrent_requests"] = {
+        "workload": f"the same 64 MiB chunks, one chunk per rdx_execute_device call, {n_st} streams / "
+                    f"workspaces round-robin (concurrent requests), {k_conc} requests",
+        "value": round(k_conc * C2_BYTES * cx.world / elc / GIB, 2), "unit": "GiB/s",
+        "us_per_request": round(elc / k_conc * 1e6, 3),
+        "roofline_frac": round(k_conc * C2_BYTES / elc / 1e9 / PEAK_GBS, 4),
+        "timing": "calls queued behind a device-side gate; HIP events: gate open -> last stream's end"}
+    for w in wss:
+        w.close()
+    return out
+
+
+def leg_c4(cx):
+    """BASELINE configs[3]: 1024 x 4 MiB f32 chunks, shuffle es=4, sum; the batch is split over ranks."""
+    torch, args, _abi = cx.torch, cx.args, cx.abi
+    from reductionist_amd.sharding import shard_range
+    lo4, hi4 = shard_range(C4_CHUNKS, cx.rank, cx.world)
+    n_local = hi4 - lo4
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED1000 + lo4)
+    v4 = torch.rand(n_local, C4_ELEMS, device="cuda", generator=g, dtype=torch.float32)
+    ex4 = v4.double().sum(dim=1).cpu()
+    c4 = v4.view(torch.uint8).reshape(n_local, C4_ELEMS, 4).transpose(1, 2).contiguous().reshape(n_local, -1)
+    del v4
+    b4 = torch.zeros(n_local, dtype=torch.float32, device="cuda")
+    n4 = torch.zeros(n_local, dtype=torch.int64, device="cuda")
+    s4 = torch.zeros(n_local, dtype=torch.int32, device="cuda")
+    creq4 = _abi.CRequest("sum", "float32", filters=[{"id": "shuffle", "element_size": 4}])
+    ptrs = [c4[i].data_ptr() for i in range(n_local)]
+
+    def step(i):
+        cx.ws.execute_batch_device(creq4, ptrs, 4 * C4_ELEMS, b4.data_ptr(), n4.data_ptr(), s4.data_ptr(),
+                                   cx.stream.cuda_stream)
+
+    for i in range(2):
+        step(i)
+    torch.cuda.synchronize()
+    assert bool((n4.cpu() == C4_ELEMS).all()) and int(s4.abs().sum()) == 0
+    assert bool(((b4.double().cpu() - ex4).abs() <= ex4.abs() * 2.0 ** -23 + 1e-3).all())
+    el4, k4 = cx.timed(step, args.c4_steps)
+    out = {"workload": "1024 x 4 MiB f32 chunks, shuffle es=4, native order, sum; batch split over ranks, one "
+                       "rdx_execute_batch_device launch per rank per step",
+           "value": round(args.c4_steps * C4_CHUNKS * 4 * C4_ELEMS / el4 / GIB, 2), "unit": "GiB/s",
+           "scaling": "strong", "steps": args.c4_steps, "ms_per_step": round(el4 / args.c4_steps * 1e3, 4),
+           "chunks_per_rank": n_local, "kernel_us_avg": round(k4 * 1e6, 2),
+           "roofline_frac": round(n_local * 4 * C4_ELEMS / k4 / 1e9 / PEAK_GBS, 4)}
+    del c4
+    return out
+
+
+def leg_f64(cx, elems, n_chunks, steps):
+    """n_chunks independent HBM-resident f64 chunks (big-endian, shuffle element_size 8, sum) per rank,
+    one rdx_execute_batch_device launch per step; results checked against an f64 sum of the values
+    (f64 chunks are summed Neumaier-compensated, DESIGN.md §3)."""
+    torch, _abi = cx.torch, cx.abi
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED2000 + cx.rank)
+    vals = torch.rand(n_chunks, elems, device="cuda", generator=g, dtype=torch.float64)
+    exact = vals.sum(dim=1).cpu()
+    b = vals.view(torch.uint8).reshape(n_chunks, elems, 8).flip(-1)            # big-endian
+    chunks = b.transpose(-1, -2).contiguous().reshape(n_chunks, 8 * elems)     # shuffle es=8
+    del vals, b
+    bodies = torch.zeros(n_chunks, dtype=torch.float64, device="cuda")
+    counts = torch.zeros(n_chunks, dtype=torch.int64, device="cuda")
+    status = torch.zeros(n_chunks, dtype=torch.int32, device="cuda")
+    creq = _abi.CRequest("sum", "float64", byte_order="big", filters=[{"id": "shuffle", "element_size": 8}])
+    ptrs = [chunks[i].data_ptr() for i in range(n_chunks)]
+
+    def step(i):
+        cx.ws.execute_batch_device(creq, ptrs, 8 * elems, bodies.data_ptr(), counts.data_ptr(), status.data_ptr(),
+                                   cx.stream.cuda_stream)
+
+    for i in range(3):
+        step(i)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0 and bool((counts.cpu() == elems).all())
+    assert bool(((bodies.cpu() - exact).abs() <= exact.abs() * 2.0 ** -44).all()), (bodies.cpu(), exact)
+    el, k = cx.timed(step, steps)
+    step_bytes = n_chunks * 8 * elems
+    return {"workload": f"{n_chunks} x {8 * elems >> 20} MiB f64 chunks per GPU, big-endian, shuffle es=8, sum; "
+                        "one batched launch per step",
+            "value": round(steps * step_bytes * cx.world / el / GIB, 2), "unit": "GiB/s", "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 5), "kernel_us_avg": round(k * 1e6, 3),
+            "roofline_frac": round(step_bytes / k / 1e9 / PEAK_GBS, 4)}
+
+
+def leg_inflate(cx, with_cpu, n_total=1024, distinct=16, reps=3):
+    """BASELINE configs[3]'s batch shape with zlib on top: 1024 x 4 MiB N(0,1) f32 chunks, byte-shuffled,
+    zlib level 1 (distinct chunks cycled), split over ranks; one rdx_decompress_batch_device launch per
+    rep.  GB/s of decompressed output; CPU: CPython zlib (the C library) on a thread pool."""
+    import zlib
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from reductionist_amd.sharding import shard_range
+    torch = cx.torch
+    lo, hi = shard_range(n_total, cx.rank, cx.world)
+    n = hi - lo
+    rng = np.random.default_rng(0x5EED2000)
+    raws, streams = [], []
+    for _ in range(distinct):
+        v = rng.standard_normal(C4_ELEMS).astype(np.float32)
+        raw = v.view(np.uint8).reshape(C4_ELEMS, 4).T.copy().tobytes()
+        c = zlib.compressobj(1, zlib.DEFLATED, 15)
+        raws.append(raw)
+        streams.append(c.compress(raw) + c.flush())
+    offs, total = [], 0
+    for s in streams:
+        offs.append(total)
+        total += (len(s) + 255) // 256 * 256
+    host = np.zeros(total, dtype=np.uint8)
+    for o, s in zip(offs, streams):
+        host[o:o + len(s)] = np.frombuffer(s, dtype=np.uint8)
+    d_in = torch.from_numpy(host).cuda()
+    raw_len = 4 * C4_ELEMS
+    d_out = torch.empty(max(1, n) * raw_len, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+    d_err = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
+    ptrs = [d_in.data_ptr() + offs[(lo + i) % distinct] for i in range(n)]
+    lens = [len(streams[(lo + i) % distinct]) for i in range(n)]
+
+    def step(i):
+        cx.ws.decompress_batch_device("zlib", ptrs, lens, d_out.data_ptr(), raw_len, d_len.data_ptr(),
+                                      d_err.data_ptr(), cx.stream.cuda_stream)
+
+    step(0)
+    torch.cuda.synchronize()
+    assert int(d_err.abs().sum()) == 0 and bool((d_len == raw_len).all())
+    assert d_out[:raw_len].cpu().numpy().tobytes() == raws[lo % distinct]
+    t = cx.dev_time(step, reps, warm=0)
+    out = {"workload": "1024 x 4 MiB N(0,1) f32 chunks, shuffle es=4, zlib level 1 (ratio %.2f), batch split over "
+                       "ranks; one rdx_decompress_batch_device launch" % (raw_len * distinct / sum(len(s) for s in streams)),
+           "value": round(n * raw_len / t / 1e9, 2), "unit": "GB/s decompressed (this rank)", "ms_per_launch":
+           round(t * 1e3, 2), "kernel": "k_inflate", "bound": "serial decode per wavefront (DESIGN.md §9), not HBM"}
+    if with_cpu:
+        threads = pool_threads()
+
+        def one(i):
+            zlib.decompress(streams[i % distinct])
+
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, range(threads)))
+            c0 = time.perf_counter()
+            list(ex.map(one, range(n_total)))
+            tz = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": round(n_total * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
+                               "kind": "library", "sample": f"CPython zlib.decompress of all {n_total} streams on a "
+                                                            f"{threads}-thread pool, {tz:.2f} s"}
+    return out
+
+
+def _c3_host():
+    import numpy as np
+    rng = np.random.default_rng(0x5EED0005)
+    v = rng.standard_normal(128 ** 3) * 100
+    v[rng.random(v.size) < 0.05] = -9999.0
+    return v
+
+
+def _c3_req(_abi, op, kind="missing_value", vals=(-9999.0,)):
+    import numpy as np
+    mv = b"".join(np.float64(x).tobytes() for x in vals)
+    return _abi.CRequest(op, "float64", shape=[128, 128, 128], selection=C3_SEL, missing_kind=kind, missing_values=mv,
+                         n_missing=len(vals))
+
+
+def leg_configs(cx):
+    """Device-resident launches of BASELINE configs[0], [2] and [4] on rotating buffers larger than the
+    Infinity Cache (HIP events on the launch stream; results checked once)."""
+    import numpy as np
+    torch, lib, _abi = cx.torch, cx.lib, cx.abi
+    out = {}
+
+    def single(creq, bufs, nbytes, k):
+        info = _abi.rdx_response_info()
+        assert lib.rdx_plan(creq.ref, nbytes, C.byref(info)) == 0
+        body = torch.zeros(max(16, info.body_bytes), dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(max(2, info.n_counts), dtype=torch.int64, device="cuda")
+        status = torch.zeros(4, dtype=torch.int32, device="cuda")
+        args = [(cx.ws.ws, creq.ref, C.c_void_p(b.data_ptr()), nbytes, C.c_void_p(body.data_ptr()),
+                 C.c_void_p(counts.data_ptr()), C.c_void_p(status.data_ptr()), cx.sh, C.byref(info)) for b in bufs]
+
+        def step(i):
+            st = lib.rdx_execute_device(*args[i % len(args)])
+            if st:
+                raise RuntimeError(_abi.status_string(st))
+
+        t = cx.dev_time(step, k, warm=len(bufs))
+        assert int(status.abs().sum()) == 0
+        return t, body, counts
+
+    # C1: f32 4 MiB contiguous sum (D-real), 64 rotating buffers
+    r1 = np.random.default_rng(0x5EED0002)
+    v1 = r1.random(1 << 20, dtype=np.float32)
+    c1 = [torch.from_numpy(v1).cuda() for _ in range(64)]
+    t, body, _ = single(_abi.CRequest("sum", "float32"), c1, 4 << 20, 1000)
+    assert abs(float(body[:4].view(torch.float32)[0]) - float(v1.astype(np.float64).sum())) < 1e-2
+    out["c1_sum_4mib"] = {"us_per_launch": round(t * 1e6, 2), "bytes_alg": 4 << 20,
+                          "roofline_frac": round((4 << 20) / t / 1e9 / PEAK_GBS, 4)}
+    # the same 64 chunks as ONE batched launch
+    bb = torch.zeros(64, dtype=torch.float32, device="cuda")
+    bc = torch.zeros(64, dtype=torch.int64, device="cuda")
+    bs = torch.zeros(64, dtype=torch.int32, device="cuda")
+    creq1 = _abi.CRequest("sum", "float32")
+    t = cx.dev_time(lambda i: cx.ws.execute_batch_device(creq1, [b.data_ptr() for b in c1], 4 << 20, bb.data_ptr(),
+                                                         bc.data_ptr(), bs.data_ptr(), cx.stream.cuda_stream), 100)
+    out["c1_batch64"] = {"us_per_launch": round(t * 1e6, 2), "us_per_chunk": round(t / 64 * 1e6, 3),
+                         "roofline_frac": round(64 * (4 << 20) / t / 1e9 / PEAK_GBS, 4)}
+    del c1
+    # C3: f64 [128,128,128] hyperslab, missing_value -9999 at 5 %, min / max, and a valid_range max
+    v3 = _c3_host()
+    c3 = [torch.from_numpy(v3).cuda() for _ in range(20)]
+    for name, creq in (("c3_min_missing_value", _c3_req(_abi, "min")), ("c3_max_missing_value", _c3_req(_abi, "max")),
+                       ("c3_max_valid_range", _c3_req(_abi, "max", "valid_range", (-250.0, 250.0)))):
+        t, body, _ = single(creq, c3, 16 << 20, 1000)
+        out[name] = {"us_per_launch": round(t * 1e6, 2), "bytes_alg": C3_NSEL * 8 + 16,
+                     "roofline_frac": round((C3_NSEL * 8 + 16) / t / 1e9 / PEAK_GBS, 4)}
+    bb = torch.zeros(20, dtype=torch.float64, device="cuda")
+    bc = torch.zeros(20, dtype=torch.int64, device="cuda")
+    bs = torch.zeros(20, dtype=torch.int32, device="cuda")
+    creq3 = _c3_req(_abi, "min")
+    t = cx.dev_time(lambda i: cx.ws.execute_batch_device(creq3, [b.data_ptr() for b in c3], 16 << 20, bb.data_ptr(),
+                                                         bc.data_ptr(), bs.data_ptr(), cx.stream.cuda_stream), 100)
+    out["c3_min_batch20"] = {"us_per_launch": round(t * 1e6, 2), "us_per_chunk": round(t / 20 * 1e6, 3),
+                             "roofline_frac": round(20 * (C3_NSEL * 8 + 16) / t / 1e9 / PEAK_GBS, 4)}
+    del c3
+    # C5: i64 [512,256,256] select -> 128 MiB
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0006)
+    c5 = [torch.randint(-2 ** 62, 2 ** 62, (512 * 256 * 256,), dtype=torch.int64, device="cuda", generator=g)
+          for _ in range(2)]
+    creq5 = _abi.CRequest("select", "int64", shape=[512, 256, 256], selection=C5_SEL)
+    t, body, counts = single(creq5, c5, 256 << 20, 40)
+    assert torch.equal(body.view(torch.int64).view(512, 128, 256), c5[1].view(512, 256, 256)[:, 64:192, :])
+    out["c5_select"] = {"us_per_launch": round(t * 1e6, 2), "bytes_alg": 2 * (128 << 20),
+                        "roofline_frac": round(2 * (128 << 20) / t / 1e9 / PEAK_GBS, 4),
+                        "note": "128 MiB read + 128 MiB written"}
+    return out
+
+
+def leg_host(cx):
+    """Host-inclusive rates (chunk in host memory -> H2D -> kernels -> D2H through rdx_execute), pageable and
+    page-locked (rdx_host_alloc) buffers, next to the raw PCIe copy of the same bytes (torch, pinned)."""
+    import numpy as np
+    torch, lib, _abi = cx.torch, cx.lib, cx.abi
+    out = {}
+
+    def pcie(nbytes_h2d, nbytes_d2h, reps=5):
+        h = torch.empty(max(nbytes_h2d, 16), dtype=torch.uint8).pin_memory()
+        d = torch.empty(max(nbytes_h2d, 16), dtype=torch.uint8, device="cuda")
+        hd = torch.empty(max(nbytes_d2h, 16), dtype=torch.uint8).pin_memory()
+        d.copy_(h, non_blocking=True)
+        hd.copy_(d[:max(nbytes_d2h, 16)], non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            d.copy_(h, non_blocking=True)
+            torch.cuda.synchronize()
+        th = (time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            hd.copy_(d[:max(nbytes_d2h, 16)], non_blocking=True)
+            torch.cuda.synchronize()
+        td = (time.perf_counter() - t0) / reps if nbytes_d2h > 64 else 0.0
+        return th, td
+
+    def host_buf(nbytes, pinned):
+        if pinned:
+            p = C.c_void_p()
+            assert lib.rdx_host_alloc(cx.eng.ctx, nbytes, C.byref(p)) == 0
+            return p, np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(p.value))
+        arr = np.empty(nbytes, dtype=np.uint8)
+        return C.c_void_p(arr.ctypes.data), arr
+
+    def run(name, creq, data, reps):
+        info = _abi.rdx_response_info()
+        assert lib.rdx_plan(creq.ref, data.nbytes, C.byref(info)) == 0
+        th, td = pcie(data.nbytes, info.body_bytes)
+        res = {"h2d_bytes": int(data.nbytes), "d2h_bytes": int(info.body_bytes),
+               "pcie_pinned_copy_ms": round((th + td) * 1e3, 3), "pcie_h2d_GBs": round(data.nbytes / th / 1e9, 1)}
+        for pinned in (False, True):
+            src, arr = host_buf(data.nbytes, pinned)
+            arr[:] = data.view(np.uint8).reshape(-1)
+            body_p, body_arr = host_buf(max(16, info.body_bytes), pinned)   # (keep the array alive)
+            counts = (C.c_int64 * max(1, info.n_counts))()
+            o = _abi.rdx_response_info()
+            for _ in range(2):
+                st = lib.rdx_execute(cx.eng.ctx, creq.ref, src, data.nbytes, body_p, info.body_bytes, counts,
+                                     info.n_counts, C.byref(o))
+                assert st == 0, (name, "pinned" if pinned else "pageable", _abi.status_string(st))
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                lib.rdx_execute(cx.eng.ctx, creq.ref, src, data.nbytes, body_p, info.body_bytes, counts,
+                                info.n_counts, C.byref(o))
+            t = (time.perf_counter() - t0) / reps
+            key = "pinned" if pinned else "pageable"
+            res[f"{key}_ms"] = round(t * 1e3, 3)
+            res[f"{key}_GiBs_chunk"] = round(data.nbytes / t / GIB, 2)
+            res[f"{key}_over_pcie"] = round(t / (th + td), 3)
+            if pinned:
+                lib.rdx_host_free(cx.eng.ctx, src)
+                lib.rdx_host_free(cx.eng.ctx, body_p)
+        out[name] = res
+
+    vals = np.random.default_rng(4).random(C2_ELEMS, dtype=np.float32)
+    c2 = np.ascontiguousarray(vals.astype(">f4").view(np.uint8).reshape(-1, 4).T).reshape(-1)
+    run("c2_sum_64mib", cx.abi.CRequest("sum", "float32", byte_order="big",
+                                        filters=[{"id": "shuffle", "element_size": 4}]), c2, 20)
+    run("c3_min_16mib", _c3_req(_abi, "min"), _c3_host(), 40)
+    c5 = np.random.default_rng(6).integers(-2 ** 62, 2 ** 62, 512 * 256 * 256, dtype=np.int64)
+    run("c5_select_256mib", _abi.CRequest("select", "int64", shape=[512, 256, 256], selection=C5_SEL), c5, 6)
+    return out
+
+
+def leg_cpu(cx, seconds):
+    """The oracle (CPU restatement of the reference's sequential path, g++ -O2) on the GPU box's host:
+    headline C2 on one core, C1 with / without the clone, C3, C5, each a bounded sample."""
     import numpy as np
     from oracle import py_oracle as oracle
-    from reductionist_amd import _abi
-    rng = np.random.default_rng(0x5EED0004)
-    vals = rng.random(C2_ELEMS, dtype=np.float32)
+    _abi = cx.abi
+    res = {}
+
+    def reps_for(creq, data, budget, clone=True):
+        t1 = oracle.bench(creq, data, 1, clone)
+        return max(1, int(budget / max(t1, 1e-6)))
+
+    # headline C2: one 64 MiB shuffled big-endian chunk, sum
+    vals = np.random.default_rng(0x5EED0004).random(C2_ELEMS, dtype=np.float32)
     data = vals.astype(">f4").view(np.uint8).reshape(C2_ELEMS, 4).T.copy().tobytes()
     creq = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
-    lib = oracle.lib()
-    src = C.create_string_buffer(data, len(data))
-    body = (C.c_uint8 * 64)()
-    counts = (C.c_int64 * 8)()
-    info = _abi.rdx_response_info()
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        st = lib.oracle_execute(C.addressof(creq.c), src, len(data), body, 64, counts, 8, C.byref(info))
-        assert st == 0
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 1000:
-            break
-    return {"value": round(reps * C2_BYTES / el / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x one 64 MiB chunk (16 Mi f32, big-endian, shuffle es=4), sum, sequential "
-                      f"oracle/rdx_oracle.cpp g++ -O2 on 1 host core, {el:.1f} s"}
+    n = reps_for(creq, data, seconds)
+    t = oracle.bench(creq, data, n, True)
+    headline = {"value": round(C2_BYTES / t / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"{n} x one 64 MiB chunk (16 Mi f32, big-endian, shuffle es=4), sum, sequential "
+                          f"oracle/rdx_oracle.cpp g++ -O2 on 1 host core, {n * t:.1f} s"}
+    # C1 (BASELINE configs[0], the reference's own CPU bench case): with and without the clone
+    v1 = np.random.default_rng(0x5EED0002).random(1 << 20, dtype=np.float32).tobytes()
+    creq1 = _abi.CRequest("sum", "float32")
+    for clone in (True, False):
+        n = reps_for(creq1, v1, 3.0, clone)
+        t = oracle.bench(creq1, v1, n, clone)
+        res["c1_sum_4mib_" + ("clone" if clone else "noclone")] = {
+            "us_per_request": round(t * 1e6, 1), "GiBs": round((4 << 20) / t / GIB, 3), "reps": n,
+            "note": "data.clone() inside the timed loop as benches/operations.rs:63" if clone else
+                    "one buffer, no per-iteration copy"}
+    v3 = _c3_host().tobytes()
+    for name, creq3 in (("c3_min_missing_value", _c3_req(_abi, "min")), ("c3_max_missing_value", _c3_req(_abi, "max"))):
+        n = reps_for(creq3, v3, 2.0)
+        t = oracle.bench(creq3, v3, n, True)
+        res[name] = {"us_per_request": round(t * 1e6, 1), "reps": n,
+                     "GBs_alg": round((C3_NSEL * 8) / t / 1e9, 3)}
+    v5 = np.random.default_rng(6).integers(-2 ** 62, 2 ** 62, 512 * 256 * 256, dtype=np.int64).tobytes()
+    creq5 = _abi.CRequest("select", "int64", shape=[512, 256, 256], selection=C5_SEL)
+    n = reps_for(creq5, v5, 3.0)
+    t = oracle.bench(creq5, v5, n, True)
+    res["c5_select"] = {"ms_per_request": round(t * 1e3, 2), "reps": n,
+                        "GBs_alg": round(2 * (128 << 20) / t / 1e9, 3)}
+    res["host"] = cpu_info()
+    return headline, res
 
 
 def cpu_baseline_c4(threads, distinct=64):
     """C4 on the host the way the reference serves it: independent requests on a worker pool
-    (thread_limit = num_cpus - 1, src/app_state.rs:22; capped at the box's CPU share).  1024 chunks of
-    4 MiB (64 distinct, cycled), unshuffle + f32 sum each, by the oracle; ctypes releases the GIL."""
+    (thread_limit = num_cpus - 1, src/app_state.rs:22; capped at the CPUs this job may use).  1024 chunks
+    of 4 MiB (64 distinct, cycled), unshuffle + f32 sum each, by the oracle; ctypes releases the GIL."""
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     from oracle import py_oracle as oracle
@@ -186,302 +749,103 @@ def cpu_baseline_c4(threads, distinct=64):
                                       f"threads, oracle g++ -O2, {el:.2f} s"}
 
 
-def inflate_batch(torch, ws, stream, rank, world, with_cpu, n_total=1024, distinct=16, reps=3):
-    """BASELINE configs[3]'s batch shape with zlib on top: 1024 x 4 MiB N(0,1) f32 chunks, byte-shuffled,
-    zlib level 1 (distinct chunks cycled), split over ranks; one rdx_decompress_batch_device launch per
-    rep.  GB/s of decompressed output; CPU: CPython zlib (the C library) on 15 threads."""
-    import zlib
-    import numpy as np
-    from concurrent.futures import ThreadPoolExecutor
-    from reductionist_amd.sharding import shard_range
-    lo, hi = shard_range(n_total, rank, world)
-    n = hi - lo
-    rng = np.random.default_rng(0x5EED2000)
-    raws, streams = [], []
-    for _ in range(distinct):
-        v = rng.standard_normal(C4_ELEMS).astype(np.float32)
-        raw = v.view(np.uint8).reshape(C4_ELEMS, 4).T.copy().tobytes()
-        c = zlib.compressobj(1, zlib.DEFLATED, 15)
-        raws.append(raw)
-        streams.append(c.compress(raw) + c.flush())
-    offs, total = [], 0
-    for s in streams:
-        offs.append(total)
-        total += (len(s) + 255) // 256 * 256
-    host = np.zeros(total, dtype=np.uint8)
-    for o, s in zip(offs, streams):
-        host[o:o + len(s)] = np.frombuffer(s, dtype=np.uint8)
-    d_in = torch.from_numpy(host).cuda()
-    raw_len = 4 * C4_ELEMS
-    d_out = torch.empty(max(1, n) * raw_len, dtype=torch.uint8, device="cuda")
-    d_len = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
-    d_err = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
-    ptrs = [d_in.data_ptr() + offs[(lo + i) % distinct] for i in range(n)]
-    lens = [len(streams[(lo + i) % distinct]) for i in range(n)]
-
-    def launch():
-        ws.decompress_batch_device("zlib", ptrs, lens, d_out.data_ptr(), raw_len, d_len.data_ptr(),
-                                   d_err.data_ptr(), stream.cuda_stream)
-
-    launch()
-    torch.cuda.synchronize()
-    assert int(d_err.abs().sum()) == 0 and bool((d_len == raw_len).all())
-    assert d_out[:raw_len].cpu().numpy().tobytes() == raws[lo % distinct]
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(reps):
-        launch()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / 1e3 / reps
-    out = {"workload": "1024 x 4 MiB N(0,1) f32 chunks, shuffle es=4, zlib level 1 (ratio %.2f), batch split over "
-                       "ranks; one rdx_decompress_batch_device launch" % (raw_len * distinct / sum(len(s) for s in streams)),
-           "value": round(n * raw_len / t / 1e9, 2), "unit": "GB/s decompressed (this rank)", "ms_per_launch":
-           round(t * 1e3, 2), "kernel": "k_inflate", "bound": "serial decode per wavefront (DESIGN.md §9), not HBM"}
-    if with_cpu:
-        threads = max(1, min(15, (os.cpu_count() or 2) - 1))
-
-        def one(i):
-            zlib.decompress(streams[i % distinct])
-
-        with ThreadPoolExecutor(threads) as ex:
-            list(ex.map(one, range(threads)))
-            c0 = time.perf_counter()
-            list(ex.map(one, range(n_total)))
-            tz = time.perf_counter() - c0
-        out["cpu_baseline"] = {"value": round(n_total * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
-                               "kind": "library", "sample": f"CPython zlib.decompress of all {n_total} streams on a "
-                                                            f"{threads}-thread pool, {tz:.2f} s"}
-    return out
+def devices_used(cx):
+    """(host, PCI bus / uuid) of this rank's device, gathered over ranks."""
+    torch = cx.torch
+    p = torch.cuda.get_device_properties(cx.device)
+    ident = None
+    for attr in ("uuid", "pci_bus_id"):
+        v = getattr(p, attr, None)
+        if v is not None:
+            ident = f"{attr}={v}"
+            break
+    mine = f"{socket.gethostname()}:{ident or f'device{cx.device}'}"
+    if cx.world == 1:
+        return [mine]
+    allv = [None] * cx.world
+    cx.dist.all_gather_object(allv, mine)
+    return allv
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "LOCAL_RANK" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    oversub = os.environ.get("RDX_BENCH_OVERSUBSCRIBE") == "1"
+    n_dev = torch.cuda.device_count()
+    if local_rank >= n_dev and not oversub:
+        raise SystemExit(f"bench.py: rank {rank} (local {local_rank}) has no GPU of its own ({n_dev} visible)")
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    from reductionist_amd import Engine, _abi
-    from reductionist_amd.sharding import device_for, shard_range
-
-    device = device_for(local_rank, torch.cuda.device_count())
+    device = local_rank % n_dev
     torch.cuda.set_device(device)
+    cx = Ctx(torch, dist, args, world, rank, device)
+    devs = devices_used(cx)
+    n_gpus = len(set(devs))
+    if n_gpus != world and not oversub:
+        raise SystemExit(f"bench.py: {world} ranks share {n_gpus} device(s): {devs}")
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    def max_over_ranks(x):
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t[0])
-
-    eng = Engine([device])
-    ws = eng.workspace(device)
-    lib = _abi.lib()
-    stream = torch.cuda.current_stream()
-    sh = C.c_void_p(stream.cuda_stream)
-
-    # ---- C2: 8 distinct 64 MiB chunks resident in HBM --------------------------------------------------
-    g = torch.Generator(device="cuda")
-    g.manual_seed(0x5EED0004 + rank)
-    vals = torch.rand(N_BUF, C2_ELEMS, device="cuda", generator=g, dtype=torch.float32)
-    chunks = shuffled_be_f32(torch, vals)
-    exact = vals.double().sum(dim=1).cpu()
-    del vals
-    bodies = torch.zeros(N_BUF, dtype=torch.float32, device="cuda")
-    counts = torch.zeros(N_BUF, dtype=torch.int64, device="cuda")
-    status = torch.zeros(N_BUF, dtype=torch.int32, device="cuda")
-    creq = _abi.CRequest("sum", "float32", byte_order="big", filters=[{"id": "shuffle", "element_size": 4}])
-    info = _abi.rdx_response_info()
-    ptrs = (C.c_void_p * N_BUF)(*[chunks[i].data_ptr() for i in range(N_BUF)])
-    batch_args = (ws.ws, creq.ref, N_BUF, ptrs, C2_BYTES, C.c_void_p(bodies.data_ptr()),
-                  C.c_void_p(counts.data_ptr()), C.c_void_p(status.data_ptr()), sh, C.byref(info))
-    single_args = [(ws.ws, creq.ref, C.c_void_p(chunks[i].data_ptr()), C2_BYTES, C.c_void_p(bodies[i:].data_ptr()),
-                    C.c_void_p(counts[i:].data_ptr()), C.c_void_p(status[i:].data_ptr()), sh, C.byref(info))
-                   for i in range(N_BUF)]
-
-    def check_results():
-        torch.cuda.synchronize()
-        got = bodies.double().cpu()
-        assert int(status.abs().sum()) == 0 and bool((counts.cpu() == C2_ELEMS).all()), (status.cpu(), counts.cpu())
-        tol = exact.abs() * 2.0 ** -23 + 1e-3
-        assert bool(((got - exact).abs() <= tol).all()), (got, exact)
-        bodies.zero_()
-        counts.zero_()
-
-    def batch_step(i):
-        st = lib.rdx_execute_batch_device(*batch_args)
-        if st:
-            raise RuntimeError(f"rdx_execute_batch_device failed: {_abi.status_string(st)}")
-
-    def single_step(i):
-        st = lib.rdx_execute_device(*single_args[i % N_BUF])
-        if st:
-            raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
-
-    def timed(step, n):
-        """n back-to-back launches on one stream, bracketed by barrier + synchronize; HIP events on the
-        launch stream around the same region give the average launch duration (gaps included)."""
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for i in range(n):
-            step(i)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        barrier()
-        return max_over_ranks(t1 - t0), ev0.elapsed_time(ev1) / 1e3 / n
-
-    for i in range(max(args.warmup, 1)):   # (at least one launch, so the check below has results)
-        batch_step(i)
-    check_results()                       # what we time is correct: every chunk vs an f64 sum
-    elapsed, kern_avg_s = timed(batch_step, args.steps)
-    check_results()
-    step_bytes = N_BUF * C2_BYTES
-    value = args.steps * step_bytes * world / elapsed / GIB
-    achieved = step_bytes / kern_avg_s / 1e9
-
-    extra = {}
+    c2 = leg_c2(cx)
+    extra = c2["extra"]
     if args.primary_only:
-        args.no_c4 = args.no_cpu_baseline = args.no_inflate = args.no_f64 = True
-    else:
-        for i in range(max(args.warmup, N_BUF)):   # every chunk at least once, whatever --warmup is
-            single_step(i)
-        check_results()
-        el1, k1 = timed(single_step, args.steps)
-        extra["c2_single_chunk"] = {
-        "workload": "the same 64 MiB chunks, one chunk per launch (rdx_execute_device)",
-        "value": round(args.steps * C2_BYTES * world / el1 / GIB, 2), "unit": "GiB/s",
-        "ms_per_step": round(el1 / args.steps * 1e3, 5), "kernel_us_avg": round(k1 * 1e6, 3),
-        "roofline_frac": round(C2_BYTES / k1 / 1e9 / PEAK_GBS, 4)}
-
-        # concurrent single-chunk requests, the way a server runs them (one request per worker thread,
-        # app.rs:123-153): one workspace + HIP stream per in-flight request, chunks round-robin, so one
-        # launch's ramp / hand-off tail overlaps the next launch's streaming
-        n_st = int(os.environ.get("RDX_BENCH_STREAMS", "4"))
-        sts = [torch.cuda.Stream() for _ in range(n_st)]
-        wss = [eng.workspace(device) for _ in range(n_st)]
-        conc_args = [(wss[i % n_st].ws,) + single_args[i][1:-2] + (C.c_void_p(sts[i % n_st].cuda_stream),
-                                                                   single_args[i][-1]) for i in range(N_BUF)]
-
-        def conc_step(i):
-            st = lib.rdx_execute_device(*conc_args[i % N_BUF])
-            if st:
-                raise RuntimeError(f"rdx_execute_device failed: {_abi.status_string(st)}")
-
-        for i in range(max(args.warmup, N_BUF)):
-            conc_step(i)
-        check_results()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            conc_step(i)
-        torch.cuda.synchronize()
-        elc = max_over_ranks(time.perf_counter() - t0)
-        barrier()
-        check_results()
-        extra["c2_concurrent_requests"] = {
-            "workload": f"the same 64 MiB chunks, one chunk per rdx_execute_device call, {n_st} streams / "
-                        "workspaces round-robin (concurrent requests)",
-            "value": round(args.steps * C2_BYTES * world / elc / GIB, 2), "unit": "GiB/s",
-            "us_per_request": round(elc / args.steps * 1e6, 3),
-            "roofline_frac": round(args.steps * C2_BYTES / elc / 1e9 / PEAK_GBS, 4),
-            "timing": "host wall clock around the K calls, synchronize on both sides"}
-        for w in wss:
-            w.close()
-
-    # ---- C4 (extra): 1024 x 4 MiB chunks, one batched launch per step ----------------------------------
+        args.no_c4 = args.no_cpu_baseline = args.no_inflate = args.no_f64 = args.no_configs = args.no_host = True
+    solo = rank == 0 and world == 1
     if not args.no_c4:
-        lo4, hi4 = shard_range(C4_CHUNKS, rank, world)
-        n_local = hi4 - lo4
-        g.manual_seed(0x5EED1000 + lo4)
-        v4 = torch.rand(n_local, C4_ELEMS, device="cuda", generator=g, dtype=torch.float32)
-        ex4 = v4.double().sum(dim=1).cpu()
-        # native byte order, shuffle es=4
-        c4 = v4.view(torch.uint8).reshape(n_local, C4_ELEMS, 4).transpose(1, 2).contiguous().reshape(n_local, -1)
-        del v4
-        b4 = torch.zeros(n_local, dtype=torch.float32, device="cuda")
-        n4 = torch.zeros(n_local, dtype=torch.int64, device="cuda")
-        s4 = torch.zeros(n_local, dtype=torch.int32, device="cuda")
-        creq4 = _abi.CRequest("sum", "float32", filters=[{"id": "shuffle", "element_size": 4}])
-        ptrs = [c4[i].data_ptr() for i in range(n_local)]
-        for _ in range(2):
-            ws.execute_batch_device(creq4, ptrs, 4 * C4_ELEMS, b4.data_ptr(), n4.data_ptr(), s4.data_ptr(),
-                                    stream.cuda_stream)
-        torch.cuda.synchronize()
-        assert bool((n4.cpu() == C4_ELEMS).all()) and int(s4.abs().sum()) == 0
-        assert bool(((b4.double().cpu() - ex4).abs() <= ex4.abs() * 2.0 ** -23 + 1e-3).all())
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        e0.record(stream)
-        for _ in range(args.c4_steps):
-            ws.execute_batch_device(creq4, ptrs, 4 * C4_ELEMS, b4.data_ptr(), n4.data_ptr(), s4.data_ptr(),
-                                    stream.cuda_stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        barrier()
-        el4 = max_over_ranks(t1 - t0)
-        k4 = e0.elapsed_time(e1) / 1e3 / args.c4_steps
-        extra["c4_batch"] = {
-            "workload": "1024 x 4 MiB f32 chunks, shuffle es=4, native order, sum; batch split over ranks",
-            "value": round(args.c4_steps * C4_CHUNKS * 4 * C4_ELEMS / el4 / GIB, 2), "unit": "GiB/s",
-            "scaling": "strong", "steps": args.c4_steps, "ms_per_step": round(el4 / args.c4_steps * 1e3, 4),
-            "chunks_per_rank": n_local,
-            "roofline_frac": round(n_local * 4 * C4_ELEMS / k4 / 1e9 / PEAK_GBS, 4)}
-        del c4
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            extra["c4_batch"]["cpu_baseline"] = cpu_baseline_c4(max(1, min(15, (os.cpu_count() or 2) - 1)))
-
-    # ---- f64 chunks (extra): north_star's "4 MiB and 64 MiB f32/f64 chunks", f64 legs --------------------
+        extra["c4_batch"] = leg_c4(cx)
+        if solo and not args.no_cpu_baseline:
+            extra["c4_batch"]["cpu_baseline"] = cpu_baseline_c4(pool_threads())
     if not args.no_f64:
-        extra["f64_64mib"] = f64_batch(torch, ws, stream, g, rank, barrier, max_over_ranks, world,
-                                       elems=8 * 1024 * 1024, n_chunks=N_BUF, steps=max(10, args.steps // 4))
-        extra["f64_4mib"] = f64_batch(torch, ws, stream, g, rank, barrier, max_over_ranks, world,
-                                      elems=512 * 1024, n_chunks=128, steps=max(10, args.steps // 4))
-
-    # ---- decompression (extra): the filter pipeline's first stage on the device (DESIGN.md §9) ------------
+        steps = max(10, args.steps // 4)
+        extra["f64_64mib"] = leg_f64(cx, 8 * 1024 * 1024, N_BUF, steps)
+        extra["f64_4mib"] = leg_f64(cx, 512 * 1024, 128, steps)
     if not args.no_inflate:
-        extra["c4z_inflate"] = inflate_batch(torch, ws, stream, rank, world, not args.no_cpu_baseline and rank == 0
-                                             and world == 1)
+        extra["c4z_inflate"] = leg_inflate(cx, solo and not args.no_cpu_baseline)
+    if world == 1 and not args.no_configs:
+        extra["configs"] = leg_configs(cx)
+        if hasattr(cx.ws, "execute_multi_device"):
+            from reductionist_amd import mixed
+            extra["mixed_requests"] = mixed.bench_leg(cx)
+    if world == 1 and not args.no_host:
+        extra["host_inclusive"] = leg_host(cx)
+    cpu_line = None
+    if solo and not args.no_cpu_baseline:
+        cpu_line, extra["cpu_baselines"] = leg_cpu(cx, args.cpu_seconds)
 
+    achieved = c2["step_bytes"] / c2["kern_avg_s"] / 1e9
     line = {
         "metric": "GiB/s device-resident chunk unshuffle+reduce (f32 sum), 1/2/4/8 MI355X",
-        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic U[0,1) f32, big-endian, byte-shuffled (es=4)",
+        "value": round(c2["value"], 2), "unit": "GiB/s", "n_gpus": n_gpus, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(c2["elapsed"] / args.steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic U[0,1) f32, big-endian, byte-shuffled (es=4)",
         "config": {"workload": "c2: f32 sum over 64 MiB chunks (16 Mi elements each), byte shuffle es=4 + "
                                "non-native (big) byte order; one step = one launch over 8 independent "
                                "HBM-resident chunks (512 MiB) per GPU, one result per chunk",
                    "chunk_bytes": C2_BYTES, "chunks_per_step": N_BUF, "elements_per_chunk": C2_ELEMS,
-                   "parallelism": f"independent chunks x{world} GPUs"},
+                   "parallelism": f"independent chunks x{n_gpus} GPUs", "ranks": world, "devices": devs},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_GBS, 4), "traffic": traffic_from_profiles("c2"),
                      "kernel": "k_all_contig<float, OP_SUM, FUSED=1, MK=0>",
-                     "kernel_us_avg": round(kern_avg_s * 1e6, 3), "bytes_alg_per_launch": step_bytes,
+                     "kernel_us_avg": round(c2["kern_avg_s"] * 1e6, 3), "bytes_alg_per_launch": c2["step_bytes"],
                      "timing": "HIP events on the launch stream around the K back-to-back launches / K"},
         "extra": extra,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        line["cpu_baseline"]["nproc"] = os.cpu_count()
+    if oversub and n_gpus != world:
+        line["oversubscribed"] = True
+    if cpu_line:
+        line["cpu_baseline"] = cpu_line
     if rank == 0:
         print(json.dumps(line), flush=True)
-    ws.close()
-    eng.close()
+    cx.ws.close()
+    cx.eng.close()
     if world > 1:
         dist.destroy_process_group()
 

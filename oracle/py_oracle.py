@@ -29,6 +29,8 @@ def lib():
         VP, U64 = C.c_void_p, C.c_uint64
         L.oracle_execute.restype = C.c_int
         L.oracle_execute.argtypes = [VP, VP, U64, VP, U64, C.POINTER(C.c_int64), U64, VP]
+        L.oracle_bench.restype = C.c_int
+        L.oracle_bench.argtypes = [VP, VP, U64, U64, C.c_int, C.POINTER(C.c_uint64)]
         L.oracle_validate_request.restype = C.c_int
         L.oracle_validate_request.argtypes = [VP]
         L.oracle_shuffle.restype = None
@@ -61,6 +63,16 @@ def execute(creq, data: bytes, body_cap: int | None = None, counts_cap: int | No
     src = C.create_string_buffer(bytes(data), max(1, n))
     st = L.oracle_execute(C.addressof(creq.c), src, n, body, body_cap, counts, counts_cap, C.byref(info))
     return st, info, bytes(body)[: info.body_bytes], [int(c) for c in counts[: info.n_counts]]
+
+
+def bench(creq, data: bytes, reps: int, clone: bool) -> float:
+    """Seconds per execution of the reference path over one chunk on this thread (oracle_bench)."""
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    ns = C.c_uint64(0)
+    st = lib().oracle_bench(C.addressof(creq.c), src, len(data), reps, 1 if clone else 0, C.byref(ns))
+    if st:
+        raise RuntimeError(f"oracle_bench failed: status {st}")
+    return ns.value / 1e9 / max(1, reps)
 
 
 def validate(creq) -> int:

@@ -28,6 +28,7 @@
 #include "../include/rdx.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -582,6 +583,8 @@ void validate_raw_size(u64 raw_size, uint32_t dtype, const rdx_request &req) {
 thread_local uint32_t g_inflate_error = 0;
 
 // src/app.rs:163-183 operation<T>
+Response execute_dtype(const rdx_request &req, std::vector<uint8_t> &data);
+
 Response operation(const rdx_request &req, const uint8_t *chunk, u64 len) {
     std::vector<uint8_t> data;
     // filter_pipeline.rs:19-34: decompress (compression.rs:18-27, oracle_inflate.cpp), then the
@@ -611,6 +614,11 @@ Response operation(const rdx_request &req, const uint8_t *chunk, u64 len) {
     for (uint32_t k = req.n_filters; k-- > 0;) data = deshuffle(data, req.filters[k].element_size);
     // app.rs:169-172: the raw size is validated when compressed or when `size` was not given
     if (req.compression != RDX_COMPRESSION_NONE || !req.has_size) validate_raw_size(data.size(), req.dtype, req);
+    return execute_dtype(req, data);
+}
+
+// operation.rs:78-96: runtime dtype -> NumOperation::execute_t::<T> (data owned, may be mutated)
+Response execute_dtype(const rdx_request &req, std::vector<uint8_t> &data) {
     switch (req.dtype) {
         case RDX_DTYPE_INT32: return execute_t<int32_t>(req, data);
         case RDX_DTYPE_INT64: return execute_t<int64_t>(req, data);
@@ -696,6 +704,34 @@ int oracle_execute(const rdx_request *req, const void *chunk, uint64_t len, void
         if (r.body.size() > body_cap || r.count.size() > counts_cap) return RDX_E_BUFFER_TOO_SMALL;
         if (!r.body.empty()) std::memcpy(body, r.body.data(), r.body.size());
         if (!r.count.empty()) std::memcpy(counts, r.count.data(), r.count.size() * sizeof(int64_t));
+        return RDX_OK;
+    } catch (const OracleError &e) {
+        return e.status;
+    } catch (...) {
+        return RDX_E_OUT_OF_MEMORY;
+    }
+}
+
+// Timing helper for bench.py's cpu_baseline legs: `reps` executions of one request over one chunk on
+// the calling thread; *ns = elapsed wall nanoseconds.  clone = 1 copies the chunk into a fresh buffer
+// every iteration, as the reference's criterion bench does (`data.clone()` inside the timed closure,
+// benches/operations.rs:63); clone = 0 runs Operation::execute on one buffer prepared outside the loop
+// (only for requests that do not mutate it: no filter, no compression, native byte order).
+int oracle_bench(const rdx_request *req, const void *chunk, uint64_t len, uint64_t reps, int clone, uint64_t *ns) {
+    try {
+        if (!req || (!chunk && len) || !ns) return RDX_E_INVALID_ARGUMENT;
+        if (!clone && (req->n_filters || req->compression != RDX_COMPRESSION_NONE ||
+                       req->byte_order == RDX_BYTE_ORDER_BIG))
+            return RDX_E_INVALID_ARGUMENT;
+        const uint8_t *src = static_cast<const uint8_t *>(chunk);
+        std::vector<uint8_t> once(src, src + len);
+        volatile u64 sink = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t i = 0; i < reps; ++i) {
+            Response r = clone ? operation(*req, src, len) : execute_dtype(*req, once);
+            sink = sink + r.body.size();
+        }
+        *ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         return RDX_OK;
     } catch (const OracleError &e) {
         return e.status;

@@ -152,11 +152,10 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
             continue;
         }
         // sliced (group == 64, one item per wave): publish, and the last slice to arrive folds them
-        constexpr int kW = packed_words<T, OP>();
+        constexpr int kR = granules<T, OP>();
         uint32_t last = 0;
         if (lane == 0) {
-            store_packed<T, OP, true>(a.out.partials + it * kW, r);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            publish<T, OP>(a.out.partials + it * kR, r, a.out.epoch);
             uint32_t *tk = a.out.tickets + o * kTicketStride;   // one L2 line per counter: same-line atomics serialise
             last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
             if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -164,11 +163,14 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
         if (!__shfl(last, 0, 64)) continue;
         Red<T, OP> acc;
         acc.init();
+        uint32_t fault = 0;
         for (uint32_t q = lane; q < a.slices; q += 64) {
             Red<T, OP> p;
-            load_packed<T, OP, true>(a.out.partials + (o * a.slices + q) * kW, p);
+            collect<T, OP>(a.out.partials + (o * a.slices + q) * kR, p, a.out.epoch, fault);
             acc.merge(p);
         }
+        if (__builtin_amdgcn_ballot_w64(fault) && lane == 0 && a.out.status)
+            __hip_atomic_fetch_or(a.out.status, (uint32_t)RDX_E_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wave_reduce(acc);
         if (lane == 0) write_result(a.out, (uint64_t)oi, acc);
     }
@@ -187,7 +189,7 @@ __device__ __forceinline__ void cols_combine(Red<T, OP> (&r)[VW], uint64_t *lds,
     }
     if (wave > 0 && lane < W) {
 #pragma unroll
-        for (int j = 0; j < VW; ++j) store_packed<T, OP, false>(lds + (((wave - 1) * 64 + lane) * VW + j) * kW, r[j]);
+        for (int j = 0; j < VW; ++j) store_packed<T, OP>(lds + (((wave - 1) * 64 + lane) * VW + j) * kW, r[j]);
     }
     __syncthreads();
     if (wave == 0 && lane < W) {
@@ -195,7 +197,7 @@ __device__ __forceinline__ void cols_combine(Red<T, OP> (&r)[VW], uint64_t *lds,
         for (int j = 0; j < VW; ++j) {
             for (int w = 0; w < kWaves - 1; ++w) {
                 Red<T, OP> o;
-                load_packed<T, OP, false>(lds + ((w * 64 + lane) * VW + j) * kW, o);
+                load_packed<T, OP>(lds + ((w * 64 + lane) * VW + j) * kW, o);
                 r[j].merge(o);
             }
         }
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     constexpr int kWaves = kBlock / 64;
     constexpr int kW = packed_words<T, OP>();
     __shared__ uint64_t lds[(kWaves - 1) * 64 * VW * kW];
-    __shared__ uint32_t s_last;
+    __shared__ uint32_t s_last, s_fault;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t W = a.group, R = 64 / W;              // lanes per row of the tile, rows per wave access
     const uint32_t c = lane & (W - 1), rsub = lane / W;
@@ -250,7 +252,9 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
         }
     }
     cols_combine<T, OP, VW>(r, lds, W);
+#if RDX_PROBES
     if (a.probe == 2) return;
+#endif
     if (a.slices == 1) {
         if (wave == 0 && lane < W && active) {
 #pragma unroll
@@ -265,34 +269,38 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     // 19.3 us).  Fold launch: record-major ([slice][c][j][word]) — k_axis_cols_fold reads a lane's
     // slice records one after another, one line per record.
     const uint64_t tile_rec = (uint64_t)W * VW;
-    const uint64_t wstride = (uint64_t)a.slices * tile_rec;     // words of one kind per tile
-    uint64_t *P = a.out.partials + (uint64_t)blockIdx.x * wstride * kW;
+    const uint64_t wstride = (uint64_t)a.slices * tile_rec;     // granules of one kind per tile
     if (a.fold_sep) {   // k_axis_cols_fold reads the records after this launch: plain stores
+        uint64_t *P = a.out.partials + (uint64_t)blockIdx.x * wstride * kW;
         if (wave == 0 && lane < W) {
 #pragma unroll
-            for (int j = 0; j < VW; ++j) store_packed<T, OP, false>(P + ((uint64_t)s * tile_rec + c * VW + j) * kW, r[j]);
+            for (int j = 0; j < VW; ++j) store_packed<T, OP>(P + ((uint64_t)s * tile_rec + c * VW + j) * kW, r[j]);
         }
         return;
     }
-    if (wave == 0) {
-        if (lane < W) {
+    uint64_t *P = a.out.partials + (uint64_t)blockIdx.x * wstride * granules<T, OP>();
+    if (wave == 0 && lane < W) {
 #pragma unroll
-            for (int j = 0; j < VW; ++j) store_packed<T, OP, true>(P + (uint64_t)s * tile_rec + c * VW + j, r[j], wstride);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-            uint32_t *tk = a.out.tickets + blockIdx.x * kTicketStride;
-            const bool last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
-            if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = last;
-        }
+        for (int j = 0; j < VW; ++j) publish<T, OP>(P + (uint64_t)s * tile_rec + c * VW + j, r[j], a.out.epoch, wstride);
+    }
+    __syncthreads();   // every record of this slice issued before thread 0 counts the arrival
+    if (threadIdx.x == 0) {
+        uint32_t *tk = a.out.tickets + blockIdx.x * kTicketStride;
+        const bool last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.slices - 1;
+        if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
+        s_fault = 0;
     }
     __syncthreads();
-    if (!s_last || a.probe == 1) return;
+    if (!s_last) return;
+#if RDX_PROBES
+    if (a.probe == 1) return;
+#endif
     const uint32_t G = kBlock / W, grp = threadIdx.x / W;    // parallel slice streams
     const uint32_t q_lo = (uint32_t)((uint64_t)grp * a.slices / G), q_hi = (uint32_t)((uint64_t)(grp + 1) * a.slices / G);
 #pragma unroll
     for (int j = 0; j < VW; ++j) r[j].init();
+    uint32_t fault = 0;
     if (active) {
         constexpr int kQ = 4;  // slices' records in flight per lane
         for (uint32_t q0 = q_lo; q0 < q_hi; q0 += kQ) {
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             for (int u = 0; u < kQ; ++u) {
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
-                    if (q0 + u < q_hi) load_packed<T, OP, true>(P + (uint64_t)(q0 + u) * tile_rec + c * VW + j, p[u][j], wstride);
+                    if (q0 + u < q_hi) collect<T, OP>(P + (uint64_t)(q0 + u) * tile_rec + c * VW + j, p[u][j], a.out.epoch, fault, wstride);
                     else p[u][j].init();
                 }
             }
@@ -312,11 +320,14 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             }
         }
     }
+    if (fault) s_fault = 1;
     cols_combine<T, OP, VW>(r, lds, W);
     if (wave == 0 && lane < W && active) {
 #pragma unroll
         for (int j = 0; j < VW; ++j) write_result(a.out, (uint64_t)(oi + (int64_t)j * a.kept.rstride[0]), r[j]);
     }
+    if (threadIdx.x == 0 && s_fault && a.out.status)
+        __hip_atomic_fetch_or(a.out.status, (uint32_t)RDX_E_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The fold of sliced column reductions as its own launch (fold_sep), parallel across outputs instead of
@@ -345,7 +356,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols_fold(const KAxis a) {
         Red<T, OP> p[4];
 #pragma unroll
         for (uint32_t u = 0; u < 4; ++u) {
-            if (s0 + u < s_hi) load_packed<T, OP, false>(P + (uint64_t)(s0 + u) * tile_rec * kW, p[u]);
+            if (s0 + u < s_hi) load_packed<T, OP>(P + (uint64_t)(s0 + u) * tile_rec * kW, p[u]);
             else p[u].init();
         }
 #pragma unroll
@@ -375,7 +386,7 @@ void launch_axis_k(const KAxis &a, int cus, hipStream_t st) {
         const dim3 grid((uint32_t)((a.n_out / VW + a.group - 1) / a.group), a.slices);
         if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1, GEN, MK>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((k_axis_cols<T, OP, false, VW, GEN, MK>), grid, block, 0, st, a);
-        if (a.slices > 1 && a.fold_sep && a.probe == 0) {
+        if (a.slices > 1 && a.fold_sep && a.probe == 0) {   // (probe is 0 unless built with RDX_PROBES)
             const uint64_t cols = (uint64_t)grid.x * a.group * (a.src.fused ? 1 : VW);   // record columns
             const bool wg = cols * 4 <= (uint64_t)cus * 4 && a.slices >= 256;   // few outputs, long folds
             const dim3 fgrid((uint32_t)(wg ? cols : (cols + kBlock / 64 - 1) / (kBlock / 64)));

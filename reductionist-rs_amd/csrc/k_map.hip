@@ -117,7 +117,8 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
         }
     }
     if constexpr (KIND == 0) {
-        if constexpr (MK != MK_NONE) finalize_count(cnt, a.out.counts, a.out.partials, a.out.tickets, gridDim.x, blockIdx.x);
+        if constexpr (MK != MK_NONE) finalize_count(cnt, a.out.counts, a.out.status, a.out.partials, a.out.tickets, a.out.epoch,
+                                                 gridDim.x, blockIdx.x);
         else if (blockIdx.x == 0 && threadIdx.x == 0) a.out.counts[0] = (int64_t)v.n;  // sliced.len()
     }
 }

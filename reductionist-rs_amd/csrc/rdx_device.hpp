@@ -395,11 +395,152 @@ __device__ __forceinline__ constexpr int packed_words() {
     return n;
 }
 
-// AGENT = agent-scope (sc1) accesses for the cross-workgroup hand-off.
-// Word k of the record at P[k * stride]: stride 1 = one record per kW consecutive words; a record
-// array laid out word-major (stride = record count) makes a wave's per-lane stores / loads of one
-// word coalesced.
-template <typename T, int OP, bool AGENT>
+// ---- cross-workgroup hand-off records ----------------------------------------------------------------
+// A partial record published to another workgroup of the same launch travels as tagged granules: 8-byte
+// words {48-bit payload, 16-bit launch epoch}, each written by ONE relaxed agent-scope atomic store
+// (global_store sc1, write-through) and read back by relaxed agent-scope atomic loads (sc1:
+// device-coherent, never served from a stale L1 copy) that retry until the granule carries this
+// launch's epoch.  Every access to a record is atomic (no data race) and a reader accepts exactly the
+// value this launch's producer stored (single-copy atomicity of an aligned 8-byte atomic), so the HIP
+// memory model needs no release/acquire pair for the record bytes: the arrival counters (relaxed RMWs,
+// totally ordered per location) only elect the workgroup that folds.  Measured against the fence form
+// (release before the counter add, acquire in the last arriver; profiles/r02_handoff_ab.jsonl): the
+// fences cost +1.5 us per 64 MiB single-chunk launch, +3 us per batched launch and +29 us on the
+// sliced axis kernels (every slice's buffer_wbl2).  Epochs come from the workspace (rdx_runtime.cpp
+// next_epoch): never 0, and the record buffer is cleared whenever the 16-bit epoch wraps, so a stale
+// granule can never carry the current tag.  A reader that sees no fresh granule within kSpinLimit polls
+// (a producer that never published: impossible short of a device fault) gives up and reports
+// RDX_E_DEVICE instead of hanging the GPU.
+//
+// Record fields -> granules: a 64-bit value / sum / compensation as two 32-bit halves; a 32-bit min/max
+// value as one; the count (< 2^47) with the NaN flag in bit 47 as one; each ±0 fold-order rank (48-bit
+// two's complement, INT64_MAX as 0x7fff_ffff_ffff) as one.  f32 sum: 3 granules, f32 min/max: 4, f64
+// min/max and sum: 5, integer sum: 3, count: 1.
+constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr uint64_t kPayload = (1ull << 48) - 1;
+constexpr int kMaxGranules = 6;
+
+__device__ __forceinline__ void put_granule(uint64_t *g, uint64_t payload, uint32_t tag) {
+    __hip_atomic_store(g, (payload & kPayload) | ((uint64_t)tag << 48), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Cold path: poll one granule until it carries `tag`; after kSpinLimit polls it returns the stale value
+// and the caller reports a fault.
+__device__ __attribute__((noinline)) uint64_t poll_granule(const uint64_t *g, uint32_t tag) {
+    uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = 0; (uint32_t)(v >> 48) != tag && i < kSpinLimit; ++i) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return v;
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ constexpr int granules() {
+    constexpr bool kRank = Red<T, OP>::kRank;
+    int n = 0;
+    if (OP != OP_COUNT) n += (OP == OP_SUM || sizeof(T) == 8) ? 2 : 1;   // value / sum
+    if (OP == OP_SUM && std::is_same_v<T, double>) n += 2;                // compensation
+    n += 1;                                                               // count (+ NaN flag)
+    if (kRank) n += 2;                                                    // ±0 ranks
+    return n;
+}
+
+__device__ __forceinline__ uint64_t rank48(int64_t r) {
+    return r == INT64_MAX ? 0x7fffffffffffull : (uint64_t)r & kPayload;
+}
+__device__ __forceinline__ int64_t unrank48(uint64_t p) {
+    p &= kPayload;
+    if (p == 0x7fffffffffffull) return INT64_MAX;
+    return (int64_t)(p << 16) >> 16;
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void encode(const Red<T, OP> &r, uint64_t (&g)[kMaxGranules]) {
+    uint64_t w[kPartialWords];
+    r.to_words(w);
+    int k = 0;
+    if constexpr (OP != OP_COUNT) {
+        if constexpr (OP == OP_SUM || sizeof(T) == 8) {
+            g[k++] = w[0] & 0xffffffffull;
+            g[k++] = w[0] >> 32;
+        } else {
+            g[k++] = w[0] & 0xffffffffull;
+        }
+    }
+    if constexpr (OP == OP_SUM && std::is_same_v<T, double>) {
+        g[k++] = w[1] & 0xffffffffull;
+        g[k++] = w[1] >> 32;
+    }
+    g[k++] = (w[2] & ((1ull << 47) - 1)) | (Red<T, OP>::kRank && w[5] ? (1ull << 47) : 0ull);
+    if constexpr (Red<T, OP>::kRank) {
+        g[k++] = rank48((int64_t)w[3]);
+        g[k++] = rank48((int64_t)w[4]);
+    }
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void decode(const uint64_t (&g)[kMaxGranules], Red<T, OP> &r) {
+    Red<T, OP> id;
+    id.init();
+    uint64_t w[kPartialWords];
+    id.to_words(w);
+    int k = 0;
+    if constexpr (OP != OP_COUNT) {
+        if constexpr (OP == OP_SUM || sizeof(T) == 8) {
+            w[0] = (g[k] & 0xffffffffull) | ((g[k + 1] & 0xffffffffull) << 32);
+            k += 2;
+        } else {
+            w[0] = g[k++] & 0xffffffffull;
+        }
+    }
+    if constexpr (OP == OP_SUM && std::is_same_v<T, double>) {
+        w[1] = (g[k] & 0xffffffffull) | ((g[k + 1] & 0xffffffffull) << 32);
+        k += 2;
+    }
+    w[2] = g[k] & ((1ull << 47) - 1);
+    if constexpr (Red<T, OP>::kRank) {
+        w[5] = (g[k] >> 47) & 1;
+        w[3] = (uint64_t)unrank48(g[k + 1]);
+        w[4] = (uint64_t)unrank48(g[k + 2]);
+    }
+    r.from_words(w);
+}
+
+// Granule j of a record at P[j * stride] (stride 1 = record-major; a word-major record array, stride =
+// record count, makes a wave's per-lane stores / loads of one granule coalesced).
+template <typename T, int OP>
+__device__ __forceinline__ void publish(uint64_t *P, const Red<T, OP> &r, uint32_t tag, uint64_t stride = 1) {
+    uint64_t g[kMaxGranules];
+    encode(r, g);
+#pragma unroll
+    for (int j = 0; j < granules<T, OP>(); ++j) put_granule(P + j * stride, g[j], tag);
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void collect(const uint64_t *P, Red<T, OP> &r, uint32_t tag, uint32_t &fault,
+                                        uint64_t stride = 1) {
+    constexpr int kG = granules<T, OP>();
+    uint64_t g[kMaxGranules] = {};
+#pragma unroll
+    for (int j = 0; j < kG; ++j) g[j] = __hip_atomic_load(P + j * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool fresh = true;
+#pragma unroll
+    for (int j = 0; j < kG; ++j) fresh &= (uint32_t)(g[j] >> 48) == tag;
+    if (__builtin_expect(!fresh, 0)) {
+#pragma unroll
+        for (int j = 0; j < kG; ++j)
+            if ((uint32_t)(g[j] >> 48) != tag) {
+                g[j] = poll_granule(P + j * stride, tag);
+                fault |= (uint32_t)(g[j] >> 48) != tag;
+            }
+    }
+    decode(g, r);
+}
+
+// Plain (untagged) packed records: within a workgroup (LDS) or read by a LATER launch (the kernel
+// boundary orders them).  Word k of the record at P[k * stride].
+template <typename T, int OP>
 __device__ __forceinline__ void store_packed(uint64_t *P, const Red<T, OP> &r, uint64_t stride = 1) {
     uint64_t w[kPartialWords];
     r.to_words(w);
@@ -407,13 +548,12 @@ __device__ __forceinline__ void store_packed(uint64_t *P, const Red<T, OP> &r, u
 #pragma unroll
     for (int i = 0; i < kPartialWords; ++i) {
         if (!word_used<T, OP>(i)) continue;
-        if constexpr (AGENT) __hip_atomic_store(P + k * stride, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else P[k * stride] = w[i];
+        P[k * stride] = w[i];
         ++k;
     }
 }
 
-template <typename T, int OP, bool AGENT>
+template <typename T, int OP>
 __device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r, uint64_t stride = 1) {
     Red<T, OP> id;
     id.init();
@@ -423,8 +563,7 @@ __device__ __forceinline__ void load_packed(const uint64_t *P, Red<T, OP> &r, ui
 #pragma unroll
     for (int i = 0; i < kPartialWords; ++i) {
         if (!word_used<T, OP>(i)) continue;
-        if constexpr (AGENT) w[i] = __hip_atomic_load(P + k * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else w[i] = P[k * stride];
+        w[i] = P[k * stride];
         ++k;
     }
     r.from_words(w);
@@ -478,45 +617,44 @@ __device__ __forceinline__ void block_reduce(Red<T, OP> &r) {
 }
 
 // Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
-// partials in workgroup order and write the response (one launch, no second kernel).
-// Hand-off form (MI355X_MICROARCH.md "Valid forms", row 1): one lane stores the partial with
-// agent-scope (sc1) stores, drains them (s_waitcnt vmcnt(0)), then adds to an arrival counter;
-// the workgroup whose add completes the count reads every partial with sc1 loads after a barrier.
-// The counter is sharded 8 ways by workgroup index (b % 8 groups share an XCD under round-robin
-// dispatch) so that arrivals do not serialise on one word (~11 ns per atomic, "fanin" row); the
-// last arrival of each shard adds to the top counter.  All counters self-reset for the next launch.
+// partials in workgroup order and write the response (one launch, no second kernel).  One lane
+// publishes the record (tagged granules, above), then adds to an arrival counter; the workgroup whose
+// add completes the count collects every record.  The counter is sharded 8 ways by workgroup index
+// (b % 8 groups share an XCD under round-robin dispatch) so that arrivals do not serialise on one word
+// (~11 ns per atomic, MI355X_MICROARCH.md "fanin" row); the last arrival of each shard adds to the top
+// counter.  All counters self-reset for the next launch.
+__device__ __forceinline__ bool arrive_last(uint32_t *tk, uint32_t n, uint32_t b) {
+    const uint32_t nsh = n < kTicketShards ? n : kTicketShards;
+    const uint32_t sh = b % kTicketShards;
+    const uint32_t members = (n - sh + kTicketShards - 1) / kTicketShards;
+    const uint32_t p1 = __hip_atomic_fetch_add(tk + (1 + sh) * kTicketStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p1 != members - 1) return false;
+    __hip_atomic_store(tk + (1 + sh) * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+}
+
 template <typename T, int OP>
 __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
-    __shared__ uint32_t s_last;
+    __shared__ uint32_t s_last, s_fault;
+    constexpr int kR = granules<T, OP>();   // u64 granules per record
     block_reduce(r);
     if (threadIdx.x == 0) {
-        constexpr int kW = packed_words<T, OP>();
-        store_packed<T, OP, true>(out.partials + ((uint64_t)chunk * bpc + b) * kW, r);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t *tk = out.tickets + (uint64_t)chunk * kTicketWords;
-        const uint32_t nsh = bpc < kTicketShards ? bpc : kTicketShards;
-        const uint32_t sh = b % kTicketShards;
-        const uint32_t members = (bpc - sh + kTicketShards - 1) / kTicketShards;
-        bool last = false;
-        const uint32_t p1 = __hip_atomic_fetch_add(tk + (1 + sh) * kTicketStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (p1 == members - 1) {
-            __hip_atomic_store(tk + (1 + sh) * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t p2 = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = p2 == nsh - 1;
-        }
-        s_last = last;
+        publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
+        s_last = arrive_last(out.tickets + (uint64_t)chunk * kTicketWords, bpc, b);
+        s_fault = 0;
     }
     __syncthreads();
     if (!s_last) return;
     Red<T, OP> acc;
     acc.init();
-    constexpr int kW = packed_words<T, OP>();
-    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kW;
+    uint32_t fault = 0;
+    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kR;
     for (uint32_t j = threadIdx.x; j < bpc; j += kBlock) {
         Red<T, OP> o;
-        load_packed<T, OP, true>(P + (uint64_t)j * kW, o);
+        collect<T, OP>(P + (uint64_t)j * kR, o, out.epoch, fault);
         acc.merge(o);
     }
+    if (fault) s_fault = 1;   // benign race: every writer stores 1
     block_reduce(acc);
     if (threadIdx.x == 0) {
         if constexpr (OP == OP_COUNT) {
@@ -526,7 +664,8 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
         }
         out.counts[chunk * out.counts_stride] = acc.cnt;
         if (out.status) {
-            const uint32_t e = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
+            uint32_t e = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
+            if (s_fault) e = RDX_E_DEVICE;
             if (!out.status_any) out.status[chunk] = e;
             else if (e) __hip_atomic_fetch_or(out.status, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else if (!Red<T, OP>::kRank && chunk == 0) out.status[0] = 0;   // nothing can fail
@@ -535,13 +674,13 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
     }
 }
 
-// Integer count across workgroups without a hot atomic: every workgroup publishes its count, the
-// sharded arrival counters elect the last one, which sums the counts (order-free: integers) and
-// writes `*dst`.  Same hand-off form as finalize_all.
-__device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint64_t *partials, uint32_t *tickets,
-                                      uint32_t nblocks, uint32_t b) {
+// Integer count across workgroups without a hot atomic: every workgroup publishes its count (one
+// tagged record word), the sharded arrival counters elect the last one, which sums the counts
+// (order-free: integers) and writes `*dst`.  Same hand-off form as finalize_all.
+__device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint32_t *status, uint64_t *partials,
+                                      uint32_t *tickets, uint32_t epoch, uint32_t nblocks, uint32_t b) {
     __shared__ int64_t part[kBlock / 64];
-    __shared__ uint32_t s_last;
+    __shared__ uint32_t s_last, s_fault;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) cnt += (int64_t)shfl_xor_u64((uint64_t)cnt, m);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
@@ -549,24 +688,23 @@ __device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint64_t *parti
     if (threadIdx.x == 0) {
         int64_t t = 0;
         for (int k = 0; k < kBlock / 64; ++k) t += part[k];
-        __hip_atomic_store(partials + b, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t nsh = nblocks < kTicketShards ? nblocks : kTicketShards;
-        const uint32_t sh = b % kTicketShards;
-        const uint32_t members = (nblocks - sh + kTicketShards - 1) / kTicketShards;
-        bool last = false;
-        const uint32_t p1 = __hip_atomic_fetch_add(tickets + (1 + sh) * kTicketStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (p1 == members - 1) {
-            __hip_atomic_store(tickets + (1 + sh) * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
-        }
-        s_last = last;
+        put_granule(partials + b, (uint64_t)t, epoch);   // a count < 2^48
+        s_last = arrive_last(tickets, nblocks, b);
+        s_fault = 0;
     }
     __syncthreads();
     if (!s_last) return;
     int64_t t = 0;
-    for (uint32_t j = threadIdx.x; j < nblocks; j += kBlock)
-        t += (int64_t)__hip_atomic_load(partials + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t fault = 0;
+    for (uint32_t j = threadIdx.x; j < nblocks; j += kBlock) {
+        uint64_t v = __hip_atomic_load(partials + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_expect((uint32_t)(v >> 48) != epoch, 0)) {
+            v = poll_granule(partials + j, epoch);
+            fault |= (uint32_t)(v >> 48) != epoch;
+        }
+        t += (int64_t)(v & kPayload);
+    }
+    if (fault) s_fault = 1;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) t += (int64_t)shfl_xor_u64((uint64_t)t, m);
     __syncthreads();
@@ -576,6 +714,7 @@ __device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint64_t *parti
         int64_t tot = 0;
         for (int k = 0; k < kBlock / 64; ++k) tot += part[k];
         *dst = tot;
+        if (s_fault && status) *status = RDX_E_DEVICE;
         __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

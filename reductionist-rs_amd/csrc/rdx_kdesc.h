@@ -10,6 +10,7 @@ constexpr int kMaxKDims = 16;        // dims left after canonicalisation (unit d
 constexpr int kInlineMissing = 16;   // missing_values lists up to this length travel in the args
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kPartialWords = 6;     // u64 words per partial record
+constexpr int kRecordU64 = 2 * kPartialWords;  // u64 slots per hand-off record (each word = 2 tagged granules)
 constexpr uint32_t kTicketShards = 8; // arrival counter shards per chunk
 constexpr uint32_t kTicketStride = 64; // u32 words between counters: one 256 B line each
 constexpr uint32_t kTicketWords = (1 + kTicketShards) * kTicketStride;
@@ -55,7 +56,7 @@ struct KOut {
     uint32_t *tickets;        // [chunk][kTicketWords] arrival counters, self-resetting
     uint32_t status_any;      // 1: one status word for all chunks (chunks = outputs of an axis
                               // reduction), NaN ORed in; the caller clears it when a NaN can set it
-    uint32_t pad;
+    uint32_t epoch;           // this launch's hand-off tag (never 0): records carry it per granule
 };
 
 // Reduction over ALL axes of a view whose elements form one ascending contiguous run
@@ -116,6 +117,24 @@ struct KAxis {
     uint32_t probe;  // tuning probe only (RDX_AXIS_PROBE): 1 = skip the slice fold, 2 = stop after streaming
     uint32_t fold_sep;  // cols, slices > 1: 0 = the tile's last slice folds (arrival counters); 1 = every
                         // slice only publishes and k_axis_cols_fold folds (a wave per output) next
+};
+
+// One request of a heterogeneous batch (k_multi.hip): an all-axes reduction over its own view, with
+// its own dtype / op / source / missing / outputs; `a.out.partials` / `a.out.tickets` point at this
+// request's slice of the workspace's hand-off buffers.
+struct KMultiItem {
+    KAllStrided a;
+    uint32_t dtype;     // rdx_dtype
+    uint32_t op;        // OpCode (COUNT / MAX / MIN / SUM)
+    uint32_t block0;    // first grid block of this request
+    uint32_t pad;
+};
+
+struct KMulti {
+    const KMultiItem *items;   // device table, one per request
+    const uint32_t *blk2item;  // device, one entry per grid block
+    uint32_t n_items;
+    uint32_t pad;
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

@@ -51,7 +51,11 @@ struct Tuning {
     int axis_cols_vw = env_int("RDX_AXIS_COLS_VW", 0);                 // tuning only: force the cols lane width
     int axis_fold_kib = env_int("RDX_AXIS_FOLD_KIB", 64);              // cols fold bytes per tile (x2 with >= 8 streams)
     int axis_fold_sep = env_int("RDX_AXIS_FOLD_SEP", -1);              // cols fold launch: -1 auto, 0 off, 1 on
+#if RDX_PROBES
     int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
+#else
+    int axis_probe = 0;   // product builds: the phase probe is compiled out (make EXTRA=-DRDX_PROBES=1)
+#endif
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
 };
@@ -73,8 +77,9 @@ struct rdx_workspace {
     int device = 0;
     int cus = 256;
     hipStream_t own_stream = nullptr;  // host path
-    DevBuf<uint64_t> partials;
+    DevBuf<uint64_t> partials;   // hand-off records (tagged granules, rdx_device.hpp publish / collect)
     DevBuf<uint32_t> tickets;
+    uint32_t epoch = 0;           // tag of the last launch's records
     DevBuf<uint8_t> scratch[2];
     DevBuf<uint64_t> miss_list;
     DevBuf<const uint8_t *> ptrs;
@@ -168,6 +173,18 @@ uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
     return (uint32_t)bpc;
 }
 
+// The hand-off tag of the next launch on this workspace: never 0 (a cleared record buffer holds 0), and
+// when the 16-bit tag wraps the record buffer is cleared on the stream first, so no stale granule
+// can carry a current tag (rdx_device.hpp, tagged granules).
+rdx_status next_epoch(rdx_workspace *ws, hipStream_t s, uint32_t &epoch) {
+    if (++ws->epoch > 0xffffu) {   // 16-bit tags
+        if (ws->partials.p) RDX_HIP(hipMemsetAsync(ws->partials.p, 0, ws->partials.cap * sizeof(uint64_t), s));
+        ws->epoch = 1;
+    }
+    epoch = ws->epoch;
+    return RDX_OK;
+}
+
 // Lanes may move 16 bytes of a view at once when its innermost dim is a contiguous, aligned run.
 uint32_t vec_width(const KView &v, uint32_t esz, const uint8_t *base, const uint8_t *const *ptrs, uint64_t n_chunks,
                    bool fused) {
@@ -231,6 +248,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
         ksrc.base = nullptr;
     }
     KOut out{};
+    if ((st = next_epoch(ws, s, out.epoch))) return st;
     out.body = d_body;
     out.counts = d_counts;
     out.status = d_status;
@@ -242,7 +260,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             KAllContig a = p.all_contig;
             const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus);
-            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
+            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
             out.tickets = ws->tickets.p;
@@ -263,7 +281,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 const int force = tuning().force_bpc;
                 if (force > 0) a.blocks_per_chunk = (uint32_t)force;
             }
-            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kPartialWords, s))) return st;
+            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
             out.tickets = ws->tickets.p;
@@ -309,7 +327,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 if ((st = ensure(ws, ws->ptrs, a.n_out, s))) return st;
                 if ((st = upload(ws, (void *)ws->ptrs.p, rows.data(), a.n_out * sizeof(void *), ws->last_ptrs, s)))
                     return st;
-                if ((st = ensure(ws, ws->partials, a.n_out * c.blocks_per_chunk * kPartialWords, s))) return st;
+                if ((st = ensure(ws, ws->partials, a.n_out * c.blocks_per_chunk * kRecordU64, s, true))) return st;
                 if ((st = ensure(ws, ws->tickets, a.n_out * kTicketWords, s, true))) return st;
                 c.src = ksrc;
                 c.src.base = nullptr;
@@ -403,7 +421,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             if (slices > 1) {   // partial records + a self-resetting arrival counter (own L2 line) per output / tile
                 const uint64_t tiles = (a.n_out / a.vec + a.group - 1) / a.group;
                 const uint64_t recs = a.mode == 0 ? a.n_out : tiles * a.group * a.vec;
-                if ((st = ensure(ws, ws->partials, recs * slices * kPartialWords, s))) return st;
+                if ((st = ensure(ws, ws->partials, recs * slices * kRecordU64, s, true))) return st;
                 if ((st = ensure(ws, ws->tickets, std::max<uint64_t>((a.mode == 0 ? a.n_out : tiles) * kTicketStride, kTicketWords),
                                  s, true)))
                     return st;
@@ -426,7 +444,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 return RDX_OK;
             }
             if (a.kind == 0) {
-                if ((st = ensure(ws, ws->partials, (uint64_t)ws->cus * 8, s))) return st;
+                if ((st = ensure(ws, ws->partials, (uint64_t)ws->cus * 8 * 2, s, true))) return st;
                 if ((st = ensure(ws, ws->tickets, kTicketWords, s, true))) return st;
                 out.partials = ws->partials.p;
                 out.tickets = ws->tickets.p;
