@@ -594,6 +594,55 @@ def leg_configs(cx):
     return out
 
 
+def leg_mixed(cx, n_pairs=10, sets=2, k=50):
+    """20 mixed requests — 10 x C1 (f32 4 MiB contiguous sum) and 10 x C3 (f64 [128,128,128] hyperslab
+    min / max, missing_value) — as ONE heterogeneous launch (rdx_execute_multi_device), rotating over
+    `sets` distinct sets of chunks (> the Infinity Cache); beside it the same 20 requests as 20
+    single-request launches on one stream."""
+    import numpy as np
+    torch, _abi = cx.torch, cx.abi
+    v3 = _c3_host()
+    v1 = np.random.default_rng(0x5EED0002).random(1 << 20, dtype=np.float32)
+    batches = []
+    for _ in range(sets):
+        items, keep = [], []
+        for i in range(n_pairs):
+            for op, creq, data, nbytes in (("sum", _abi.CRequest("sum", "float32"), v1, 4 << 20),
+                                           ("min" if i % 2 == 0 else "max", _c3_req(_abi, "min" if i % 2 == 0 else "max"),
+                                            v3, 16 << 20)):
+                d = torch.from_numpy(data).cuda()
+                body = torch.zeros(2, dtype=torch.float64, device="cuda")
+                counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+                status = torch.zeros(1, dtype=torch.int32, device="cuda")
+                keep.append((creq, d, body, counts, status))
+                items.append((creq, d.data_ptr(), nbytes, body.data_ptr(), counts.data_ptr(), status.data_ptr()))
+        batches.append((items, keep))
+    alg = n_pairs * ((4 << 20) + C3_NSEL * 8 + 32)
+
+    def multi_step(i):
+        st, _ = cx.ws.execute_multi_device(batches[i % sets][0], cx.stream.cuda_stream)
+        assert not any(st)
+
+    t = cx.dev_time(multi_step, k, warm=sets)
+    for _, keep in batches:
+        assert all(int(kk[4][0]) == 0 for kk in keep)
+        assert all(int(kk[3][0]) == (1 << 20) for kk in keep[0::2])
+    flat = [it for items, _ in batches for it in items]
+
+    def serial_step(i):
+        creq, dptr, nbytes, b, c, s_ = flat[i % len(flat)]
+        cx.ws.execute_device(creq, dptr, nbytes, b, c, s_, cx.stream.cuda_stream)
+
+    ts = cx.dev_time(serial_step, k * 2 * n_pairs, warm=len(flat)) * 2 * n_pairs
+    return {"workload": f"{2 * n_pairs} mixed requests per launch: {n_pairs} x C1 (f32 4 MiB sum) + {n_pairs} x C3 "
+                        "(f64 hyperslab min/max, missing_value), each its own request; rdx_execute_multi_device",
+            "us_per_launch": round(t * 1e6, 2), "us_per_request": round(t / (2 * n_pairs) * 1e6, 3),
+            "bytes_alg_per_launch": alg, "roofline_frac": round(alg / t / 1e9 / PEAK_GBS, 4),
+            "serial_single_launches_us": round(ts * 1e6, 2),
+            "serial_roofline_frac": round(alg / ts / 1e9 / PEAK_GBS, 4),
+            "timing": "HIP events on the launch stream around K back-to-back calls (host table upload included)"}
+
+
 def leg_host(cx):
     """Host-inclusive rates (chunk in host memory -> H2D -> kernels -> D2H through rdx_execute), pageable and
     page-locked (rdx_host_alloc) buffers, next to the raw PCIe copy of the same bytes (torch, pinned)."""
@@ -810,9 +859,7 @@ def main():
         extra["c4z_inflate"] = leg_inflate(cx, solo and not args.no_cpu_baseline)
     if world == 1 and not args.no_configs:
         extra["configs"] = leg_configs(cx)
-        if hasattr(cx.ws, "execute_multi_device"):
-            from reductionist_amd import mixed
-            extra["mixed_requests"] = mixed.bench_leg(cx)
+        extra["mixed_requests"] = leg_mixed(cx)
     if world == 1 and not args.no_host:
         extra["host_inclusive"] = leg_host(cx)
     cpu_line = None

@@ -205,6 +205,25 @@ rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req,
                        int64_t *counts, uint64_t counts_capacity,
                        rdx_response_info *info);
 
+/* The same, with response buffers the engine allocates: one call for any request — including a gzip /
+ * zlib chunk, whose response size is only known after inflating it (calling rdx_plan + rdx_execute for
+ * a compressed chunk would need a sizing call that inflates it twice).  body / counts live in one
+ * page-locked block from a per-context pool, so a Rust host can hand them to the HTTP response without
+ * a copy (bytes::Bytes::from_owner, freeing with rdx_result_free when the response is dropped); `counts`
+ * is exactly CBORResponse's count_as_bytes when option_count_as_bytes is set (models.rs:379-401: the
+ * i64 counts in native byte order), and info.shape the u64 array of shape_as_bytes.
+ * Select from page-locked input into a page-locked response (this API, or rdx_execute with
+ * rdx_host_alloc buffers) is pipelined: the chunk's H2D and the response's D2H overlap. */
+typedef struct rdx_result {
+    rdx_response_info info;
+    void *body;            /* info.body_bytes bytes (16-byte aligned) */
+    int64_t *counts;       /* info.n_counts values */
+    uint64_t reserved[2];
+} rdx_result;
+rdx_status rdx_execute_owned(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len,
+                             rdx_result **out);
+void rdx_result_free(rdx_context *ctx, rdx_result *result);
+
 /* Device-resident path: everything already in HBM, nothing copied, asynchronous on `stream`.
  * A workspace holds the per-stream scratch (partials, arrival tickets, unshuffle buffers); use one
  * workspace per concurrently used stream. `d_status` (device, one uint32 per chunk, may be NULL)
@@ -229,6 +248,29 @@ rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req,
                                     uint64_t chunk_len,
                                     void *d_bodies, int64_t *d_counts, uint32_t *d_status,
                                     void *stream, rdx_response_info *info);
+
+/* One request of a heterogeneous batch (rdx_execute_multi_device): each carries its own request. */
+typedef struct rdx_multi_item {
+    const rdx_request *req;   /* its own op, dtype, shape, selection, axes, byte order, filters, missing */
+    const void *d_chunk;      /* device pointer to the raw (uncompressed) chunk */
+    uint64_t chunk_len;
+    void *d_body;             /* device, >= rdx_plan's body_bytes */
+    int64_t *d_counts;        /* device, >= rdx_plan's n_counts */
+    uint32_t *d_status;       /* device word (may be NULL): 0 or a status raised in the kernels */
+} rdx_multi_item;
+
+/* Many independent requests on one stream — the request-level concurrency of src/app.rs:147-152
+ * (every HTTP request is its own operation<T>() call) folded into as few launches as possible: every
+ * all-axes request (axis unset) whose filters fuse (at most filters[0] with element_size == sizeof(T))
+ * and whose missing_values list has at most 16 entries runs in ONE heterogeneous launch (k_multi), each
+ * with its own dtype, op, view, byte order and missing predicate; the others (axis reductions, select,
+ * axis = [], filter chains, long missing lists) run as their own launches on the same stream, after it.
+ * statuses[i] (HOST, n entries) receives request i's planning status — an invalid request does not stop
+ * the others; infos[i] (HOST, may be NULL) its response shape and sizes.  Compressed requests are
+ * refused per item (RDX_E_INVALID_ARGUMENT): decompress them first (rdx_decompress_batch_device).
+ * Returns RDX_OK unless the launch itself failed. */
+rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_multi_item *items, void *stream,
+                                    uint32_t *statuses, rdx_response_info *infos);
 
 /* compression::decompress (src/compression.rs:18-27, gzip and zlib) for a batch of n device-resident
  * compressed streams, asynchronous on `stream`: stream i (h_in_ptrs[i] device pointer, h_in_lens[i]

@@ -1,0 +1,67 @@
+//! Wiring of the GPU plugins into reductionist-rs's router (changes to `src/app.rs`, reference
+//! app.rs:46-79 / 123-183).  Not compiled here (no cargo).
+//!
+//! * start-up: `app::init` (app.rs:46-53) also creates the engine's device pool when the server runs with
+//!   `--use-gpu` / `REDUCTIONIST_USE_GPU` (a new clap flag beside `use_rayon`, cli.rs:7-98), listing the
+//!   devices in `REDUCTIONIST_GPU_DEVICES` (default: all visible);
+//! * routes: `/v2/{count,max,min,select,sum}` go to `operation_handler::<operations_gpu::GpuX>` instead of
+//!   `operations::X` (app.rs:63-67);
+//! * the synchronous part: `operation_gpu::<T>` replaces `operation::<T>` (app.rs:163-183) for the GPU
+//!   plugins, which take the RAW chunk — the engine runs filter_pipeline and validate_raw_size itself.
+
+use bytes::Bytes;
+use tracing::debug_span;
+
+use crate::{compression, error::ActiveStorageError, models, operation, operations_gpu};
+
+/// In `app::init` (app.rs:46-53).
+pub fn init_gpu(args: &crate::cli::CommandLineArgs) {
+    if args.use_gpu {
+        operations_gpu::init(&args.gpu_devices).expect("no usable gfx950 device");
+    }
+}
+
+/// In `router` (app.rs:60-79): the GPU routes.
+pub fn gpu_routes() -> axum::Router<crate::app_state::SharedAppState> {
+    use axum::routing::post;
+    axum::Router::new()
+        .route("/count", post(operation_handler::<operations_gpu::GpuCount>))
+        .route("/max", post(operation_handler::<operations_gpu::GpuMax>))
+        .route("/min", post(operation_handler::<operations_gpu::GpuMin>))
+        .route("/select", post(operation_handler::<operations_gpu::GpuSelect>))
+        .route("/sum", post(operation_handler::<operations_gpu::GpuSum>))
+}
+
+/// Replaces `operation::<T>` (app.rs:163-183) for the GPU plugins; `operation_handler` (app.rs:123-153)
+/// calls it in place of `operation` (under the same task permit / rayon spawn).
+pub fn operation_gpu<T: operation::Operation>(
+    request_data: models::RequestData,
+    data: Bytes,
+) -> Result<models::Response, ActiveStorageError> {
+    // One request = one DEFLATE stream, and a stream is serial: a wavefront decodes a 4 MiB chunk in
+    // ~100-220 ms, a CPU core in ~4-7 ms.  A lone compressed request therefore keeps the
+    // reference's host decompression (compression.rs:18-27); chunks are inflated on the device only in
+    // batches (rdx_decompress_batch_device).  blosc2 is decoded on the host always.
+    let (request_data, data) = match request_data.compression {
+        Some(c) => {
+            let d = compression::decompress(c, &data)?;
+            let mut rd = request_data;
+            rd.compression = None;
+            (rd, d)
+        }
+        None => (request_data, data),
+    };
+    // Bytes -> Vec<u8> without a copy, as the reference asserts (app.rs:173-181)
+    let vec: Vec<u8> = data.into();
+    debug_span!("operation_gpu").in_scope(|| T::execute(&request_data, vec))
+}
+
+// `operation_handler` body change (app.rs:147-152):
+//
+//     if state.args.use_rayon {
+//         tokio_rayon::spawn(move || operation_gpu::<T>(request_data, data)).await
+//     } else {
+//         let _task_permit = state.resource_manager.task().await?;
+//         operation_gpu::<T>(request_data, data)
+//     }
+use crate::app::operation_handler;

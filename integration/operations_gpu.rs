@@ -1,0 +1,289 @@
+//! GPU `Operation` plugins for reductionist-rs: the same plugin surface (`operation.rs:53-66`) backed by
+//! the MI355X engine through `rdx_ffi` (this directory).  New file for the reference crate:
+//! `src/operations_gpu.rs`; `app.rs` routes `/v2/{count,max,min,select,sum}` to `GpuCount` ... `GpuSum`
+//! when the server runs with a GPU (see `app_gpu.rs`).  Not compiled in this image (no cargo): checked
+//! textually by `tests/test_integration_cpu.py`.
+//!
+//! Each `execute` takes the RAW chunk (still compressed, still shuffled): the engine runs
+//! `filter_pipeline` (`filter_pipeline.rs:19-34`), `validate_raw_size` (`app.rs:169-172`), the byte-order
+//! swap and slicing (`array.rs:147-208`, `:93-144`) and the `NumOperation` (`operations.rs`) in the
+//! reference's order, and returns the first error the reference would raise.
+
+use std::os::raw::c_void;
+use std::sync::OnceLock;
+
+use bytes::Bytes;
+
+use crate::error::ActiveStorageError;
+use crate::models::{self, Compression, DType, Filter, Order, ReductionAxes};
+use crate::operation::Operation;
+use crate::rdx_ffi::*;
+use crate::types::{ByteOrder, Missing};
+
+/// The engine's device pool: one per process, created at start-up (`app::init`, app.rs:46-53).
+struct Ctx(*mut RdxContext);
+unsafe impl Send for Ctx {}
+unsafe impl Sync for Ctx {} // rdx_execute* are thread-safe (include/rdx.h, rdx_context)
+
+static CTX: OnceLock<Ctx> = OnceLock::new();
+
+pub fn init(devices: &[i32]) -> Result<(), ActiveStorageError> {
+    let mut ctx = std::ptr::null_mut();
+    check(unsafe { rdx_context_create(devices.as_ptr(), devices.len() as i32, &mut ctx) }, None)?;
+    let _ = CTX.set(Ctx(ctx));
+    Ok(())
+}
+
+fn ctx() -> *mut RdxContext {
+    CTX.get().expect("operations_gpu::init not called").0
+}
+
+/// `Gpu<OP>` — OP: 0 count, 1 max, 2 min, 3 select, 4 sum (rdx_op).
+pub struct Gpu<const OP: u32>;
+pub type GpuCount = Gpu<0>;
+pub type GpuMax = Gpu<1>;
+pub type GpuMin = Gpu<2>;
+pub type GpuSelect = Gpu<3>;
+pub type GpuSum = Gpu<4>;
+
+impl<const OP: u32> Operation for Gpu<OP> {
+    fn execute(rd: &models::RequestData, data: Vec<u8>) -> Result<models::Response, ActiveStorageError> {
+        let req = Marshalled::new(rd, OP)?;
+        let mut res: *mut RdxResult = std::ptr::null_mut();
+        // One call, any request (compressed chunks included): the engine sizes and allocates the
+        // response in page-locked memory (include/rdx.h rdx_execute_owned).
+        check(
+            unsafe { rdx_execute_owned(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, &mut res) },
+            rd.compression,
+        )?;
+        let owner = Owned(res);
+        let info = unsafe { (*res).info };
+        let shape: Vec<usize> = info.shape[..info.ndim as usize].iter().map(|&s| s as usize).collect();
+        let counts: Vec<i64> = owner.counts().to_vec();
+        // the body stays in the engine's page-locked block until the HTTP response is dropped
+        let body = Bytes::from_owner(owner);
+        Ok(models::Response::new(
+            body,
+            dtype_of(info.dtype),
+            shape,
+            counts,
+            rd.option_shape_as_bytes.unwrap_or(false),
+            rd.option_count_as_bytes.unwrap_or(false),
+        ))
+    }
+}
+
+/// An `RdxResult` owned by a `Bytes` (freed back to the engine's pool on drop).
+struct Owned(*mut RdxResult);
+unsafe impl Send for Owned {}
+unsafe impl Sync for Owned {}
+
+impl Owned {
+    fn counts(&self) -> &[i64] {
+        unsafe { std::slice::from_raw_parts((*self.0).counts, (*self.0).info.n_counts as usize) }
+    }
+}
+
+impl AsRef<[u8]> for Owned {
+    fn as_ref(&self) -> &[u8] {
+        unsafe { std::slice::from_raw_parts((*self.0).body as *const u8, (*self.0).info.body_bytes as usize) }
+    }
+}
+
+impl Drop for Owned {
+    fn drop(&mut self) {
+        unsafe { rdx_result_free(ctx(), self.0) }
+    }
+}
+
+/// `RequestData` (models.rs:133-176) as the plain C request of include/rdx.h; owns the arrays the
+/// request points into.
+struct Marshalled {
+    c: RdxRequest,
+    _shape: Vec<u64>,
+    _selection: Vec<RdxSlice>,
+    _axes: Vec<u64>,
+    _filters: Vec<RdxFilter>,
+    _missing: Vec<u8>,
+}
+
+impl Marshalled {
+    fn new(rd: &models::RequestData, op: u32) -> Result<Self, ActiveStorageError> {
+        let shape: Vec<u64> = rd.shape.iter().flatten().map(|&s| s as u64).collect();
+        let selection: Vec<RdxSlice> = rd
+            .selection
+            .iter()
+            .flatten()
+            .map(|s| RdxSlice { start: s.start as i64, end: s.end as i64, stride: s.stride as i64 })
+            .collect();
+        let (axes_kind, axes): (u32, Vec<u64>) = match &rd.axis {
+            ReductionAxes::All => (0, vec![]),
+            ReductionAxes::One(a) => (1, vec![*a as u64]),
+            ReductionAxes::Multi(v) => (2, v.iter().map(|&a| a as u64).collect()),
+        };
+        let filters: Vec<RdxFilter> = rd
+            .filters
+            .iter()
+            .flatten()
+            .map(|f| match f {
+                Filter::Shuffle { element_size } => RdxFilter { id: 1, reserved: 0, element_size: *element_size as u64 },
+                Filter::ShuffleSimd { element_size } => {
+                    RdxFilter { id: 2, reserved: 0, element_size: *element_size as u64 }
+                }
+            })
+            .collect();
+        // Missing<DValue> -> raw values of the request dtype with the reference's own conversion
+        // (missing.rs:85-110 / dvalue.rs:43-83), so IncompatibleMissing is raised exactly as today.
+        let (kind, missing) = match &rd.missing {
+            None => (0, vec![]),
+            Some(m) => marshal_missing(rd.dtype, m)?,
+        };
+        let n_values = match kind {
+            0 => 0,
+            5 => 2,
+            2 => missing.len() as u64 / rd.dtype.size_of() as u64,
+            _ => 1,
+        };
+        let c = RdxRequest {
+            abi_version: RDX_ABI_VERSION,
+            op,
+            dtype: dtype_code(rd.dtype),
+            byte_order: match rd.byte_order {
+                None => 0,
+                Some(ByteOrder::Little) => 1,
+                Some(ByteOrder::Big) => 2,
+            },
+            order: match rd.order {
+                None => 0,
+                Some(Order::C) => 1,
+                Some(Order::F) => 2,
+            },
+            axes_kind,
+            ndim: shape.len() as u32,
+            n_axes: axes.len() as u32,
+            shape: if shape.is_empty() { std::ptr::null() } else { shape.as_ptr() },
+            selection: if selection.is_empty() { std::ptr::null() } else { selection.as_ptr() },
+            axes: if axes_kind == 0 { std::ptr::null() } else { axes.as_ptr() },
+            n_filters: filters.len() as u32,
+            compression: match rd.compression {
+                None => 0,
+                Some(Compression::Gzip) => 1,
+                Some(Compression::Zlib) => 2,
+                Some(Compression::Blosc2) => 3,
+            },
+            filters: if filters.is_empty() { std::ptr::null() } else { filters.as_ptr() },
+            missing: RdxMissing { kind, reserved: 0, n_values, values: missing.as_ptr() as *const c_void },
+            has_size: rd.size.is_some() as u32,
+            reserved: 0,
+            size: rd.size.unwrap_or(0) as u64,
+        };
+        Ok(Marshalled { c, _shape: shape, _selection: selection, _axes: axes, _filters: filters, _missing: missing })
+    }
+}
+
+fn marshal_missing(dtype: DType, m: &Missing<crate::types::DValue>) -> Result<(u32, Vec<u8>), ActiveStorageError> {
+    fn typed<T: crate::operation::Element + zerocopy::AsBytes>(
+        m: &Missing<crate::types::DValue>,
+    ) -> Result<(u32, Vec<u8>), ActiveStorageError> {
+        let t = Missing::<T>::try_from(m)?;
+        let mut out = Vec::new();
+        let kind = match &t {
+            Missing::MissingValue(v) => {
+                out.extend_from_slice(v.as_bytes());
+                1
+            }
+            Missing::MissingValues(vs) => {
+                vs.iter().for_each(|v| out.extend_from_slice(v.as_bytes()));
+                2
+            }
+            Missing::ValidMin(v) => {
+                out.extend_from_slice(v.as_bytes());
+                3
+            }
+            Missing::ValidMax(v) => {
+                out.extend_from_slice(v.as_bytes());
+                4
+            }
+            Missing::ValidRange(a, b) => {
+                out.extend_from_slice(a.as_bytes());
+                out.extend_from_slice(b.as_bytes());
+                5
+            }
+        };
+        Ok((kind, out))
+    }
+    match dtype {
+        DType::Int32 => typed::<i32>(m),
+        DType::Int64 => typed::<i64>(m),
+        DType::Uint32 => typed::<u32>(m),
+        DType::Uint64 => typed::<u64>(m),
+        DType::Float32 => typed::<f32>(m),
+        DType::Float64 => typed::<f64>(m),
+    }
+}
+
+fn dtype_code(d: DType) -> u32 {
+    match d {
+        DType::Int32 => 0,
+        DType::Int64 => 1,
+        DType::Uint32 => 2,
+        DType::Uint64 => 3,
+        DType::Float32 => 4,
+        DType::Float64 => 5,
+    }
+}
+
+fn dtype_of(code: u32) -> DType {
+    match code {
+        0 => DType::Int32,
+        1 => DType::Int64,
+        2 => DType::Uint32,
+        3 => DType::Uint64,
+        4 => DType::Float32,
+        _ => DType::Float64,
+    }
+}
+
+/// rdx_status -> the ActiveStorageError the reference raises for the same condition (error.rs:242-376).
+pub fn check(st: i32, compression: Option<Compression>) -> Result<(), ActiveStorageError> {
+    use status::*;
+    match st {
+        OK => Ok(()),
+        // models.rs:242-313 validators / validate_raw_size -> 400
+        E_REQUEST_VALIDATION => Err(ActiveStorageError::RequestDataValidationSingle(
+            validator::ValidationError::new("request data is not valid"),
+        )),
+        // array.rs:18-27 zerocopy length / alignment -> 500 (error.rs:271)
+        E_FROM_BYTES => Err(ActiveStorageError::FromBytes { type_name: "T" }),
+        // array.rs:58-63 ndarray from_shape -> 400
+        E_SHAPE_INVALID => {
+            Err(ActiveStorageError::ShapeInvalid(ndarray::ShapeError::from_kind(ndarray::ErrorKind::OutOfBounds)))
+        }
+        // shuffle.rs:21 assert_eq!(len % element_size, 0): the reference panics; parity
+        E_SHUFFLE_LENGTH => panic!("assertion `left == right` failed"),
+        // operations.rs:181-183,355-357: NaN in a min/max comparison panics in the reference; parity
+        E_NAN_UNORDERED => panic!("unexpected undefined order error for min"),
+        // compression.rs:29-57 blosc2 is decoded on the host (compression::decompress) before the call
+        E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 on the GPU".into() }),
+        // compression.rs:60-82 -> DecompressionFlate2 / DecompressionZune, 400 (error.rs:247-249)
+        E_DECOMPRESSION => {
+            let code = unsafe { rdx_inflate_last_error() };
+            let msg = unsafe { std::ffi::CStr::from_ptr(rdx_inflate_error_string(code)) }.to_string_lossy().into_owned();
+            Err(match compression {
+                // compression.rs:184 reads the message back from DecodeErrorStatus::GenericStr
+                Some(Compression::Zlib) => ActiveStorageError::DecompressionZune(
+                    zune_inflate::errors::InflateDecodeErrors::new_with_error(
+                        zune_inflate::errors::DecodeErrorStatus::GenericStr(msg),
+                    ),
+                ),
+                _ => ActiveStorageError::DecompressionFlate2(std::io::Error::new(std::io::ErrorKind::InvalidInput, msg)),
+            })
+        }
+        // device-side failures are the engine's own: a 500 of their own variant (error_gpu.rs)
+        E_OUT_OF_MEMORY => Err(ActiveStorageError::GpuEngine { status: st, error: "device or pinned memory exhausted".into() }),
+        _ => {
+            let msg = unsafe { std::ffi::CStr::from_ptr(rdx_status_string(st)) }.to_string_lossy().into_owned();
+            Err(ActiveStorageError::GpuEngine { status: st, error: msg })
+        }
+    }
+}

@@ -12,28 +12,84 @@
 namespace rdx {
 namespace {
 
-constexpr int kMultiDims = 4;   // canonical dims kept in registers; deeper views read the table per vector
+constexpr int kMultiDims = 4;   // canonical dims of a k_multi view (deeper views run as their own launch)
+
+// Per-workgroup copy of the request fields its lanes use per element (filled from the request table).
+struct MultiShared {
+    uint64_t list[kInlineMissing];   // missing_values
+    uint32_t count[kMultiDims];
+    uint64_t magic[kMultiDims];
+    int64_t vstride[kMultiDims], rstride[kMultiDims];
+    int64_t base_off, r0;
+};
+
+// The missing predicate of one request (missing.rs:114-122 / operations.rs:25-33): the comparison
+// forms branch-free on two scalars, a missing_values list (<= 16, reference order) from LDS, so the
+// request's descriptor never has to live in scalar registers whole (a 16-entry list there spilled the
+// kernel's SGPRs into its inner loop).
+template <typename T>
+struct MultiMiss {
+    T a, hi;
+    bool eq_on, lo_on, hi_on, filt;
+    uint32_t n_list;
+    const uint64_t *list;   // LDS
+    __device__ __forceinline__ bool included(T x) const {
+        bool missing = (eq_on & (x == a)) | (lo_on & (x < a)) | (hi_on & (x > hi));
+        for (uint32_t i = 0; i < n_list; ++i) missing |= x == from_bits64<T>(list[i]);
+        bool inc = !missing;
+        if constexpr (std::is_floating_point_v<T>) inc = inc & !(filt & (lo_on | hi_on) & (x != x));
+        return inc;
+    }
+};
 
 template <typename T, int OP, bool FUSED, int VW>
-__device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, uint32_t b) {
+__device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, uint32_t b, MultiShared *sd) {
     constexpr int kU = VW > 1 ? 4 : 8;
     const KAllStrided &a = it->a;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint8_t *base = a.src.base;
+    const uint64_t plane = a.src.plane;
     const bool bswap = a.src.bswap;
     const KView &v = a.view;
-    const int nd = v.ndim;
+    MultiMiss<T> mm;
+    {
+        const uint32_t k = a.miss.kind;
+        mm.a = from_bits64<T>(a.miss.v0);
+        mm.hi = k == RDX_MISSING_VALID_MAX ? mm.a : from_bits64<T>(a.miss.v1);
+        mm.eq_on = k == RDX_MISSING_VALUE;
+        mm.lo_on = k == RDX_MISSING_VALID_MIN || k == RDX_MISSING_VALID_RANGE;
+        mm.hi_on = k == RDX_MISSING_VALID_MAX || k == RDX_MISSING_VALID_RANGE;
+        mm.filt = a.filter_semantics != 0;
+        mm.n_list = k == RDX_MISSING_VALUES ? a.miss.n : 0;   // <= kInlineMissing (longer lists run alone)
+        if (threadIdx.x < mm.n_list) sd->list[threadIdx.x] = a.miss.inl[threadIdx.x];
+        if (threadIdx.x < kMultiDims) {
+            const int k = threadIdx.x;
+            const bool in = k < v.ndim;
+            sd->count[k] = in ? v.count[k] : 1u;
+            sd->magic[k] = in ? v.div[k].magic : 0ull;
+            sd->vstride[k] = in ? v.vstride[k] : 0;
+            sd->rstride[k] = in ? v.rstride[k] : 0;
+        }
+        if (threadIdx.x == 0) {
+            sd->base_off = v.base_off;
+            sd->r0 = v.r0;
+        }
+        mm.list = sd->list;
+        __syncthreads();
+    }
+    // The view's (<= kMultiDims, host-checked) dims reach every lane through LDS, i.e. as vector
+    // registers: held in scalar registers beside the rest of the request they spilled in the loop.
     uint32_t cnt[kMultiDims];
     uint64_t mag[kMultiDims];
     int64_t vs[kMultiDims], rs[kMultiDims];
 #pragma unroll
     for (int k = 0; k < kMultiDims; ++k) {
-        cnt[k] = k < nd ? v.count[k] : 1;
-        mag[k] = k < nd ? v.div[k].magic : 0;
-        vs[k] = k < nd ? v.vstride[k] : 0;
-        rs[k] = k < nd ? v.rstride[k] : 0;
+        cnt[k] = sd->count[k];
+        mag[k] = sd->magic[k];
+        vs[k] = sd->vstride[k];
+        rs[k] = sd->rstride[k];
     }
-    const bool deep = nd > kMultiDims;
+    const int64_t base_off = sd->base_off, r0 = sd->r0;
     Red<T, OP> r;
     r.init();
     const uint64_t nv = v.n / VW;
@@ -50,31 +106,21 @@ __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, ui
             ok[u] = g < g_end;
             if (!ok[u]) g = g0;  // clamped into the range: the load issues unconditionally
             uint32_t q = (uint32_t)(g * VW);
-            int64_t o = v.base_off, rr = v.r0;
-            if (!deep) {
+            int64_t o = base_off, rr = r0;
 #pragma unroll
-                for (int k = 0; k < kMultiDims; ++k) {
-                    const uint32_t qn = udiv(q, mag[k]);
-                    const uint32_t idx = q - qn * cnt[k];
-                    o += (int64_t)idx * vs[k];
-                    rr += (int64_t)idx * rs[k];
-                    q = qn;
-                }
-            } else {
-                for (int k = 0; k < nd; ++k) {
-                    const uint32_t qn = udiv(q, v.div[k].magic);
-                    const uint32_t idx = q - qn * v.count[k];
-                    o += (int64_t)idx * v.vstride[k];
-                    rr += (int64_t)idx * v.rstride[k];
-                    q = qn;
-                }
+            for (int k = 0; k < kMultiDims; ++k) {
+                const uint32_t qn = udiv(q, mag[k]);
+                const uint32_t idx = q - qn * cnt[k];
+                o += (int64_t)idx * vs[k];
+                if constexpr (Red<T, OP>::kRank) rr += (int64_t)idx * rs[k];
+                q = qn;
             }
             off[u] = o;
             rk[u] = rr;
         }
         Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) raw_load(raw[u], base, a.src.plane, (uint64_t)off[u]);
+        for (int u = 0; u < kU; ++u) raw_load(raw[u], base, plane, (uint64_t)off[u]);
 #pragma unroll
         for (int u = 0; u < kU; ++u) raw_cvt(raw[u], bswap, x[u]);
 #pragma unroll
@@ -82,7 +128,7 @@ __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, ui
             if (!ok[u]) continue;
 #pragma unroll
             for (int j = 0; j < VW; ++j) {
-                if (!included_mk<T, MK_ANY>(a.miss, x[u][j], a.filter_semantics)) continue;
+                if (!mm.included(x[u][j])) continue;
                 if constexpr (OP == OP_COUNT) r.cnt += 1;
                 else r.add(x[u][j], [&]() { return rk[u] + (int64_t)j * rs[0]; });
             }
@@ -92,34 +138,35 @@ __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, ui
 }
 
 template <typename T, int OP>
-__device__ __forceinline__ void multi_paths(const KMultiItem *__restrict__ it, uint32_t b) {
+__device__ __forceinline__ void multi_paths(const KMultiItem *__restrict__ it, uint32_t b, MultiShared *sl) {
     constexpr int VWV = 16 / (int)sizeof(T);
-    if (it->a.src.fused) multi_body<T, OP, true, 1>(it, b);
-    else if (it->a.vec > 1) multi_body<T, OP, false, VWV>(it, b);
-    else multi_body<T, OP, false, 1>(it, b);
+    if (it->a.src.fused) multi_body<T, OP, true, 1>(it, b, sl);
+    else if (it->a.vec > 1) multi_body<T, OP, false, VWV>(it, b, sl);
+    else multi_body<T, OP, false, 1>(it, b, sl);
 }
 
 template <typename T>
-__device__ __forceinline__ void multi_ops(const KMultiItem *__restrict__ it, uint32_t b) {
+__device__ __forceinline__ void multi_ops(const KMultiItem *__restrict__ it, uint32_t b, MultiShared *sl) {
     switch (it->op) {
-        case OP_COUNT: multi_paths<T, OP_COUNT>(it, b); break;
-        case OP_MAX: multi_paths<T, OP_MAX>(it, b); break;
-        case OP_MIN: multi_paths<T, OP_MIN>(it, b); break;
-        default: multi_paths<T, OP_SUM>(it, b); break;
+        case OP_COUNT: multi_paths<T, OP_COUNT>(it, b, sl); break;
+        case OP_MAX: multi_paths<T, OP_MAX>(it, b, sl); break;
+        case OP_MIN: multi_paths<T, OP_MIN>(it, b, sl); break;
+        default: multi_paths<T, OP_SUM>(it, b, sl); break;
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_multi(const KMulti m) {
+    __shared__ MultiShared s_req;
     const uint32_t item = m.blk2item[blockIdx.x];
     const KMultiItem *__restrict__ it = m.items + item;
     const uint32_t b = blockIdx.x - it->block0;
     switch (it->dtype) {
-        case RDX_DTYPE_INT32: multi_ops<int32_t>(it, b); break;
-        case RDX_DTYPE_INT64: multi_ops<int64_t>(it, b); break;
-        case RDX_DTYPE_UINT32: multi_ops<uint32_t>(it, b); break;
-        case RDX_DTYPE_UINT64: multi_ops<uint64_t>(it, b); break;
-        case RDX_DTYPE_FLOAT32: multi_ops<float>(it, b); break;
-        default: multi_ops<double>(it, b); break;
+        case RDX_DTYPE_INT32: multi_ops<int32_t>(it, b, &s_req); break;
+        case RDX_DTYPE_INT64: multi_ops<int64_t>(it, b, &s_req); break;
+        case RDX_DTYPE_UINT32: multi_ops<uint32_t>(it, b, &s_req); break;
+        case RDX_DTYPE_UINT64: multi_ops<uint64_t>(it, b, &s_req); break;
+        case RDX_DTYPE_FLOAT32: multi_ops<float>(it, b, &s_req); break;
+        default: multi_ops<double>(it, b, &s_req); break;
     }
 }
 

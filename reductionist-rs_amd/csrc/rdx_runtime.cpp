@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -58,6 +60,7 @@ struct Tuning {
 #endif
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
+    int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 4);   // k_multi fill target
 };
 
 const Tuning &tuning() {
@@ -103,6 +106,20 @@ struct rdx_workspace {
     DevBuf<uint8_t> raw;
     std::vector<uint8_t> last_zptrs, last_zlens;
     uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
+    // heterogeneous batches (k_multi): request table + block map, staged through a ring of slots so
+    // that call i+1's upload (on copy_stream) overlaps call i's kernel instead of queueing behind it
+    static constexpr int kTableSlots = 4;
+    struct TableSlot {
+        uint8_t *dev = nullptr, *host = nullptr;   // device table / its page-locked staging
+        size_t dev_cap = 0, host_cap = 0;
+        hipEvent_t copied = nullptr, consumed = nullptr;
+        bool used = false;
+    } tables[kTableSlots];
+    uint32_t table_next = 0;
+    hipStream_t copy_stream = nullptr;
+    // pipelined host path (map_pipelined): a second stream and one event per piece
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t piece_ev[8] = {};
 };
 
 struct rdx_context {
@@ -111,6 +128,10 @@ struct rdx_context {
     std::vector<std::vector<rdx_workspace *>> free_ws;  // per device index
     std::vector<rdx_workspace *> all_ws;
     std::atomic<uint64_t> rr{0};
+    // page-locked response buffers of rdx_execute_owned (size class -> free blocks; block -> class)
+    std::map<uint64_t, std::vector<void *>> pinned_free;
+    std::map<void *, uint64_t> pinned_class;
+    uint64_t pinned_cached = 0;
 };
 
 namespace {
@@ -157,6 +178,59 @@ rdx_status upload(rdx_workspace *ws, void *dst, const void *src, size_t bytes, s
     RDX_HIP(hipEventRecord(ws->upload_done, s));
     ws->upload_pending = true;
     cache.assign(static_cast<const uint8_t *>(src), static_cast<const uint8_t *>(src) + bytes);
+    return RDX_OK;
+}
+
+// A per-call table (k_multi's request table + block map) into device memory without putting the copy
+// engine's latency between two kernels of the stream: the copy runs on the workspace's copy stream
+// (overlapping whatever `s` is still executing) and `s` waits for it with an event; a ring of slots
+// keeps the tables of the calls in flight intact (a slot is reused once the kernel that read it, four
+// calls ago, has completed).  Call table_consumed() right after the launch that reads *dev.
+rdx_status stage_table(rdx_workspace *ws, const uint8_t *src, size_t bytes, hipStream_t s, const uint8_t **dev,
+                       rdx_workspace::TableSlot **slot) {
+    if (!ws->copy_stream) RDX_HIP(hipStreamCreateWithFlags(&ws->copy_stream, hipStreamNonBlocking));
+    rdx_workspace::TableSlot &t = ws->tables[ws->table_next++ % rdx_workspace::kTableSlots];
+    if (!t.copied) RDX_HIP(hipEventCreateWithFlags(&t.copied, hipEventDisableTiming));
+    if (!t.consumed) RDX_HIP(hipEventCreateWithFlags(&t.consumed, hipEventDisableTiming));
+    if (t.used) {
+        RDX_HIP(hipEventSynchronize(t.consumed));
+        t.used = false;
+    }
+    if (t.host_cap < bytes) {
+        if (t.host) RDX_HIP(hipHostFree(t.host));
+        t.host = nullptr;
+        t.host_cap = 0;
+        const size_t want = std::max(bytes, (size_t)65536);
+        RDX_HIP(hipHostMalloc((void **)&t.host, want, hipHostMallocDefault));
+        t.host_cap = want;
+    }
+    if (t.dev_cap < bytes) {
+        if (t.dev) RDX_HIP(hipFree(t.dev));
+        t.dev = nullptr;
+        t.dev_cap = 0;
+        const size_t want = std::max(bytes, (size_t)65536);
+        RDX_HIP(hipMalloc((void **)&t.dev, want));
+        t.dev_cap = want;
+    }
+    std::memcpy(t.host, src, bytes);
+    RDX_HIP(hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, ws->copy_stream));
+    RDX_HIP(hipEventRecord(t.copied, ws->copy_stream));
+    RDX_HIP(hipStreamWaitEvent(s, t.copied, 0));
+    *dev = t.dev;
+    *slot = &t;
+    return RDX_OK;
+}
+
+rdx_status ensure_aux(rdx_workspace *ws) {
+    if (!ws->aux_stream) RDX_HIP(hipStreamCreateWithFlags(&ws->aux_stream, hipStreamNonBlocking));
+    for (hipEvent_t &e : ws->piece_ev)
+        if (!e) RDX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return RDX_OK;
+}
+
+rdx_status table_consumed(rdx_workspace::TableSlot *t, hipStream_t s) {
+    RDX_HIP(hipEventRecord(t->consumed, s));
+    t->used = true;
     return RDX_OK;
 }
 
@@ -562,6 +636,21 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->zout_len.p);
     fr(ws->zerr.p);
     fr(ws->raw.p);
+    if (ws->copy_stream) (void)hipStreamSynchronize(ws->copy_stream);
+    for (auto &t : ws->tables) {
+        if (t.used) (void)hipEventSynchronize(t.consumed);
+        fr(t.dev);
+        if (t.host) (void)hipHostFree(t.host);
+        if (t.copied) (void)hipEventDestroy(t.copied);
+        if (t.consumed) (void)hipEventDestroy(t.consumed);
+    }
+    if (ws->copy_stream) (void)hipStreamDestroy(ws->copy_stream);
+    if (ws->aux_stream) {
+        (void)hipStreamSynchronize(ws->aux_stream);
+        (void)hipStreamDestroy(ws->aux_stream);
+    }
+    for (hipEvent_t e : ws->piece_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ws->zback) (void)hipHostFree(ws->zback);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
@@ -573,6 +662,215 @@ bool is_gfx950(int dev) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+// ---- host-resident execution (rdx_execute / rdx_execute_owned) --------------------------------------
+// Page-locked response buffers for rdx_execute_owned, pooled per context: pinning a buffer per request
+// costs more than the request (hipHostMalloc of 128 MiB: milliseconds), so freed blocks are kept by size
+// class (powers of two from 4 KiB) up to kPoolCap bytes per context.
+constexpr uint64_t kPoolCap = 2ull << 30;
+
+uint64_t pool_class(uint64_t bytes) {
+    uint64_t c = 4096;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+rdx_status pool_alloc(rdx_context *ctx, uint64_t bytes, void **out) {
+    const uint64_t c = pool_class(std::max<uint64_t>(bytes, 1));
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        auto it = ctx->pinned_free.find(c);
+        if (it != ctx->pinned_free.end() && !it->second.empty()) {
+            *out = it->second.back();
+            it->second.pop_back();
+            ctx->pinned_cached -= c;
+            ctx->pinned_class[*out] = c;
+            return RDX_OK;
+        }
+    }
+    RDX_HIP(hipSetDevice(ctx->devices[0]));
+    RDX_HIP(hipHostMalloc(out, c, hipHostMallocPortable));
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->pinned_class[*out] = c;
+    return RDX_OK;
+}
+
+void pool_free(rdx_context *ctx, void *p) {
+    std::unique_lock<std::mutex> g(ctx->mu);
+    auto it = ctx->pinned_class.find(p);
+    if (it == ctx->pinned_class.end()) return;
+    const uint64_t c = it->second;
+    ctx->pinned_class.erase(it);
+    if (ctx->pinned_cached + c <= kPoolCap) {
+        ctx->pinned_free[c].push_back(p);
+        ctx->pinned_cached += c;
+        return;
+    }
+    g.unlock();
+    (void)hipHostFree(p);
+}
+
+bool is_pinned(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();   // a pageable pointer is not an error for the caller
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Select / axis=[] (Mode::Map) from page-locked host memory into page-locked host memory, pipelined:
+// the output is cut along its outermost dim into pieces; piece k's input slab crosses PCIe on the
+// workspace stream while piece k-1 is gathered and its output comes back on the aux stream, so the H2D
+// of the chunk and the D2H of the response (the two directions of the link) overlap instead of adding up
+// (C5: 256 MiB in + 128 MiB out).
+constexpr int kMapPieces = 8;
+
+rdx_status map_pipelined(rdx_workspace *ws, const ExecPlan &p, const uint8_t *chunk, uint64_t len, uint8_t *body,
+                         int64_t *counts) {
+    const KView &v = p.map.view;
+    const int outer = v.ndim - 1;
+    const uint64_t N = v.count[outer], inner = v.n / N;
+    const int64_t vs = v.vstride[outer];
+    const uint64_t out_es = p.info.body_bytes / v.n;
+    const int S = (int)std::min<uint64_t>(N, kMapPieces);
+    hipStream_t sa = ws->own_stream, sb = ws->aux_stream;
+    rdx_status st;
+    if ((st = ensure(ws, ws->chunk, std::max<uint64_t>(len, 16), sa))) return st;
+    if ((st = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), sa))) return st;
+    if ((st = ensure(ws, ws->counts, std::max<uint64_t>(p.map.kind == 0 ? (uint64_t)S : p.info.n_counts, 1), sa)))
+        return st;
+    if ((st = ensure(ws, ws->status, (uint64_t)S, sa))) return st;
+    RDX_HIP(hipStreamSynchronize(sa));   // allocations done before the aux stream uses them
+    int64_t lo_in = 0, hi_in = 0;        // element extent of one outer index over the inner dims
+    for (int k = 0; k < outer; ++k) {
+        const int64_t span = (int64_t)(v.count[k] - 1) * v.vstride[k];
+        (span < 0 ? lo_in : hi_in) += span;
+    }
+    const uint64_t esz = p.fused ? 1 : p.esz;
+    for (int k = 0; k < S; ++k) {
+        const uint64_t a = (uint64_t)k * N / S, b = (uint64_t)(k + 1) * N / S;
+        const int64_t o0 = v.base_off + (int64_t)a * vs, o1 = v.base_off + (int64_t)(b - 1) * vs;
+        const int64_t lo = std::min(o0, o1) + lo_in, hi = std::max(o0, o1) + hi_in;
+        const uint64_t blo = (uint64_t)lo * esz, bhi = std::min<uint64_t>(len, (uint64_t)(hi + 1) * esz);
+        if (bhi > blo) RDX_HIP(hipMemcpyAsync(ws->chunk.p + blo, chunk + blo, bhi - blo, hipMemcpyHostToDevice, sa));
+        RDX_HIP(hipEventRecord(ws->piece_ev[k], sa));
+        RDX_HIP(hipStreamWaitEvent(sb, ws->piece_ev[k], 0));
+        ExecPlan pk = p;
+        KView &w = pk.map.view;
+        w.count[outer] = (uint32_t)(b - a);
+        w.div[outer] = make_div((uint32_t)(b - a));
+        w.base_off = o0;
+        w.n = inner * (b - a);
+        uint8_t *d_body = ws->body.p + a * inner * out_es;
+        int64_t *d_counts = p.map.kind == 0 ? ws->counts.p + k : ws->counts.p + a * inner;
+        if ((st = run_device(ws, pk, ws->chunk.p, nullptr, 1, len, d_body, d_counts, ws->status.p + k, sb))) return st;
+        RDX_HIP(hipMemcpyAsync(body + a * inner * out_es, d_body, inner * (b - a) * out_es, hipMemcpyDeviceToHost, sb));
+        if (p.map.kind != 0)
+            RDX_HIP(hipMemcpyAsync(counts + a * inner, d_counts, inner * (b - a) * sizeof(int64_t), hipMemcpyDeviceToHost, sb));
+    }
+    int64_t piece_counts[kMapPieces];
+    uint32_t piece_status[kMapPieces];
+    if (p.map.kind == 0) RDX_HIP(hipMemcpyAsync(piece_counts, ws->counts.p, S * sizeof(int64_t), hipMemcpyDeviceToHost, sb));
+    RDX_HIP(hipMemcpyAsync(piece_status, ws->status.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, sb));
+    RDX_HIP(hipStreamSynchronize(sb));
+    uint32_t any = 0;
+    for (int k = 0; k < S; ++k) any |= piece_status[k];
+    if (any) return (rdx_status)any;
+    if (p.map.kind == 0) {
+        int64_t c = 0;
+        for (int k = 0; k < S; ++k) c += piece_counts[k];
+        counts[0] = c;
+    }
+    return RDX_OK;
+}
+
+// operation<T>() for a chunk in host memory (app.rs:163-183): plan, bind the response buffers
+// (caller-provided or pooled), H2D, kernels, D2H; blocks until the response is in host memory.
+rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t *chunk, uint64_t chunk_len,
+                        const std::function<rdx_status(const rdx_response_info &, void **, int64_t **)> &bind,
+                        rdx_response_info *info) {
+    const bool compressed = req.compression != RDX_COMPRESSION_NONE;
+    ExecPlan p;
+    rdx_status st;
+    void *body = nullptr;
+    int64_t *counts = nullptr;
+    if (!compressed) {
+        if ((st = make_plan(req, chunk_len, p))) return st;
+        *info = p.info;
+        if ((st = bind(p.info, &body, &counts))) return st;
+    } else if (req.compression == RDX_COMPRESSION_BLOSC2) {
+        return RDX_E_UNSUPPORTED;
+    }
+
+    // take a workspace (round-robin device, then any free workspace of it)
+    rdx_workspace *ws = nullptr;
+    size_t di = 0;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        di = (size_t)(ctx->rr++ % ctx->devices.size());
+        if (!ctx->free_ws[di].empty()) {
+            ws = ctx->free_ws[di].back();
+            ctx->free_ws[di].pop_back();
+        }
+    }
+    if (!ws) {
+        if ((st = create_workspace(ctx->devices[di], &ws))) return st;
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->all_ws.push_back(ws);
+    }
+    auto run = [&]() -> rdx_status {
+        RDX_HIP(hipSetDevice(ws->device));
+        hipStream_t s = ws->own_stream;
+        rdx_status r;
+        if (!compressed && p.mode == Mode::Map && p.unfused_es.empty() && !p.fused && p.map.view.ndim >= 1 &&
+            p.map.view.count[p.map.view.ndim - 1] >= 2 && chunk_len >= (32ull << 20) && is_pinned(chunk) &&
+            is_pinned(body) && (p.map.kind == 0 || is_pinned(counts))) {
+            if ((r = ensure_aux(ws))) return r;
+            return map_pipelined(ws, p, chunk, chunk_len, static_cast<uint8_t *>(body), counts);
+        }
+        if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
+        if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
+        if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
+        if ((r = ensure(ws, ws->status, 1, s))) return r;
+        if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
+        const uint8_t *src = ws->chunk.p;
+        uint64_t len = chunk_len;
+        if (compressed) {  // the chunk crossed PCIe compressed; inflate it in HBM, then plan on its size
+            uint64_t hint = 0;
+            if (req.compression == RDX_COMPRESSION_GZIP && chunk_len >= 18) {  // RFC 1952 ISIZE
+                const uint8_t *t = chunk + chunk_len - 4;
+                hint = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+            }
+            if ((r = decompress_request(ws, req, ws->chunk.p, chunk_len, hint, s, &len))) return r;
+            src = ws->raw.p;
+            if ((r = make_plan(req, len, p))) return r;
+            *info = p.info;
+            if ((r = bind(p.info, &body, &counts))) return r;
+            if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
+            if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
+        }
+        RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
+        if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
+            return r;
+        uint32_t status = 0;
+        if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
+        if (p.info.n_counts)
+            RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipStreamSynchronize(s));
+        if (status) return (rdx_status)status;
+        return RDX_OK;
+    };
+    st = run();
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->free_ws[di].push_back(ws);
+    }
+    return st;
 }
 
 }  // namespace
@@ -653,6 +951,8 @@ rdx_status rdx_context_create(const int *devices, int n_devices, rdx_context **o
 void rdx_context_destroy(rdx_context *ctx) {
     if (!ctx) return;
     for (rdx_workspace *ws : ctx->all_ws) destroy_workspace(ws);
+    for (auto &kv : ctx->pinned_free)
+        for (void *p : kv.second) (void)hipHostFree(p);
     delete ctx;
 }
 
@@ -791,6 +1091,128 @@ rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req, u
                       static_cast<uint8_t *>(d_bodies), d_counts, d_status, static_cast<hipStream_t>(stream));
 }
 
+rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_multi_item *items, void *stream,
+                                    uint32_t *statuses, rdx_response_info *infos) {
+    if (!ws || (n && (!items || !statuses))) return RDX_E_INVALID_ARGUMENT;
+    if (n == 0) return RDX_OK;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    RDX_HIP(hipSetDevice(ws->device));
+    std::vector<KMultiItem> table;
+    std::vector<uint32_t> blk2item;
+    std::vector<uint64_t> rest;   // requests that run as their own launches
+    uint64_t blocks = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const rdx_multi_item &it = items[i];
+        statuses[i] = RDX_E_INVALID_ARGUMENT;
+        if (!it.req) continue;
+        if (it.req->compression != RDX_COMPRESSION_NONE) continue;
+        ExecPlan p;
+        const rdx_status st = make_plan(*it.req, it.chunk_len, p);
+        statuses[i] = st;
+        if (st) continue;
+        if (infos) infos[i] = p.info;
+        if ((!it.d_chunk && it.chunk_len) || (!it.d_body && p.info.body_bytes) || (!it.d_counts && p.info.n_counts)) {
+            statuses[i] = RDX_E_INVALID_ARGUMENT;
+            continue;
+        }
+        const bool all = (p.mode == Mode::AllStrided && p.all_strided.view.ndim <= 4) ||   // k_multi.hip kMultiDims
+                         (p.mode == Mode::AllContig && p.all_contig.n < (1ull << 32) && p.all_contig.n > 0);
+        if (!all || !p.unfused_es.empty() || !p.miss_list.empty() || table.size() >= 0xffffffffull ||
+            blocks >= (1ull << 30)) {
+            rest.push_back(i);
+            continue;
+        }
+        KMultiItem m{};
+        KAllStrided &a = m.a;
+        if (p.mode == Mode::AllStrided) {
+            a = p.all_strided;
+        } else {
+            const KAllContig &c = p.all_contig;
+            a.view.ndim = 1;
+            a.view.base_off = (int64_t)c.off;
+            a.view.r0 = c.r0;
+            a.view.n = c.n;
+            a.view.count[0] = (uint32_t)c.n;
+            a.view.div[0] = make_div((uint32_t)c.n);
+            a.view.vstride[0] = 1;
+            a.view.rstride[0] = c.rs;
+            a.filter_semantics = c.filter_semantics;
+        }
+        a.src.base = static_cast<const uint8_t *>(it.d_chunk);
+        a.src.ptrs = nullptr;
+        a.src.plane = it.chunk_len / p.esz;
+        a.src.fused = p.fused;
+        a.src.bswap = p.bswap;
+        a.miss = p.miss;
+        a.vec = vec_width(a.view, p.esz, a.src.base, nullptr, 1, p.fused);
+        // workgroups for one load round trip per lane (scaled down below when the batch overfills the chip)
+        const uint64_t per_block = (uint64_t)kBlock * (a.vec > 1 ? 4 : 8);
+        const uint64_t want = (a.view.n / a.vec + per_block - 1) / per_block;
+        a.blocks_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ws->cus * 8));
+        a.out.body = static_cast<uint8_t *>(it.d_body);
+        a.out.counts = it.d_counts;
+        a.out.status = it.d_status;
+        m.dtype = p.dtype;
+        m.op = p.op;
+        blocks += a.blocks_per_chunk;
+        table.push_back(m);
+    }
+    rdx_status st;
+    if (!table.empty()) {
+        // One residency round of the chip (4 k_multi workgroups per CU) serves the whole batch: a batch
+        // that wants more gets proportionally fewer, longer-running workgroups per request (each lane
+        // keeps 4-8 loads in flight per step), so no request pays several dispatch + hand-off rounds.
+        const uint64_t target = (uint64_t)ws->cus * tuning().multi_blocks_per_cu;
+        if (blocks > target) {
+            const double scale = (double)target / (double)blocks;
+            blocks = 0;
+            for (KMultiItem &m : table) {
+                m.a.blocks_per_chunk = (uint32_t)std::max<double>(1.0, std::ceil(m.a.blocks_per_chunk * scale));
+                blocks += m.a.blocks_per_chunk;
+            }
+        }
+        blk2item.reserve(blocks);
+        blocks = 0;
+        for (size_t k = 0; k < table.size(); ++k) {
+            table[k].block0 = (uint32_t)blocks;
+            blk2item.insert(blk2item.end(), table[k].a.blocks_per_chunk, (uint32_t)k);
+            blocks += table[k].a.blocks_per_chunk;
+        }
+        if ((st = ensure(ws, ws->partials, blocks * kRecordU64, s, true))) return st;
+        if ((st = ensure(ws, ws->tickets, table.size() * kTicketWords, s, true))) return st;
+        uint32_t epoch = 0;
+        if ((st = next_epoch(ws, s, epoch))) return st;
+        for (size_t k = 0; k < table.size(); ++k) {
+            KOut &o = table[k].a.out;
+            o.partials = ws->partials.p + (uint64_t)table[k].block0 * kRecordU64;
+            o.tickets = ws->tickets.p + k * kTicketWords;
+            o.epoch = epoch;
+        }
+        const size_t tbytes = table.size() * sizeof(KMultiItem), mbytes = blk2item.size() * sizeof(uint32_t);
+        std::vector<uint8_t> host(tbytes + mbytes);
+        std::memcpy(host.data(), table.data(), tbytes);
+        std::memcpy(host.data() + tbytes, blk2item.data(), mbytes);
+        const uint8_t *dev = nullptr;
+        rdx_workspace::TableSlot *slot = nullptr;
+        if ((st = stage_table(ws, host.data(), host.size(), s, &dev, &slot))) return st;
+        KMulti km{};
+        km.items = reinterpret_cast<const KMultiItem *>(dev);
+        km.blk2item = reinterpret_cast<const uint32_t *>(dev + tbytes);
+        km.n_items = (uint32_t)table.size();
+        RDX_HIP(launch_multi(km, (uint32_t)blocks, s));
+        if ((st = table_consumed(slot, s))) return st;
+    }
+    for (uint64_t i : rest) {
+        const rdx_multi_item &it = items[i];
+        ExecPlan p;
+        if ((st = make_plan(*it.req, it.chunk_len, p))) return st;   // planned above
+        statuses[i] = run_device(ws, p, static_cast<const uint8_t *>(it.d_chunk), nullptr, 1, it.chunk_len,
+                                 static_cast<uint8_t *>(it.d_body), it.d_counts, it.d_status, s);
+        if (statuses[i] == RDX_E_DEVICE || statuses[i] == RDX_E_OUT_OF_MEMORY) return (rdx_status)statuses[i];
+    }
+    return RDX_OK;
+}
+
 rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, uint64_t n,
                                        const void *const *h_in_ptrs, const uint64_t *h_in_lens, void *d_out,
                                        uint64_t out_capacity, uint64_t *d_out_lens, uint32_t *d_errors, void *stream) {
@@ -811,78 +1233,47 @@ rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, 
 rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len, void *body,
                        uint64_t body_capacity, int64_t *counts, uint64_t counts_capacity, rdx_response_info *info) {
     if (!ctx || !req || !info || (!chunk && chunk_len)) return RDX_E_INVALID_ARGUMENT;
-    const bool compressed = req->compression != RDX_COMPRESSION_NONE;
-    ExecPlan p;
-    rdx_status st;
-    if (!compressed) {
-        if ((st = make_plan(*req, chunk_len, p))) return st;
-        *info = p.info;
-        if (body_capacity < p.info.body_bytes || counts_capacity < p.info.n_counts) return RDX_E_BUFFER_TOO_SMALL;
-        if ((!body && p.info.body_bytes) || (!counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
-    } else if (req->compression == RDX_COMPRESSION_BLOSC2) {
-        return RDX_E_UNSUPPORTED;
-    }
-
-    // take a workspace (round-robin device, then any free workspace of it)
-    rdx_workspace *ws = nullptr;
-    size_t di = 0;
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        di = (size_t)(ctx->rr++ % ctx->devices.size());
-        if (!ctx->free_ws[di].empty()) {
-            ws = ctx->free_ws[di].back();
-            ctx->free_ws[di].pop_back();
-        }
-    }
-    if (!ws) {
-        if ((st = create_workspace(ctx->devices[di], &ws))) return st;
-        std::lock_guard<std::mutex> g(ctx->mu);
-        ctx->all_ws.push_back(ws);
-    }
-    auto run = [&]() -> rdx_status {
-        RDX_HIP(hipSetDevice(ws->device));
-        hipStream_t s = ws->own_stream;
-        rdx_status r;
-        if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
-        if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
-        if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
-        if ((r = ensure(ws, ws->status, 1, s))) return r;
-        if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
-        const uint8_t *src = ws->chunk.p;
-        uint64_t len = chunk_len;
-        if (compressed) {  // the chunk crossed PCIe compressed; inflate it in HBM, then plan on its size
-            uint64_t hint = 0;
-            if (req->compression == RDX_COMPRESSION_GZIP && chunk_len >= 18) {  // RFC 1952 ISIZE
-                const uint8_t *t = static_cast<const uint8_t *>(chunk) + chunk_len - 4;
-                hint = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
-            }
-            if ((r = decompress_request(ws, *req, ws->chunk.p, chunk_len, hint, s, &len))) return r;
-            src = ws->raw.p;
-            if ((r = make_plan(*req, len, p))) return r;
-            *info = p.info;
-            if (body_capacity < p.info.body_bytes || counts_capacity < p.info.n_counts) return RDX_E_BUFFER_TOO_SMALL;
-            if ((!body && p.info.body_bytes) || (!counts && p.info.n_counts)) return RDX_E_INVALID_ARGUMENT;
-            if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
-            if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
-        }
-        RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
-        if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
-            return r;
-        uint32_t status = 0;
-        if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
-        if (p.info.n_counts)
-            RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        RDX_HIP(hipStreamSynchronize(s));
-        if (status) return (rdx_status)status;
+    auto bind = [&](const rdx_response_info &inf, void **b, int64_t **c) -> rdx_status {
+        if (body_capacity < inf.body_bytes || counts_capacity < inf.n_counts) return RDX_E_BUFFER_TOO_SMALL;
+        if ((!body && inf.body_bytes) || (!counts && inf.n_counts)) return RDX_E_INVALID_ARGUMENT;
+        *b = body;
+        *c = counts;
         return RDX_OK;
     };
-    st = run();
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        ctx->free_ws[di].push_back(ws);
+    return execute_host(ctx, *req, static_cast<const uint8_t *>(chunk), chunk_len, bind, info);
+}
+
+rdx_status rdx_execute_owned(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len,
+                             rdx_result **out) {
+    if (!ctx || !req || !out || (!chunk && chunk_len)) return RDX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    auto *r = new (std::nothrow) rdx_result();
+    if (!r) return RDX_E_OUT_OF_MEMORY;
+    auto bind = [&](const rdx_response_info &inf, void **b, int64_t **c) -> rdx_status {
+        // one page-locked block: body (16 B aligned) then the counts
+        const uint64_t bb = (inf.body_bytes + 15) / 16 * 16;
+        void *mem = nullptr;
+        rdx_status st = pool_alloc(ctx, bb + inf.n_counts * sizeof(int64_t), &mem);
+        if (st) return st;
+        r->body = mem;
+        r->counts = reinterpret_cast<int64_t *>(static_cast<uint8_t *>(mem) + bb);
+        *b = r->body;
+        *c = r->counts;
+        return RDX_OK;
+    };
+    const rdx_status st = execute_host(ctx, *req, static_cast<const uint8_t *>(chunk), chunk_len, bind, &r->info);
+    if (st) {
+        rdx_result_free(ctx, r);
+        return st;
     }
-    return st;
+    *out = r;
+    return RDX_OK;
+}
+
+void rdx_result_free(rdx_context *ctx, rdx_result *r) {
+    if (!r) return;
+    if (r->body) pool_free(ctx, r->body);
+    delete r;
 }
 
 }  // extern "C"

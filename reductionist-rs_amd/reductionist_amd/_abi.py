@@ -75,6 +75,16 @@ class rdx_response_info(C.Structure):
         return [int(self.shape[i]) for i in range(self.ndim)]
 
 
+class rdx_multi_item(C.Structure):
+    _fields_ = [("req", C.POINTER(rdx_request)), ("d_chunk", C.c_void_p), ("chunk_len", C.c_uint64),
+                ("d_body", C.c_void_p), ("d_counts", C.c_void_p), ("d_status", C.c_void_p)]
+
+
+class rdx_result(C.Structure):
+    _fields_ = [("info", rdx_response_info), ("body", C.c_void_p), ("counts", C.POINTER(C.c_int64)),
+                ("reserved", C.c_uint64 * 2)]
+
+
 class CRequest:
     """Owns the ctypes arrays an rdx_request points into (keep it alive during the call)."""
 
@@ -153,6 +163,9 @@ def _declare(lib):
         "rdx_inflate_error_string": (C.c_char_p, [C.c_uint32]),
         "rdx_inflate_last_error": (C.c_uint32, []),
         "rdx_decompress_batch_device": (C.c_int, [VP, C.c_uint32, U64, P(VP), P(U64), VP, U64, VP, VP, VP]),
+        "rdx_execute_multi_device": (C.c_int, [VP, U64, P(rdx_multi_item), VP, P(C.c_uint32), info_p]),
+        "rdx_execute_owned": (C.c_int, [VP, req_p, VP, U64, P(P(rdx_result))]),
+        "rdx_result_free": (None, [VP, P(rdx_result)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -167,7 +180,8 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_missing_from_u64", "rdx_missing_from_f64", "rdx_execute", "rdx_host_alloc", "rdx_host_free",
             "rdx_workspace_create",
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
-            "rdx_inflate_last_error", "rdx_decompress_batch_device"]
+            "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
+            "rdx_execute_owned", "rdx_result_free"]
 
 
 def lib():

@@ -57,6 +57,34 @@ class Engine:
                                   info.n_counts, C.byref(info))
         return st, info, bytes(body)[: info.body_bytes], [int(c) for c in counts[: info.n_counts]]
 
+    def execute_owned(self, creq: _abi.CRequest, data):
+        """rdx_execute_owned: one call, engine-allocated (pooled, page-locked) response buffers, for any
+        request incl. gzip / zlib chunks.  `data`: bytes, or (pointer, length) of host memory."""
+        if isinstance(data, tuple):
+            src, n = C.c_void_p(data[0]), data[1]
+        else:
+            src, n = (C.c_char_p(bytes(data)) if len(data) else None), len(data)
+        res = C.POINTER(_abi.rdx_result)()
+        st = self.lib.rdx_execute_owned(self.ctx, creq.ref, src, n, C.byref(res))
+        if st != _abi.OK:
+            return st, _abi.rdx_response_info(), b"", []
+        r = res.contents
+        info = _abi.rdx_response_info.from_buffer_copy(r.info)
+        body = C.string_at(r.body, info.body_bytes) if info.body_bytes else b""
+        counts = [int(r.counts[i]) for i in range(info.n_counts)]
+        self.lib.rdx_result_free(self.ctx, res)
+        return st, info, body, counts
+
+    def host_alloc(self, nbytes: int):
+        """Page-locked host buffer (rdx_host_alloc) as (pointer, numpy uint8 view); free with host_free."""
+        import numpy as np
+        p = C.c_void_p()
+        check(self.lib.rdx_host_alloc(self.ctx, nbytes, C.byref(p)))
+        return p.value, np.ctypeslib.as_array((C.c_uint8 * max(1, nbytes)).from_address(p.value))
+
+    def host_free(self, ptr: int):
+        self.lib.rdx_host_free(self.ctx, C.c_void_p(ptr))
+
     def execute(self, creq: _abi.CRequest, data: bytes):
         st, info, body, counts = self.execute_raw(creq, data)
         check(st)
@@ -98,6 +126,19 @@ class Workspace:
                                                 C.c_void_p(d_status or 0), C.c_void_p(stream or 0),
                                                 C.byref(info)))
         return info
+
+    def execute_multi_device(self, items, stream: int | None):
+        """Heterogeneous batch (rdx_execute_multi_device): items = [(creq, d_chunk, chunk_len, d_body,
+        d_counts, d_status or None), ...].  Returns (per-request planning statuses, response infos)."""
+        n = len(items)
+        arr = (_abi.rdx_multi_item * max(1, n))()
+        for i, (creq, d_chunk, ln, d_body, d_counts, d_status) in enumerate(items):
+            arr[i] = _abi.rdx_multi_item(C.pointer(creq.c), d_chunk or None, ln, d_body or None, d_counts or None,
+                                         d_status or None)
+        statuses = (C.c_uint32 * max(1, n))()
+        infos = (_abi.rdx_response_info * max(1, n))()
+        check(self.lib.rdx_execute_multi_device(self.ws, n, arr, C.c_void_p(stream or 0), statuses, infos))
+        return [int(x) for x in statuses[:n]], [infos[i] for i in range(n)]
 
     def decompress_batch_device(self, compression: str, d_streams: Sequence[int], lens: Sequence[int], d_out: int,
                                 out_capacity: int, d_out_lens: int, d_errors: int, stream: int | None) -> None:

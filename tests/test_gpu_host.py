@@ -1,0 +1,116 @@
+"""Host-resident entry points beyond rdx_execute's plain path:
+
+* rdx_execute_owned — engine-allocated (pooled, page-locked) response buffers, one call for any request,
+  compressed chunks included (no sizing call that inflates twice); random requests vs the oracle.
+* the pipelined select / axis=[] path (chunk and response in page-locked memory: the chunk's H2D and the
+  response's D2H overlap piece by piece) — C5 at full size and other >= 32 MiB layouts, bit-exact.
+"""
+import ctypes as C
+import zlib
+
+import numpy as np
+import pytest
+
+from helpers import encode_filters, make_request, random_case
+from oracle import py_oracle as oracle
+from reductionist_amd import _abi
+from test_gpu_parity import same_result
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(op, req, got, exp):
+    st, info, body, counts = got
+    ost, oinfo, obody, ocounts = exp
+    assert st == ost, (op, req, st, ost)
+    if ost:
+        return
+    assert info.shape_list() == oinfo.shape_list() and counts == ocounts, (op, req)
+    assert same_result(_abi.DTYPE_NAMES[oinfo.dtype], body, obody), (op, req)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_owned_random_differential(engine, seed):
+    rng = np.random.default_rng(7000 + seed)
+    n = 0
+    while n < 250:
+        op, req, raw = random_case(rng, allow_nan=True, max_dim=12)
+        data = encode_filters(raw, req.get("filters"), oracle.shuffle)
+        if rng.random() < 0.25:
+            req["compression"] = "gzip" if rng.random() < 0.5 else "zlib"
+            c = zlib.compressobj(int(rng.integers(0, 10)), zlib.DEFLATED, 31 if req["compression"] == "gzip" else 15)
+            data = c.compress(data) + c.flush()
+        try:
+            creq = make_request(op, req, oracle.convert)
+        except ValueError:
+            continue
+        _check(op, req, engine.execute_owned(creq, data), oracle.execute(creq, data))
+        n += 1
+
+
+def test_owned_pool_reuse_and_large(engine):
+    """Pool blocks are reused across sizes; a 128 MiB select comes back in a pooled block."""
+    rng = np.random.default_rng(5)
+    for n in (1, 1000, 1 << 20, 123457, 1 << 20):
+        v = rng.integers(-1000, 1000, n).astype(np.int64)
+        creq = make_request("select", {"dtype": "int64"}, oracle.convert)
+        st, info, body, counts = engine.execute_owned(creq, v.tobytes())
+        assert st == 0 and counts == [n] and body == v.tobytes()
+
+
+def _pinned_run(engine, creq, data: np.ndarray):
+    """rdx_execute with the chunk and the response in rdx_host_alloc buffers (the pipelined path)."""
+    lib = _abi.lib()
+    info = _abi.rdx_response_info()
+    assert lib.rdx_plan(creq.ref, data.nbytes, C.byref(info)) == 0
+    src, arr = engine.host_alloc(data.nbytes)
+    arr[:] = data.view(np.uint8).reshape(-1)
+    bp, barr = engine.host_alloc(max(16, info.body_bytes))
+    cp, carr = engine.host_alloc(max(8, 8 * info.n_counts))
+    out = _abi.rdx_response_info()
+    st = lib.rdx_execute(engine.ctx, creq.ref, C.c_void_p(src), data.nbytes, C.c_void_p(bp), info.body_bytes,
+                         C.cast(C.c_void_p(cp), C.POINTER(C.c_int64)), info.n_counts, C.byref(out))
+    body = barr[: info.body_bytes].tobytes()
+    counts = [int(x) for x in carr[: 8 * info.n_counts].view(np.int64)]
+    for p in (src, bp, cp):
+        engine.host_free(p)
+    return st, out, body, counts
+
+
+def test_c5_select_pipelined_full_size(engine):
+    """BASELINE configs[4] from page-locked memory: i64 [512,256,256], selection -> 128 MiB, bit-exact."""
+    rng = np.random.default_rng(0x5EED0006)
+    vals = rng.integers(-2 ** 63, 2 ** 63 - 1, 512 * 256 * 256, dtype=np.int64)
+    req = {"dtype": "int64", "shape": [512, 256, 256], "selection": [[0, 512, 1], [64, 192, 1], [0, 256, 1]]}
+    creq = make_request("select", req, oracle.convert)
+    st, info, body, counts = _pinned_run(engine, creq, vals)
+    assert st == 0 and counts == [16777216] and info.shape_list() == [512, 128, 256]
+    assert np.array_equal(np.frombuffer(body, dtype=np.int64), vals.reshape(512, 256, 256)[:, 64:192, :].ravel())
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_pipelined_map_layouts(engine, case):
+    """>= 32 MiB maps through the pipelined path vs the oracle: reversed outer dim, F-order select,
+    missing data (select's non-missing count summed over pieces), axis=[] values + 0/1 counts, Count
+    with axis=[], big-endian; outer dims not divisible by the piece count."""
+    rng = np.random.default_rng(300 + case)
+    dtype, op, shape, sel, extra = [
+        ("float64", "select", [67, 256, 256], [[66, None, -1], [3, 250, 2], [0, 256, 1]], {}),
+        ("float32", "select", [256, 256, 160], [[0, 256, 1], [0, 256, 1], [10, 150, 1]], {"order": "F"}),
+        ("int32", "select", [300, 200, 160], [[5, 299, 1], [0, 200, 3], [0, 160, 1]], {"missing": {"valid_min": -50}}),
+        ("float32", "sum", [200, 300, 150], [[0, 200, 1], [10, 290, 1], [0, 150, 1]], {"axis": [],
+                                                                                         "missing": {"valid_max": 20.0}}),
+        ("int64", "count", [70, 256, 256], None, {"axis": [], "missing": {"missing_values": [1, 2, 3]}}),
+        ("uint32", "select", [9, 1024, 1024], [[1, 9, 1], [0, 1024, 1], [0, 1024, 2]], {"byte_order": "big"}),
+    ][case]
+    n = int(np.prod(shape))
+    v = rng.integers(-100, 100, n) if not dtype.startswith("u") else rng.integers(0, 1000, n)
+    v = v.astype(dtype)
+    req = {"dtype": dtype, "shape": shape, **extra}
+    if sel:
+        req["selection"] = [[a, b if b is not None else -n - 1, c] for a, b, c in sel]
+    raw = v.astype(v.dtype.newbyteorder(">")) if req.get("byte_order") == "big" else v
+    assert raw.nbytes >= 32 << 20
+    creq = make_request(op, req, oracle.convert)
+    got = _pinned_run(engine, creq, raw)
+    _check(op, req, got, oracle.execute(creq, raw.tobytes()))
