@@ -168,6 +168,8 @@ void slice_axis(View &v, size_t ax, const rdx_slice &s) {
     if (m == 0) off = 0;
     else if (step < 0) off = (end - 1) * stride;
     else off = start * stride;
+    // stride 0 never gets here in the reference (models.rs:187-194 rejects it; ndarray asserts step != 0)
+    if (step == 0) throw OracleError{RDX_E_REQUEST_VALIDATION};
     const u64 abs_step = (u64)(step < 0 ? -step : step);
     u64 d = abs_step == 1 ? m : (m / abs_step + (m % abs_step ? 1 : 0));
     v.offset += off;

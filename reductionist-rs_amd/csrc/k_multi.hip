@@ -14,13 +14,9 @@ namespace {
 
 constexpr int kMultiDims = 4;   // canonical dims of a k_multi view (deeper views run as their own launch)
 
-// Per-workgroup copy of the request fields its lanes use per element (filled from the request table).
+// Per-workgroup copy of a request's missing_values list (compared per element from LDS).
 struct MultiShared {
-    uint64_t list[kInlineMissing];   // missing_values
-    uint32_t count[kMultiDims];
-    uint64_t magic[kMultiDims];
-    int64_t vstride[kMultiDims], rstride[kMultiDims];
-    int64_t base_off, r0;
+    uint64_t list[kInlineMissing];
 };
 
 // The missing predicate of one request (missing.rs:114-122 / operations.rs:25-33): the comparison
@@ -44,7 +40,7 @@ struct MultiMiss {
 
 template <typename T, int OP, bool FUSED, int VW>
 __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, uint32_t b, MultiShared *sd) {
-    constexpr int kU = VW > 1 ? 4 : 8;
+    constexpr int kU = 4;   // loads in flight per lane per step (8 for the lighter bodies measured slower)
     const KAllStrided &a = it->a;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint8_t *base = a.src.base;
@@ -62,34 +58,23 @@ __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, ui
         mm.filt = a.filter_semantics != 0;
         mm.n_list = k == RDX_MISSING_VALUES ? a.miss.n : 0;   // <= kInlineMissing (longer lists run alone)
         if (threadIdx.x < mm.n_list) sd->list[threadIdx.x] = a.miss.inl[threadIdx.x];
-        if (threadIdx.x < kMultiDims) {
-            const int k = threadIdx.x;
-            const bool in = k < v.ndim;
-            sd->count[k] = in ? v.count[k] : 1u;
-            sd->magic[k] = in ? v.div[k].magic : 0ull;
-            sd->vstride[k] = in ? v.vstride[k] : 0;
-            sd->rstride[k] = in ? v.rstride[k] : 0;
-        }
-        if (threadIdx.x == 0) {
-            sd->base_off = v.base_off;
-            sd->r0 = v.r0;
-        }
         mm.list = sd->list;
         __syncthreads();
     }
-    // The view's (<= kMultiDims, host-checked) dims reach every lane through LDS, i.e. as vector
-    // registers: held in scalar registers beside the rest of the request they spilled in the loop.
+    // The view's dims: uniform loads of the request table (scalar registers); the host pads every
+    // view to kMultiDims dims with count 1 / stride 0 (rdx_execute_multi_device).
     uint32_t cnt[kMultiDims];
     uint64_t mag[kMultiDims];
     int64_t vs[kMultiDims], rs[kMultiDims];
 #pragma unroll
     for (int k = 0; k < kMultiDims; ++k) {
-        cnt[k] = sd->count[k];
-        mag[k] = sd->magic[k];
-        vs[k] = sd->vstride[k];
-        rs[k] = sd->rstride[k];
+        cnt[k] = v.count[k];
+        mag[k] = v.div[k].magic;
+        vs[k] = v.vstride[k];
+        rs[k] = v.rstride[k];
     }
-    const int64_t base_off = sd->base_off, r0 = sd->r0;
+    const int64_t base_off = v.base_off, r0 = v.r0;
+    const int nd = v.ndim;   // dims >= nd are padding (count 1): skipped by a uniform branch
     Red<T, OP> r;
     r.init();
     const uint64_t nv = v.n / VW;
@@ -109,7 +94,8 @@ __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, ui
             int64_t o = base_off, rr = r0;
 #pragma unroll
             for (int k = 0; k < kMultiDims; ++k) {
-                const uint32_t qn = udiv(q, mag[k]);
+                if (k > 0 && k >= nd) break;
+                const uint32_t qn = k + 1 < nd ? udiv(q, mag[k]) : 0u;   // the last dim needs no division
                 const uint32_t idx = q - qn * cnt[k];
                 o += (int64_t)idx * vs[k];
                 if constexpr (Red<T, OP>::kRank) rr += (int64_t)idx * rs[k];
@@ -140,8 +126,7 @@ __device__ __forceinline__ void multi_body(const KMultiItem *__restrict__ it, ui
 template <typename T, int OP>
 __device__ __forceinline__ void multi_paths(const KMultiItem *__restrict__ it, uint32_t b, MultiShared *sl) {
     constexpr int VWV = 16 / (int)sizeof(T);
-    if (it->a.src.fused) multi_body<T, OP, true, 1>(it, b, sl);
-    else if (it->a.vec > 1) multi_body<T, OP, false, VWV>(it, b, sl);
+    if (it->a.vec > 1) multi_body<T, OP, false, VWV>(it, b, sl);
     else multi_body<T, OP, false, 1>(it, b, sl);
 }
 
@@ -155,7 +140,10 @@ __device__ __forceinline__ void multi_ops(const KMultiItem *__restrict__ it, uin
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_multi(const KMulti m) {
+#ifndef RDX_MULTI_WAVES
+#define RDX_MULTI_WAVES 5   // >= 5 waves per SIMD: <= 102 VGPRs (the heaviest body needs 95)
+#endif
+__global__ __launch_bounds__(kBlock, RDX_MULTI_WAVES) void k_multi(const KMulti m) {
     __shared__ MultiShared s_req;
     const uint32_t item = m.blk2item[blockIdx.x];
     const KMultiItem *__restrict__ it = m.items + item;

@@ -60,7 +60,7 @@ struct Tuning {
 #endif
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
-    int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 4);   // k_multi fill target
+    int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
 };
 
 const Tuning &tuning() {
@@ -108,7 +108,7 @@ struct rdx_workspace {
     uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
     // heterogeneous batches (k_multi): request table + block map, staged through a ring of slots so
     // that call i+1's upload (on copy_stream) overlaps call i's kernel instead of queueing behind it
-    static constexpr int kTableSlots = 4;
+    static constexpr int kTableSlots = 32;
     struct TableSlot {
         uint8_t *dev = nullptr, *host = nullptr;   // device table / its page-locked staging
         size_t dev_cap = 0, host_cap = 0;
@@ -184,8 +184,8 @@ rdx_status upload(rdx_workspace *ws, void *dst, const void *src, size_t bytes, s
 // A per-call table (k_multi's request table + block map) into device memory without putting the copy
 // engine's latency between two kernels of the stream: the copy runs on the workspace's copy stream
 // (overlapping whatever `s` is still executing) and `s` waits for it with an event; a ring of slots
-// keeps the tables of the calls in flight intact (a slot is reused once the kernel that read it, four
-// calls ago, has completed).  Call table_consumed() right after the launch that reads *dev.
+// keeps the tables of the calls in flight intact (a slot is reused once the kernel that read it,
+// kTableSlots calls ago, has completed).  Call table_consumed() right after the launch that reads *dev.
 rdx_status stage_table(rdx_workspace *ws, const uint8_t *src, size_t bytes, hipStream_t s, const uint8_t **dev,
                        rdx_workspace::TableSlot **slot) {
     if (!ws->copy_stream) RDX_HIP(hipStreamCreateWithFlags(&ws->copy_stream, hipStreamNonBlocking));
@@ -1117,7 +1117,10 @@ rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_mul
         }
         const bool all = (p.mode == Mode::AllStrided && p.all_strided.view.ndim <= 4) ||   // k_multi.hip kMultiDims
                          (p.mode == Mode::AllContig && p.all_contig.n < (1ull << 32) && p.all_contig.n > 0);
-        if (!all || !p.unfused_es.empty() || !p.miss_list.empty() || table.size() >= 0xffffffffull ||
+        // byte-shuffled chunks (fused unshuffle) run as their own launches: the plane-transposing
+        // k_all_contig serves them far better than per-element byte gathers, and k_multi's register
+        // budget (its heaviest body sets every workgroup's occupancy) stays that of plain loads
+        if (!all || p.fused || !p.unfused_es.empty() || !p.miss_list.empty() || table.size() >= 0xffffffffull ||
             blocks >= (1ull << 30)) {
             rest.push_back(i);
             continue;
@@ -1137,6 +1140,12 @@ rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_mul
             a.view.vstride[0] = 1;
             a.view.rstride[0] = c.rs;
             a.filter_semantics = c.filter_semantics;
+        }
+        for (int k = a.view.ndim; k < 4; ++k) {   // k_multi.hip reads kMultiDims = 4 dims
+            a.view.count[k] = 1;
+            a.view.div[k] = make_div(1);
+            a.view.vstride[k] = 0;
+            a.view.rstride[k] = 0;
         }
         a.src.base = static_cast<const uint8_t *>(it.d_chunk);
         a.src.ptrs = nullptr;
@@ -1159,7 +1168,7 @@ rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_mul
     }
     rdx_status st;
     if (!table.empty()) {
-        // One residency round of the chip (4 k_multi workgroups per CU) serves the whole batch: a batch
+        // One residency round of the chip (5 k_multi workgroups per CU) serves the whole batch: a batch
         // that wants more gets proportionally fewer, longer-running workgroups per request (each lane
         // keeps 4-8 loads in flight per step), so no request pays several dispatch + hand-off rounds.
         const uint64_t target = (uint64_t)ws->cus * tuning().multi_blocks_per_cu;

@@ -1,0 +1,28 @@
+"""The host code under AddressSanitizer + UndefinedBehaviorSanitizer: the product planner
+(rdx_plan.cpp) and the oracle built with -fsanitize=address,undefined -fno-sanitize-recover=all, driven
+by tests/cpp/test_sanitize.cpp (random requests planner-vs-oracle, inflate on corrupted streams).  Any
+sanitizer report fails the run."""
+import os
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+SRCS = [ROOT / "tests" / "cpp" / "test_sanitize.cpp", ROOT / "reductionist-rs_amd" / "csrc" / "rdx_plan.cpp",
+        ROOT / "oracle" / "rdx_oracle.cpp", ROOT / "oracle" / "oracle_inflate.cpp"]
+DEPS = SRCS + [ROOT / "include" / "rdx.h", ROOT / "reductionist-rs_amd" / "csrc" / "rdx_plan.hpp",
+               ROOT / "reductionist-rs_amd" / "csrc" / "rdx_kdesc.h"]
+
+
+def _binary():
+    out = ROOT / "tests" / "cpp" / "build" / "test_sanitize"
+    if not out.exists() or out.stat().st_mtime < max(p.stat().st_mtime for p in DEPS):
+        out.parent.mkdir(exist_ok=True)
+        subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                        "-fno-omit-frame-pointer", *map(str, SRCS), "-o", str(out)], check=True)
+    return out
+
+
+def test_planner_and_oracle_under_asan_ubsan():
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(_binary()), "4000"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0 and "sanitize: ok" in r.stdout, (r.stdout + r.stderr)[-4000:]

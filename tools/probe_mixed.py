@@ -18,7 +18,7 @@ class A:
 def main():
     import torch.distributed as dist
     cx = bench.Ctx(torch, dist, A(), 1, 0, 0)
-    print(json.dumps(bench.leg_mixed(cx, k=int(sys.argv[1]) if len(sys.argv) > 1 else 50)), flush=True)
+    print(json.dumps(bench.leg_mixed(cx, k=int(sys.argv[1]) if len(sys.argv) > 1 else 30)), flush=True)
 
 
 if __name__ == "__main__":
