@@ -24,6 +24,8 @@ extra (every number DESIGN.md quotes comes from here):
   c4z_inflate            the batch compressed with zlib, decompressed on the device
   configs                (N=1) device-resident C1, C3 (min / max / valid_range) and C5 select launches
   mixed_requests         (N=1) 20 mixed C1/C3 requests in ONE heterogeneous launch (rdx_execute_multi_device)
+  concurrent_native      (N=1) C1 / C2 / C3 requests from native C++ threads (rdx_conc_bench: own workspace
+                         and stream per thread, execute + synchronize per request, no Python on the path)
   host_inclusive         (N=1) C2 / C3 / C5 through rdx_execute from pageable and pinned host memory,
                          next to the raw PCIe copy time of the same bytes
   cpu_baselines          (N=1) the oracle (CPU restatement of the reference path) on host cores: C1 with
@@ -594,7 +596,7 @@ def leg_configs(cx):
     return out
 
 
-def leg_mixed(cx, n_pairs=10, sets=2, k=30):
+def leg_mixed(cx, n_pairs=10, sets=2, k=30, serial=True):
     """20 mixed requests — 10 x C1 (f32 4 MiB contiguous sum) and 10 x C3 (f64 [128,128,128] hyperslab
     min / max, missing_value) — as ONE heterogeneous launch (rdx_execute_multi_device), rotating over
     `sets` distinct sets of chunks (> the Infinity Cache).  Device time: the k calls are queued behind a
@@ -648,6 +650,15 @@ def leg_mixed(cx, n_pairs=10, sets=2, k=30):
         assert all(int(kk[4][0]) == 0 for kk in keep)
         assert all(int(kk[3][0]) == (1 << 20) for kk in keep[0::2])
         assert all(int(kk[3][0]) > 0 for kk in keep[1::2])
+    res = {"workload": f"{n} mixed requests per launch: {n_pairs} x C1 (f32 4 MiB sum) + {n_pairs} x C3 "
+                       "(f64 hyperslab min/max, missing_value), each its own request; rdx_execute_multi_device",
+           "us_per_launch": round(t * 1e6, 2), "us_per_request": round(t / n * 1e6, 3),
+           "bytes_alg_per_launch": alg, "roofline_frac": round(alg / t / 1e9 / PEAK_GBS, 4),
+           "host_us_per_call": round(host * 1e6, 1),
+           "timing": f"{k} calls queued behind a device-side gate; HIP events gate open -> last kernel end / {k} "
+                     "(table uploads overlap on the copy stream)"}
+    if not serial:
+        return res
     flat = [kk for _, _, _, keep in sets_c for kk in keep]
     sargs = [(cx.ws.ws, kk[0].ref, C.c_void_p(kk[1].data_ptr()), kk[1].numel() * kk[1].element_size(),
               C.c_void_p(kk[2].data_ptr()), C.c_void_p(kk[3].data_ptr()), C.c_void_p(kk[4].data_ptr()), cx.sh,
@@ -660,15 +671,28 @@ def leg_mixed(cx, n_pairs=10, sets=2, k=30):
 
     ts, _ = gated(serial_step, 4 * n, 0.01 + 4 * n * 50e-6)
     ts *= n
-    return {"workload": f"{n} mixed requests per launch: {n_pairs} x C1 (f32 4 MiB sum) + {n_pairs} x C3 "
-                        "(f64 hyperslab min/max, missing_value), each its own request; rdx_execute_multi_device",
-            "us_per_launch": round(t * 1e6, 2), "us_per_request": round(t / n * 1e6, 3),
-            "bytes_alg_per_launch": alg, "roofline_frac": round(alg / t / 1e9 / PEAK_GBS, 4),
-            "host_us_per_call": round(host * 1e6, 1),
-            "serial_single_launches_us": round(ts * 1e6, 2),
-            "serial_roofline_frac": round(alg / ts / 1e9 / PEAK_GBS, 4),
-            "timing": f"{k} calls queued behind a device-side gate; HIP events gate open -> last kernel end / {k} "
-                      "(table uploads overlap on the copy stream)"}
+    res.update({"serial_single_launches_us": round(ts * 1e6, 2),
+                "serial_roofline_frac": round(alg / ts / 1e9 / PEAK_GBS, 4)})
+    return res
+
+
+def leg_native_concurrent(cx):
+    """Concurrent single-chunk requests from native C++ threads (reductionist-rs_amd/rdx_conc_bench: each
+    thread its own workspace + stream, rdx_execute_device + synchronize per request, the way Tokio/Rayon
+    workers run requests, app.rs:147-152), 1 thread and the worker-pool size (num_cpus - 1, capped at the
+    box's CPU share)."""
+    exe = ROOT / "reductionist-rs_amd" / "rdx_conc_bench"
+    if not exe.exists():
+        return {"skipped": f"{exe} not built"}
+    out = []
+    pool = pool_threads()
+    for cfg, threads, reqs in (("c3", 1, 2000), ("c3", pool, 2000), ("c1", 1, 2000), ("c1", pool, 2000),
+                               ("c2", 1, 300), ("c2", 4, 300)):
+        r = subprocess.run([str(exe), cfg, str(threads), str(reqs)], capture_output=True, text=True, timeout=120)
+        if r.returncode != 0:
+            raise RuntimeError(f"rdx_conc_bench {cfg} {threads}: {r.stderr[-500:]}")
+        out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    return out
 
 
 def leg_host(cx):
@@ -888,6 +912,7 @@ def main():
     if world == 1 and not args.no_configs:
         extra["configs"] = leg_configs(cx)
         extra["mixed_requests"] = leg_mixed(cx)
+        extra["concurrent_native"] = leg_native_concurrent(cx)
     if world == 1 and not args.no_host:
         extra["host_inclusive"] = leg_host(cx)
     cpu_line = None
