@@ -119,23 +119,46 @@ struct KAxis {
                         // slice only publishes and k_axis_cols_fold folds (a wave per output) next
 };
 
-// One request of a heterogeneous batch (k_multi.hip): an all-axes reduction over its own view, with
-// its own dtype / op / source / missing / outputs; `a.out.partials` / `a.out.tickets` point at this
-// request's slice of the workspace's hand-off buffers.
-struct KMultiItem {
-    KAllStrided a;
-    uint32_t dtype;     // rdx_dtype
-    uint32_t op;        // OpCode (COUNT / MAX / MIN / SUM)
-    uint32_t block0;    // first grid block of this request
-    uint32_t pad;
+// One request of a heterogeneous batch (k_multi.hip): an all-axes reduction over its own view of at
+// most kMultiDims dims, with its own dtype / op / source / missing predicate / outputs.  Compact (152 B)
+// so that a whole batch travels in the launch's kernel arguments: no table upload, no copy-engine or
+// cross-stream event between the host call and the kernel.
+constexpr int kMultiDims = 4;
+constexpr int kMultiMaxItems = 24;   // requests per launch (the kernel arguments stay under 4 KiB)
+enum : uint8_t {                     // KMultiReq::flags
+    kMultiEq0 = 1,                   // x == v0 is missing  (MISSING_VALUE, MISSING_VALUES[0])
+    kMultiEq1 = 2,                   // x == v1 is missing  (MISSING_VALUES[1])
+    kMultiLo = 4,                    // x < v0 is missing   (VALID_MIN, VALID_RANGE)
+    kMultiHi = 8,                    // x > v1 is missing   (VALID_MAX, VALID_RANGE)
+    kMultiFilt = 16,                 // Count(All) semantics: NaN excluded under a valid_* predicate
+    kMultiBswap = 32,                // non-native byte order
 };
+struct KMultiReq {
+    const uint8_t *base;             // the request's chunk
+    uint8_t *body;
+    int64_t *counts;
+    uint32_t *status;                // may be NULL
+    int64_t base_off, r0;            // view origin (elements) and its rank
+    uint64_t v0, v1;                 // predicate operands (bit patterns of T)
+    uint64_t magic[kMultiDims - 1];  // Div::magic of count[0..2] (the outermost index needs no division)
+    int32_t vstride[kMultiDims];     // element strides, innermost first (dims >= ndim: 0)
+    int32_t rstride[kMultiDims];     // rank strides
+    uint32_t count[kMultiDims - 1];  // dim extents, innermost first
+    uint32_t n;                      // elements in the view (< 2^32)
+    uint32_t block0;                 // first grid block of this request
+    uint32_t bpc;                    // its blocks
+    uint8_t dtype, op, vec, ndim;    // rdx_dtype, OpCode, elements per 16-B lane load (1 = scalar), dims
+    uint8_t flags, pad8[3];
+};
+static_assert(sizeof(KMultiReq) == 152, "KMultiReq layout");
 
-struct KMulti {
-    const KMultiItem *items;   // device table, one per request
-    const uint32_t *blk2item;  // device, one entry per grid block
-    uint32_t n_items;
-    uint32_t pad;
+struct KMultiArgs {
+    uint64_t *partials;              // hand-off records: request k's block b at (block0 + b) * kRecordU64
+    uint32_t *tickets;               // request k's arrival counters at k * kTicketWords
+    uint32_t n_items, epoch;
+    KMultiReq req[kMultiMaxItems];
 };
+static_assert(sizeof(KMultiArgs) <= 4096, "k_multi arguments exceed 4 KiB");
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]
 // (operations.rs:188-210, :58-67).  out index g -> element offset via `view` (dims

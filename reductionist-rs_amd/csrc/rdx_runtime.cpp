@@ -106,17 +106,6 @@ struct rdx_workspace {
     DevBuf<uint8_t> raw;
     std::vector<uint8_t> last_zptrs, last_zlens;
     uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
-    // heterogeneous batches (k_multi): request table + block map, staged through a ring of slots so
-    // that call i+1's upload (on copy_stream) overlaps call i's kernel instead of queueing behind it
-    static constexpr int kTableSlots = 32;
-    struct TableSlot {
-        uint8_t *dev = nullptr, *host = nullptr;   // device table / its page-locked staging
-        size_t dev_cap = 0, host_cap = 0;
-        hipEvent_t copied = nullptr, consumed = nullptr;
-        bool used = false;
-    } tables[kTableSlots];
-    uint32_t table_next = 0;
-    hipStream_t copy_stream = nullptr;
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
     hipEvent_t piece_ev[8] = {};
@@ -181,56 +170,10 @@ rdx_status upload(rdx_workspace *ws, void *dst, const void *src, size_t bytes, s
     return RDX_OK;
 }
 
-// A per-call table (k_multi's request table + block map) into device memory without putting the copy
-// engine's latency between two kernels of the stream: the copy runs on the workspace's copy stream
-// (overlapping whatever `s` is still executing) and `s` waits for it with an event; a ring of slots
-// keeps the tables of the calls in flight intact (a slot is reused once the kernel that read it,
-// kTableSlots calls ago, has completed).  Call table_consumed() right after the launch that reads *dev.
-rdx_status stage_table(rdx_workspace *ws, const uint8_t *src, size_t bytes, hipStream_t s, const uint8_t **dev,
-                       rdx_workspace::TableSlot **slot) {
-    if (!ws->copy_stream) RDX_HIP(hipStreamCreateWithFlags(&ws->copy_stream, hipStreamNonBlocking));
-    rdx_workspace::TableSlot &t = ws->tables[ws->table_next++ % rdx_workspace::kTableSlots];
-    if (!t.copied) RDX_HIP(hipEventCreateWithFlags(&t.copied, hipEventDisableTiming));
-    if (!t.consumed) RDX_HIP(hipEventCreateWithFlags(&t.consumed, hipEventDisableTiming));
-    if (t.used) {
-        RDX_HIP(hipEventSynchronize(t.consumed));
-        t.used = false;
-    }
-    if (t.host_cap < bytes) {
-        if (t.host) RDX_HIP(hipHostFree(t.host));
-        t.host = nullptr;
-        t.host_cap = 0;
-        const size_t want = std::max(bytes, (size_t)65536);
-        RDX_HIP(hipHostMalloc((void **)&t.host, want, hipHostMallocDefault));
-        t.host_cap = want;
-    }
-    if (t.dev_cap < bytes) {
-        if (t.dev) RDX_HIP(hipFree(t.dev));
-        t.dev = nullptr;
-        t.dev_cap = 0;
-        const size_t want = std::max(bytes, (size_t)65536);
-        RDX_HIP(hipMalloc((void **)&t.dev, want));
-        t.dev_cap = want;
-    }
-    std::memcpy(t.host, src, bytes);
-    RDX_HIP(hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, ws->copy_stream));
-    RDX_HIP(hipEventRecord(t.copied, ws->copy_stream));
-    RDX_HIP(hipStreamWaitEvent(s, t.copied, 0));
-    *dev = t.dev;
-    *slot = &t;
-    return RDX_OK;
-}
-
 rdx_status ensure_aux(rdx_workspace *ws) {
     if (!ws->aux_stream) RDX_HIP(hipStreamCreateWithFlags(&ws->aux_stream, hipStreamNonBlocking));
     for (hipEvent_t &e : ws->piece_ev)
         if (!e) RDX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    return RDX_OK;
-}
-
-rdx_status table_consumed(rdx_workspace::TableSlot *t, hipStream_t s) {
-    RDX_HIP(hipEventRecord(t->consumed, s));
-    t->used = true;
     return RDX_OK;
 }
 
@@ -636,15 +579,6 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->zout_len.p);
     fr(ws->zerr.p);
     fr(ws->raw.p);
-    if (ws->copy_stream) (void)hipStreamSynchronize(ws->copy_stream);
-    for (auto &t : ws->tables) {
-        if (t.used) (void)hipEventSynchronize(t.consumed);
-        fr(t.dev);
-        if (t.host) (void)hipHostFree(t.host);
-        if (t.copied) (void)hipEventDestroy(t.copied);
-        if (t.consumed) (void)hipEventDestroy(t.consumed);
-    }
-    if (ws->copy_stream) (void)hipStreamDestroy(ws->copy_stream);
     if (ws->aux_stream) {
         (void)hipStreamSynchronize(ws->aux_stream);
         (void)hipStreamDestroy(ws->aux_stream);
@@ -1091,23 +1025,126 @@ rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req, u
                       static_cast<uint8_t *>(d_bodies), d_counts, d_status, static_cast<hipStream_t>(stream));
 }
 
+namespace {
+
+bool fits_i32(int64_t v) { return v >= INT32_MIN && v <= INT32_MAX; }
+
+// A planned all-axes request as a k_multi descriptor; false when it runs as its own launch instead.
+// Byte-shuffled chunks (fused unshuffle) stay out: the plane-transposing k_all_contig serves them far
+// better than per-element byte gathers, and k_multi's register budget (its heaviest body sets every
+// workgroup's occupancy) stays that of plain loads.
+bool multi_req(const ExecPlan &p, const rdx_multi_item &it, KMultiReq &q) {
+    if (p.fused || !p.unfused_es.empty() || !p.miss_list.empty()) return false;
+    KView v{};
+    uint32_t filt = 0;
+    if (p.mode == Mode::AllStrided && p.all_strided.view.ndim <= kMultiDims && p.all_strided.view.ndim >= 1) {
+        v = p.all_strided.view;
+        filt = p.all_strided.filter_semantics;
+    } else if (p.mode == Mode::AllContig && p.all_contig.n > 0 && p.all_contig.n < (1ull << 32)) {
+        const KAllContig &c = p.all_contig;
+        v.ndim = 1;
+        v.base_off = (int64_t)c.off;
+        v.r0 = c.r0;
+        v.n = c.n;
+        v.count[0] = (uint32_t)c.n;
+        v.vstride[0] = 1;
+        v.rstride[0] = c.rs;
+        filt = c.filter_semantics;
+    } else {
+        return false;
+    }
+    if (v.n == 0 || v.n >= (1ull << 31)) return false;   // k_multi's 32-bit index arithmetic
+    const KMissing &m = p.miss;
+    if (m.kind == RDX_MISSING_VALUES && m.n > 2) return false;   // longer lists: k_all_strided's list scan
+    q = KMultiReq{};
+    for (int k = 0; k < kMultiDims; ++k) {
+        const bool real = k < v.ndim;
+        if (real && (!fits_i32(v.vstride[k]) || !fits_i32(v.rstride[k]))) return false;
+        q.vstride[k] = real ? (int32_t)v.vstride[k] : 0;
+        q.rstride[k] = real ? (int32_t)v.rstride[k] : 0;
+        if (k < kMultiDims - 1) {
+            q.count[k] = real ? v.count[k] : 1u;
+            q.magic[k] = make_div(q.count[k]).magic;
+        }
+    }
+    q.base = static_cast<const uint8_t *>(it.d_chunk);
+    q.body = static_cast<uint8_t *>(it.d_body);
+    q.counts = it.d_counts;
+    q.status = it.d_status;
+    q.base_off = v.base_off;
+    q.r0 = v.r0;
+    q.n = (uint32_t)v.n;
+    q.dtype = (uint8_t)p.dtype;
+    q.op = (uint8_t)p.op;
+    q.ndim = (uint8_t)v.ndim;
+    q.vec = (uint8_t)vec_width(v, p.esz, q.base, nullptr, 1, false);
+    uint8_t f = p.bswap ? kMultiBswap : 0;
+    if (filt) f |= kMultiFilt;
+    switch (m.kind) {
+        case RDX_MISSING_VALUE: f |= kMultiEq0; q.v0 = m.v0; break;
+        case RDX_MISSING_VALUES:
+            if (m.n >= 1) { f |= kMultiEq0; q.v0 = m.inl[0]; }
+            if (m.n >= 2) { f |= kMultiEq1; q.v1 = m.inl[1]; }
+            break;
+        case RDX_MISSING_VALID_MIN: f |= kMultiLo; q.v0 = m.v0; break;
+        case RDX_MISSING_VALID_MAX: f |= kMultiHi; q.v1 = m.v0; break;
+        case RDX_MISSING_VALID_RANGE: f |= kMultiLo | kMultiHi; q.v0 = m.v0; q.v1 = m.v1; break;
+        default: break;
+    }
+    q.flags = f;
+    // workgroups for one load round trip per lane (scaled down when the launch overfills the chip)
+    const uint64_t per_block = (uint64_t)kBlock * (q.vec > 1 ? 4 : 8);
+    q.bpc = (uint32_t)std::max<uint64_t>(1, (v.n / q.vec + per_block - 1) / per_block);
+    return true;
+}
+
+// One k_multi launch over reqs[0..n): one residency round of the chip (5 workgroups per CU) serves the
+// whole launch; a launch that wants more gets proportionally fewer, longer-running workgroups per request
+// (each lane keeps 4-8 loads in flight per step), so no request pays several dispatch + hand-off rounds.
+rdx_status launch_multi_group(rdx_workspace *ws, const KMultiReq *reqs, uint32_t n, hipStream_t s) {
+    KMultiArgs args;
+    args.n_items = n;
+    const uint64_t target = (uint64_t)ws->cus * tuning().multi_blocks_per_cu;
+    uint64_t want = 0;
+    for (uint32_t k = 0; k < n; ++k) want += std::min<uint64_t>(reqs[k].bpc, (uint64_t)ws->cus * 8);
+    const double scale = want > target ? (double)target / (double)want : 1.0;
+    uint64_t blocks = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        KMultiReq &q = args.req[k];
+        q = reqs[k];
+        q.bpc = (uint32_t)std::max<double>(1.0, std::ceil(std::min<uint64_t>(q.bpc, (uint64_t)ws->cus * 8) * scale));
+        q.block0 = (uint32_t)blocks;
+        blocks += q.bpc;
+    }
+    rdx_status st;
+    if ((st = ensure(ws, ws->partials, blocks * kRecordU64, s, true))) return st;
+    if ((st = ensure(ws, ws->tickets, (uint64_t)n * kTicketWords, s, true))) return st;
+    if ((st = next_epoch(ws, s, args.epoch))) return st;
+    args.partials = ws->partials.p;
+    args.tickets = ws->tickets.p;
+    RDX_HIP(launch_multi(args, (uint32_t)blocks, s));
+    return RDX_OK;
+}
+
+}  // namespace
+
 rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_multi_item *items, void *stream,
                                     uint32_t *statuses, rdx_response_info *infos) {
     if (!ws || (n && (!items || !statuses))) return RDX_E_INVALID_ARGUMENT;
     if (n == 0) return RDX_OK;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     RDX_HIP(hipSetDevice(ws->device));
-    std::vector<KMultiItem> table;
-    std::vector<uint32_t> blk2item;
+    KMultiReq group[kMultiMaxItems];
+    uint32_t in_group = 0;
     std::vector<uint64_t> rest;   // requests that run as their own launches
-    uint64_t blocks = 0;
+    rdx_status st;
     for (uint64_t i = 0; i < n; ++i) {
         const rdx_multi_item &it = items[i];
         statuses[i] = RDX_E_INVALID_ARGUMENT;
         if (!it.req) continue;
         if (it.req->compression != RDX_COMPRESSION_NONE) continue;
         ExecPlan p;
-        const rdx_status st = make_plan(*it.req, it.chunk_len, p);
+        st = make_plan(*it.req, it.chunk_len, p);
         statuses[i] = st;
         if (st) continue;
         if (infos) infos[i] = p.info;
@@ -1115,102 +1152,16 @@ rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_mul
             statuses[i] = RDX_E_INVALID_ARGUMENT;
             continue;
         }
-        const bool all = (p.mode == Mode::AllStrided && p.all_strided.view.ndim <= 4) ||   // k_multi.hip kMultiDims
-                         (p.mode == Mode::AllContig && p.all_contig.n < (1ull << 32) && p.all_contig.n > 0);
-        // byte-shuffled chunks (fused unshuffle) run as their own launches: the plane-transposing
-        // k_all_contig serves them far better than per-element byte gathers, and k_multi's register
-        // budget (its heaviest body sets every workgroup's occupancy) stays that of plain loads
-        if (!all || p.fused || !p.unfused_es.empty() || !p.miss_list.empty() || table.size() >= 0xffffffffull ||
-            blocks >= (1ull << 30)) {
+        if (!multi_req(p, it, group[in_group])) {
             rest.push_back(i);
             continue;
         }
-        KMultiItem m{};
-        KAllStrided &a = m.a;
-        if (p.mode == Mode::AllStrided) {
-            a = p.all_strided;
-        } else {
-            const KAllContig &c = p.all_contig;
-            a.view.ndim = 1;
-            a.view.base_off = (int64_t)c.off;
-            a.view.r0 = c.r0;
-            a.view.n = c.n;
-            a.view.count[0] = (uint32_t)c.n;
-            a.view.div[0] = make_div((uint32_t)c.n);
-            a.view.vstride[0] = 1;
-            a.view.rstride[0] = c.rs;
-            a.filter_semantics = c.filter_semantics;
+        if (++in_group == (uint32_t)kMultiMaxItems) {
+            if ((st = launch_multi_group(ws, group, in_group, s))) return st;
+            in_group = 0;
         }
-        for (int k = a.view.ndim; k < 4; ++k) {   // k_multi.hip reads kMultiDims = 4 dims
-            a.view.count[k] = 1;
-            a.view.div[k] = make_div(1);
-            a.view.vstride[k] = 0;
-            a.view.rstride[k] = 0;
-        }
-        a.src.base = static_cast<const uint8_t *>(it.d_chunk);
-        a.src.ptrs = nullptr;
-        a.src.plane = it.chunk_len / p.esz;
-        a.src.fused = p.fused;
-        a.src.bswap = p.bswap;
-        a.miss = p.miss;
-        a.vec = vec_width(a.view, p.esz, a.src.base, nullptr, 1, p.fused);
-        // workgroups for one load round trip per lane (scaled down below when the batch overfills the chip)
-        const uint64_t per_block = (uint64_t)kBlock * (a.vec > 1 ? 4 : 8);
-        const uint64_t want = (a.view.n / a.vec + per_block - 1) / per_block;
-        a.blocks_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ws->cus * 8));
-        a.out.body = static_cast<uint8_t *>(it.d_body);
-        a.out.counts = it.d_counts;
-        a.out.status = it.d_status;
-        m.dtype = p.dtype;
-        m.op = p.op;
-        blocks += a.blocks_per_chunk;
-        table.push_back(m);
     }
-    rdx_status st;
-    if (!table.empty()) {
-        // One residency round of the chip (5 k_multi workgroups per CU) serves the whole batch: a batch
-        // that wants more gets proportionally fewer, longer-running workgroups per request (each lane
-        // keeps 4-8 loads in flight per step), so no request pays several dispatch + hand-off rounds.
-        const uint64_t target = (uint64_t)ws->cus * tuning().multi_blocks_per_cu;
-        if (blocks > target) {
-            const double scale = (double)target / (double)blocks;
-            blocks = 0;
-            for (KMultiItem &m : table) {
-                m.a.blocks_per_chunk = (uint32_t)std::max<double>(1.0, std::ceil(m.a.blocks_per_chunk * scale));
-                blocks += m.a.blocks_per_chunk;
-            }
-        }
-        blk2item.reserve(blocks);
-        blocks = 0;
-        for (size_t k = 0; k < table.size(); ++k) {
-            table[k].block0 = (uint32_t)blocks;
-            blk2item.insert(blk2item.end(), table[k].a.blocks_per_chunk, (uint32_t)k);
-            blocks += table[k].a.blocks_per_chunk;
-        }
-        if ((st = ensure(ws, ws->partials, blocks * kRecordU64, s, true))) return st;
-        if ((st = ensure(ws, ws->tickets, table.size() * kTicketWords, s, true))) return st;
-        uint32_t epoch = 0;
-        if ((st = next_epoch(ws, s, epoch))) return st;
-        for (size_t k = 0; k < table.size(); ++k) {
-            KOut &o = table[k].a.out;
-            o.partials = ws->partials.p + (uint64_t)table[k].block0 * kRecordU64;
-            o.tickets = ws->tickets.p + k * kTicketWords;
-            o.epoch = epoch;
-        }
-        const size_t tbytes = table.size() * sizeof(KMultiItem), mbytes = blk2item.size() * sizeof(uint32_t);
-        std::vector<uint8_t> host(tbytes + mbytes);
-        std::memcpy(host.data(), table.data(), tbytes);
-        std::memcpy(host.data() + tbytes, blk2item.data(), mbytes);
-        const uint8_t *dev = nullptr;
-        rdx_workspace::TableSlot *slot = nullptr;
-        if ((st = stage_table(ws, host.data(), host.size(), s, &dev, &slot))) return st;
-        KMulti km{};
-        km.items = reinterpret_cast<const KMultiItem *>(dev);
-        km.blk2item = reinterpret_cast<const uint32_t *>(dev + tbytes);
-        km.n_items = (uint32_t)table.size();
-        RDX_HIP(launch_multi(km, (uint32_t)blocks, s));
-        if ((st = table_consumed(slot, s))) return st;
-    }
+    if (in_group && (st = launch_multi_group(ws, group, in_group, s))) return st;
     for (uint64_t i : rest) {
         const rdx_multi_item &it = items[i];
         ExecPlan p;
