@@ -656,7 +656,7 @@ def leg_mixed(cx, n_pairs=10, sets=2, k=30, serial=True):
            "bytes_alg_per_launch": alg, "roofline_frac": round(alg / t / 1e9 / PEAK_GBS, 4),
            "host_us_per_call": round(host * 1e6, 1),
            "timing": f"{k} calls queued behind a device-side gate; HIP events gate open -> last kernel end / {k} "
-                     "(table uploads overlap on the copy stream)"}
+                     "(the request descriptors travel in the kernel arguments)"}
     if not serial:
         return res
     flat = [kk for _, _, _, keep in sets_c for kk in keep]
