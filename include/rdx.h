@@ -261,10 +261,12 @@ typedef struct rdx_multi_item {
 
 /* Many independent requests on one stream — the request-level concurrency of src/app.rs:147-152
  * (every HTTP request is its own operation<T>() call) folded into as few launches as possible: every
- * all-axes request (axis unset) whose filters fuse (at most filters[0] with element_size == sizeof(T))
- * and whose missing_values list has at most 16 entries runs in ONE heterogeneous launch (k_multi), each
- * with its own dtype, op, view, byte order and missing predicate; the others (axis reductions, select,
- * axis = [], filter chains, long missing lists) run as their own launches on the same stream, after it.
+ * all-axes request (axis unset) over an unshuffled chunk (no filters) whose view has < 2^31 elements
+ * in at most 4 canonical dims and whose missing_values list has at most 2 entries runs in a
+ * heterogeneous launch (k_multi, up to 24 requests per launch, their descriptors in the kernel
+ * arguments), each with its own dtype, op, view, byte order and missing predicate; the others (axis
+ * reductions, select, axis = [], shuffled chunks, longer missing lists) run as their own launches on
+ * the same stream, after them.
  * statuses[i] (HOST, n entries) receives request i's planning status — an invalid request does not stop
  * the others; infos[i] (HOST, may be NULL) its response shape and sizes.  Compressed requests are
  * refused per item (RDX_E_INVALID_ARGUMENT): decompress them first (rdx_decompress_batch_device).
