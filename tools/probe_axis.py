@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Axis-reduction probe: event time per launch for a set of axis configs under this process's
-tuning environment (tools/sweep_axis.sh runs it once per setting).  One JSON line per config."""
+tuning environment (run it once per setting).  One JSON line per config."""
 import ctypes as C
 import json
 import os

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Latency probe for small single-chunk launches (C1, C3 and a C3-sized contiguous run): event time
-per launch over K back-to-back launches, for the RDX_FORCE_BPC of this process (tools/sweep_small.sh
-runs it once per setting).  One JSON line per config."""
+per launch over K back-to-back launches, for the RDX_FORCE_BPC of this process (run it
+once per setting).  One JSON line per config."""
 import ctypes as C
 import json
 import os
