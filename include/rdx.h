@@ -286,6 +286,30 @@ rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, 
                                        void *d_out, uint64_t out_capacity,
                                        uint64_t *d_out_lens, uint32_t *d_errors, void *stream);
 
+/* ---- response serialisation ------------------------------------------------------------------- *
+ * The HTTP body of a successful request: serde_cbor::to_vec(&CBORResponse::new(&response))
+ * (src/app.rs:33-40, src/models.rs:355-416, serde_cbor 0.11.2): a CBOR map of 7 entries in field order
+ * bytes, dtype, shape, shape_as_bytes, count, count_as_bytes, byte_order; integers in their shortest
+ * form; `option_shape_as_bytes` / `option_count_as_bytes` move shape / count into native-endian u64 /
+ * i64 byte strings and leave empty arrays (models.rs:379-401).  A large count vector (an axis reduction
+ * with many outputs, axis = []) is encoded where it was computed: rdx_cbor_encode_device packs the
+ * device-resident body and counts into the CBOR body on the device (one pass over the counts: a
+ * decoupled look-back scan of the per-count encoded lengths), so only the packed response crosses PCIe. */
+#define RDX_CBOR_SHAPE_AS_BYTES 1u   /* RequestData.option_shape_as_bytes (models.rs:173) */
+#define RDX_CBOR_COUNT_AS_BYTES 2u   /* RequestData.option_count_as_bytes (models.rs:175) */
+/* Upper bound of the encoded size (every count at its longest, 9 bytes). */
+uint64_t rdx_cbor_bound(const rdx_response_info *info, uint32_t flags);
+/* Host buffers in, host buffer out; *out_len = bytes written.  RDX_E_BUFFER_TOO_SMALL when out_cap is
+ * short of the exact size (then *out_len = the size needed). */
+rdx_status rdx_cbor_encode(const rdx_response_info *info, const void *body, const int64_t *counts, uint32_t flags,
+                           void *out, uint64_t out_cap, uint64_t *out_len);
+/* Device buffers in (e.g. rdx_execute_device's outputs), device buffer out (>= rdx_cbor_bound bytes),
+ * asynchronous on `stream`: *d_out_len (device u64) receives the encoded length, *d_status (device
+ * word, may be NULL) 0 or RDX_E_DEVICE. */
+rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *info, const void *d_body,
+                                  const int64_t *d_counts, uint32_t flags, void *d_out, uint64_t out_cap,
+                                  uint64_t *d_out_len, uint32_t *d_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

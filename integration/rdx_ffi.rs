@@ -19,6 +19,9 @@
 //!                                     new: device-resident, batched and heterogeneous entry points
 //!   rdx_decompress_batch_device       compression.rs:18-27 `decompress` for a batch of device streams
 //!   rdx_inflate_last_error / _string  the detail of RDX_E_DECOMPRESSION (error.rs:33-41)
+//!   rdx_cbor_bound / _encode / _encode_device
+//!                                     app.rs:33-40 `serde_cbor::to_vec(&CBORResponse::new(&self))`
+//!                                     (models.rs:355-416), host or device-resident outputs
 
 #![allow(non_camel_case_types, dead_code)]
 
@@ -27,6 +30,9 @@ use std::os::raw::{c_char, c_int, c_void};
 
 pub const RDX_ABI_VERSION: u32 = 1;
 pub const RDX_MAX_NDIM: usize = 32;
+/// rdx_cbor_* flags: RequestData.option_shape_as_bytes / option_count_as_bytes (models.rs:173-175)
+pub const RDX_CBOR_SHAPE_AS_BYTES: u32 = 1;
+pub const RDX_CBOR_COUNT_AS_BYTES: u32 = 2;
 
 /// `rdx_status` (include/rdx.h).
 pub mod status {
@@ -205,6 +211,28 @@ extern "C" {
         out_capacity: u64,
         d_out_lens: *mut u64,
         d_errors: *mut u32,
+        stream: *mut c_void,
+    ) -> c_int;
+    pub fn rdx_cbor_bound(info: *const RdxResponseInfo, flags: u32) -> u64;
+    pub fn rdx_cbor_encode(
+        info: *const RdxResponseInfo,
+        body: *const c_void,
+        counts: *const i64,
+        flags: u32,
+        out: *mut c_void,
+        out_cap: u64,
+        out_len: *mut u64,
+    ) -> c_int;
+    pub fn rdx_cbor_encode_device(
+        ws: *mut RdxWorkspace,
+        info: *const RdxResponseInfo,
+        d_body: *const c_void,
+        d_counts: *const i64,
+        flags: u32,
+        d_out: *mut c_void,
+        out_cap: u64,
+        d_out_len: *mut u64,
+        d_status: *mut u32,
         stream: *mut c_void,
     ) -> c_int;
 }

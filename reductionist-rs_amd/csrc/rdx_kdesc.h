@@ -160,6 +160,26 @@ struct KMultiArgs {
 };
 static_assert(sizeof(KMultiArgs) <= 4096, "k_multi arguments exceed 4 KiB");
 
+// Response serialisation (k_cbor.hip): the CBOR body's host-known segments and the count array to encode.
+constexpr int kCborFixedMax = 1024;   // segment A (map head, "bytes", body head) + segment B (dtype .. count head)
+constexpr int kCborTailMax = 64;      // segment D ("count_as_bytes" + head) + segment F ("byte_order": "little")
+struct KCbor {
+    uint8_t *out;               // the encoded response (device)
+    const int64_t *counts;      // the count array's values (device)
+    uint64_t n;                 // counts encoded as the array (0: empty or count_as_bytes)
+    uint64_t c_off;             // offset of the array's first integer in out
+    uint64_t b_off;             // offset of segment B (after the body)
+    uint64_t raw_len;           // bytes of the count_as_bytes payload between D and F (copied by the host)
+    uint64_t *out_len;          // device: total encoded length
+    uint32_t *status;           // device, may be NULL: RDX_E_DEVICE on a look-back fault
+    uint64_t *records;          // one tagged granule per tile (look-back)
+    uint32_t *tile_ctr;         // tile counter, zero between launches
+    uint32_t epoch, n_tiles, vec;
+    uint32_t a_len, b_len, d_len, f_len, pad;
+    uint8_t fixed[kCborFixedMax];   // A then B
+    uint8_t tail[kCborTailMax];     // D then F
+};
+
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]
 // (operations.rs:188-210, :58-67).  out index g -> element offset via `view` (dims
 // innermost-first in OUTPUT order).

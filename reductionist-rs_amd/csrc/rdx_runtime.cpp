@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/rdx.h"
+#include "rdx_cbor.hpp"
 #include "rdx_kernels.hpp"
 #include "rdx_plan.hpp"
 
@@ -1170,6 +1171,56 @@ rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_mul
                                  static_cast<uint8_t *>(it.d_body), it.d_counts, it.d_status, s);
         if (statuses[i] == RDX_E_DEVICE || statuses[i] == RDX_E_OUT_OF_MEMORY) return (rdx_status)statuses[i];
     }
+    return RDX_OK;
+}
+
+rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *info, const void *d_body,
+                                  const int64_t *d_counts, uint32_t flags, void *d_out, uint64_t out_cap,
+                                  uint64_t *d_out_len, uint32_t *d_status, void *stream) {
+    if (!ws || !info || !d_out || !d_out_len) return RDX_E_INVALID_ARGUMENT;
+    CborLayout L;
+    if (rdx_status st = cbor_layout(*info, flags, L)) return st;
+    if ((L.body_len && !d_body) || (L.n_counts && !d_counts)) return RDX_E_INVALID_ARGUMENT;
+    if (out_cap < L.fixed() + (L.count_array ? 9 * L.n_counts : 0)) return RDX_E_BUFFER_TOO_SMALL;
+    if (L.a.size() + L.b.size() > (size_t)kCborFixedMax || L.d.size() + L.f.size() > (size_t)kCborTailMax)
+        return RDX_E_UNSUPPORTED;   // cannot happen: ndim <= RDX_MAX_NDIM bounds both
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    RDX_HIP(hipSetDevice(ws->device));
+    KCbor m{};
+    uint8_t *out = static_cast<uint8_t *>(d_out);
+    m.out = out;
+    m.counts = d_counts;
+    m.n = L.count_array ? L.n_counts : 0;
+    const uint64_t tiles = (m.n + 2047) / 2048;   // k_cbor.hip kCborTile
+    if (tiles > 0xffffffffull) return RDX_E_UNSUPPORTED;
+    m.n_tiles = (uint32_t)tiles;
+    m.c_off = L.c_off();
+    m.b_off = L.b_off();
+    m.raw_len = L.count_raw ? 8 * L.n_counts : 0;
+    m.out_len = d_out_len;
+    m.status = d_status;
+    m.vec = (reinterpret_cast<uintptr_t>(d_counts) % 16) == 0;
+    m.a_len = (uint32_t)L.a.size();
+    m.b_len = (uint32_t)L.b.size();
+    m.d_len = (uint32_t)L.d.size();
+    m.f_len = (uint32_t)L.f.size();
+    std::memcpy(m.fixed, L.a.data(), L.a.size());
+    std::memcpy(m.fixed + L.a.size(), L.b.data(), L.b.size());
+    std::memcpy(m.tail, L.d.data(), L.d.size());
+    std::memcpy(m.tail + L.d.size(), L.f.data(), L.f.size());
+    rdx_status st;
+    if (m.n_tiles) {
+        if ((st = ensure(ws, ws->partials, m.n_tiles, s, true))) return st;
+        if ((st = ensure(ws, ws->tickets, kTicketWords, s, true))) return st;
+        if ((st = next_epoch(ws, s, m.epoch))) return st;
+        m.records = ws->partials.p;
+        m.tile_ctr = ws->tickets.p;
+    }
+    if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
+    if (L.body_len) RDX_HIP(hipMemcpyAsync(out + L.body_off(), d_body, L.body_len, hipMemcpyDeviceToDevice, s));
+    if (L.count_raw)   // c.to_ne_bytes() of every count (models.rs:383-385), after segment D
+        RDX_HIP(hipMemcpyAsync(out + m.c_off + L.d.size(), d_counts, m.raw_len, hipMemcpyDeviceToDevice, s));
+    RDX_HIP(launch_cbor(m, s));
     return RDX_OK;
 }
 

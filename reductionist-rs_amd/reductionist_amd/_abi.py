@@ -34,6 +34,7 @@ DTYPE_NAMES = {v: k for k, v in DTYPES.items()}
 BYTE_ORDER = {None: 0, "little": 1, "big": 2}
 ORDER = {None: 0, "C": 1, "F": 2}
 AXES_ALL, AXES_ONE, AXES_MULTI = 0, 1, 2
+CBOR_SHAPE_AS_BYTES, CBOR_COUNT_AS_BYTES = 1, 2   # rdx_cbor_* flags (RequestData.option_*_as_bytes)
 FILTER_IDS = {"shuffle": 1, "shuffle_simd": 2}
 COMPRESSION = {None: 0, "gzip": 1, "zlib": 2, "blosc2": 3}
 MISSING_KINDS = {None: 0, "missing_value": 1, "missing_values": 2, "valid_min": 3, "valid_max": 4,
@@ -166,6 +167,9 @@ def _declare(lib):
         "rdx_execute_multi_device": (C.c_int, [VP, U64, P(rdx_multi_item), VP, P(C.c_uint32), info_p]),
         "rdx_execute_owned": (C.c_int, [VP, req_p, VP, U64, P(P(rdx_result))]),
         "rdx_result_free": (None, [VP, P(rdx_result)]),
+        "rdx_cbor_bound": (U64, [P(rdx_response_info), C.c_uint32]),
+        "rdx_cbor_encode": (C.c_int, [P(rdx_response_info), VP, VP, C.c_uint32, VP, U64, P(U64)]),
+        "rdx_cbor_encode_device": (C.c_int, [VP, P(rdx_response_info), VP, VP, C.c_uint32, VP, U64, VP, VP, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -181,7 +185,7 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_workspace_create",
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
             "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
-            "rdx_execute_owned", "rdx_result_free"]
+            "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device"]
 
 
 def lib():
