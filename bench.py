@@ -26,6 +26,8 @@ extra (every number DESIGN.md quotes comes from here):
   mixed_requests         (N=1) 20 mixed C1/C3 requests in ONE heterogeneous launch (rdx_execute_multi_device)
   concurrent_native      (N=1) C1 / C2 / C3 requests from native C++ threads (rdx_conc_bench: own workspace
                          and stream per thread, execute + synchronize per request, no Python on the path)
+  cbor_response          (N=1) the CBOR response body of an axis = [] count over the C5 shape (32 Mi counts)
+                         packed on the device (rdx_cbor_encode_device) vs the host encoder
   host_inclusive         (N=1) C2 / C3 / C5 through rdx_execute from pageable and pinned host memory,
                          next to the raw PCIe copy time of the same bytes
   cpu_baselines          (N=1) the oracle (CPU restatement of the reference path) on host cores: C1 with
@@ -695,6 +697,72 @@ def leg_native_concurrent(cx):
     return out
 
 
+def leg_cbor(cx, with_cpu):
+    """Response serialisation of a large count vector where it was computed (rdx_cbor_encode_device):
+    axis = [] count over the C5 chunk shape (i64 [512,256,256], missing_value) gives a 256 MiB i64 body and
+    32 Mi counts; the CBOR body (serde_cbor CBORResponse, app.rs:33-40) is packed on the device.  Device
+    time per call (HIP events, K back-to-back calls): the whole call (body copy + count array) and the
+    count-array kernel alone (a body-less layout); against the engine's host encoder on one core."""
+    import numpy as np
+    torch, lib, _abi = cx.torch, cx.lib, cx.abi
+    n = 512 * 256 * 256
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED00CB)
+    d = torch.randint(0, 4, (n,), dtype=torch.int64, device="cuda", generator=g)
+    creq = _abi.CRequest("count", "int64", shape=[512, 256, 256], axis=[], missing_kind="missing_value",
+                         missing_values=np.int64(1).tobytes(), n_missing=1)
+    pinfo = _abi.rdx_response_info()
+    assert lib.rdx_plan(creq.ref, n * 8, C.byref(pinfo)) == 0
+    body = torch.empty(pinfo.body_bytes, dtype=torch.uint8, device="cuda")
+    counts = torch.empty(pinfo.n_counts, dtype=torch.int64, device="cuda")
+    info = cx.ws.execute_device(creq, d.data_ptr(), n * 8, body.data_ptr(), counts.data_ptr(), None,
+                                cx.stream.cuda_stream)
+    bare = _abi.rdx_response_info.from_buffer_copy(info)
+    bare.body_bytes = 0
+    out = {}
+    for name, inf, flags in (("count_array", info, 0), ("count_array_kernel_only", bare, 0),
+                             ("count_as_bytes", info, _abi.CBOR_COUNT_AS_BYTES)):
+        bound = lib.rdx_cbor_bound(C.byref(inf), flags)
+        dst = torch.empty(bound, dtype=torch.uint8, device="cuda")
+        dlen = torch.zeros(1, dtype=torch.int64, device="cuda")
+        args = (cx.ws.ws, C.byref(inf), C.c_void_p(body.data_ptr()), C.c_void_p(counts.data_ptr()), flags,
+                C.c_void_p(dst.data_ptr()), bound, C.c_void_p(dlen.data_ptr()), None, cx.sh)
+
+        def step(i, args=args):
+            st = lib.rdx_cbor_encode_device(*args)
+            if st:
+                raise RuntimeError(_abi.status_string(st))
+
+        t = cx.dev_time(step, 20)
+        enc = int(dlen[0])
+        clen = enc - (lib.rdx_cbor_bound(C.byref(inf), flags) - (9 * n if flags == 0 else 0))
+        moved = 2 * inf.body_bytes + 8 * n + (clen if flags == 0 else 8 * n)
+        out[name] = {"us_per_call": round(t * 1e6, 2), "encoded_bytes": enc, "bytes_moved": moved,
+                     "roofline_frac": round(moved / t / 1e9 / PEAK_GBS, 4)}
+        del dst
+    out["raw_response_bytes"] = int(info.body_bytes + 8 * n)
+    out["note"] = ("bytes_moved = body read + write (device copy) + counts read + encoded count bytes written; "
+                   "the packed body is what crosses PCIe instead of body + 8 B per count")
+    if with_cpu:
+        hb = np.empty(info.body_bytes, dtype=np.uint8)
+        hc = counts.cpu().numpy()
+        hb[:] = body.cpu().numpy()
+        cap = lib.rdx_cbor_bound(C.byref(info), 0)
+        buf = np.empty(cap, dtype=np.uint8)
+        ln = C.c_uint64()
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            st = lib.rdx_cbor_encode(C.byref(info), hb.ctypes.data, hc.ctypes.data, 0, buf.ctypes.data, cap,
+                                     C.byref(ln))
+            assert st == 0
+        th = (time.perf_counter() - t0) / reps
+        assert ln.value == out["count_array"]["encoded_bytes"]
+        out["cpu_host_encoder"] = {"ms_per_call": round(th * 1e3, 2), "cores": 1,
+                                   "note": "rdx_cbor_encode (C++, -O2) on host buffers, same response"}
+    return out
+
+
 def leg_host(cx):
     """Host-inclusive rates (chunk in host memory -> H2D -> kernels -> D2H through rdx_execute), pageable and
     page-locked (rdx_host_alloc) buffers, next to the raw PCIe copy of the same bytes (torch, pinned)."""
@@ -913,6 +981,7 @@ def main():
         extra["configs"] = leg_configs(cx)
         extra["mixed_requests"] = leg_mixed(cx)
         extra["concurrent_native"] = leg_native_concurrent(cx)
+        extra["cbor_response"] = leg_cbor(cx, solo and not args.no_cpu_baseline)
     if world == 1 and not args.no_host:
         extra["host_inclusive"] = leg_host(cx)
     cpu_line = None

@@ -304,8 +304,9 @@ uint64_t rdx_cbor_bound(const rdx_response_info *info, uint32_t flags);
 rdx_status rdx_cbor_encode(const rdx_response_info *info, const void *body, const int64_t *counts, uint32_t flags,
                            void *out, uint64_t out_cap, uint64_t *out_len);
 /* Device buffers in (e.g. rdx_execute_device's outputs), device buffer out (>= rdx_cbor_bound bytes),
- * asynchronous on `stream`: *d_out_len (device u64) receives the encoded length, *d_status (device
- * word, may be NULL) 0 or RDX_E_DEVICE. */
+ * asynchronous on `stream`: *d_out_len (device u64) receives the encoded length; *d_status (device word,
+ * may be NULL) is set to 0 (reserved for device-side failures; the encoder never waits on another
+ * workgroup's progress, so it has none today). */
 rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *info, const void *d_body,
                                   const int64_t *d_counts, uint32_t flags, void *d_out, uint64_t out_cap,
                                   uint64_t *d_out_len, uint32_t *d_status, void *stream);

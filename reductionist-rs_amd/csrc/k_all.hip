@@ -200,6 +200,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 
 template <typename T, int OP, bool FUSED, int MK, int UNR>
 __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
+    RDX_STAMP(0);
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
     const uint8_t *base = chunk_base(a.src, chunk);
@@ -283,6 +284,7 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
         load_tile<T, FUSED, false>(x0, base, a.src.plane, va + nfull * te, vb);
         consume_tile<T, OP, FUSED, MK, false>(r, x0, a, va + nfull * te, vb, selA, selB);
     }
+    RDX_STAMP(1);
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
 
@@ -476,5 +478,15 @@ hipError_t RDX_KFN(launch_all_contig)(uint32_t op, const KAllContig &a, uint32_t
 hipError_t RDX_KFN(launch_all_strided)(uint32_t op, const KAllStrided &a, uint32_t n_chunks, hipStream_t s) {
     return launch_strided_op<RDX_T>(op, a, n_chunks, s);
 }
+
+#if RDX_PROBES
+}  // namespace rdx
+// probe builds: the phase timeline of the last all-axes launch of this dtype (rdx_device.hpp RDX_STAMP)
+extern "C" int RDX_KFN(rdx_probe_read)(uint64_t *host, uint32_t n) {
+    if (n > 4 * 8192) n = 4 * 8192;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rdx::g_rdx_probe), n * sizeof(uint64_t)) == hipSuccess ? 0 : 1;
+}
+namespace rdx {
+#endif
 
 }  // namespace rdx

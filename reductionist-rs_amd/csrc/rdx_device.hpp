@@ -416,6 +416,21 @@ __device__ __forceinline__ constexpr int packed_words() {
 // value as one; the count (< 2^47) with the NaN flag in bit 47 as one; each ±0 fold-order rank (48-bit
 // two's complement, INT64_MAX as 0x7fff_ffff_ffff) as one.  f32 sum: 3 granules, f32 min/max: 4, f64
 // min/max and sum: 5, integer sum: 3, count: 1.
+// Phase timeline of the all-axes kernels (probe builds only, make EXTRA=-DRDX_PROBES=1): per workgroup
+// [0] first instruction, [1] streaming done, [2] record published + counter added, [3] fold done (last
+// arriver), in wall-clock ticks (100 MHz).  Read back by rdx_probe_read_<dtype> (k_all.hip).
+#if RDX_PROBES
+static __device__ uint64_t g_rdx_probe[4 * 8192];
+#define RDX_STAMP(slot)                                                              \
+    do {                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x < 8192) g_rdx_probe[4 * blockIdx.x + (slot)] = wall_clock64(); \
+    } while (0)
+#else
+#define RDX_STAMP(slot) \
+    do {                \
+    } while (0)
+#endif
+
 constexpr uint32_t kSpinLimit = 1u << 22;
 constexpr uint64_t kPayload = (1ull << 48) - 1;
 constexpr int kMaxGranules = 6;
@@ -643,6 +658,7 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
         s_last = arrive_last(out.tickets + (uint64_t)chunk * kTicketWords, bpc, b);
         s_fault = 0;
     }
+    RDX_STAMP(2);
     __syncthreads();
     if (!s_last) return;
     Red<T, OP> acc;
@@ -672,6 +688,7 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
         }
         __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    RDX_STAMP(3);
 }
 
 // Integer count across workgroups without a hot atomic: every workgroup publishes its count (one

@@ -1198,7 +1198,6 @@ rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *in
     m.b_off = L.b_off();
     m.raw_len = L.count_raw ? 8 * L.n_counts : 0;
     m.out_len = d_out_len;
-    m.status = d_status;
     m.vec = (reinterpret_cast<uintptr_t>(d_counts) % 16) == 0;
     m.a_len = (uint32_t)L.a.size();
     m.b_len = (uint32_t)L.b.size();
@@ -1208,19 +1207,28 @@ rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *in
     std::memcpy(m.fixed + L.a.size(), L.b.data(), L.b.size());
     std::memcpy(m.tail, L.d.data(), L.d.size());
     std::memcpy(m.tail + L.d.size(), L.f.data(), L.f.size());
+    // the body / count_as_bytes payload copies ride in the same launch when 16-byte loads and
+    // dword-aligned 16-byte stores fit them (large bodies: the body head makes segment A 12 bytes)
+    const auto al = [](const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
+    m.body = static_cast<const uint8_t *>(d_body);
+    m.body_len = L.body_len;
+    m.copy_body = L.body_len && al(d_body, 16) && al(out + L.body_off(), 4);
+    m.copy_raw = L.count_raw && al(d_counts, 16) && al(out + m.c_off + L.d.size(), 4);
+    const uint64_t copy_bytes = (m.copy_body ? L.body_len : 0) + (m.copy_raw ? m.raw_len : 0);
+    const uint64_t copy_blocks = std::min<uint64_t>((copy_bytes + 65535) / 65536, (uint64_t)ws->cus * 8);
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>({1, tiles, copy_blocks});
     rdx_status st;
     if (m.n_tiles) {
         if ((st = ensure(ws, ws->partials, m.n_tiles, s, true))) return st;
-        if ((st = ensure(ws, ws->tickets, kTicketWords, s, true))) return st;
         if ((st = next_epoch(ws, s, m.epoch))) return st;
         m.records = ws->partials.p;
-        m.tile_ctr = ws->tickets.p;
     }
     if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
-    if (L.body_len) RDX_HIP(hipMemcpyAsync(out + L.body_off(), d_body, L.body_len, hipMemcpyDeviceToDevice, s));
-    if (L.count_raw)   // c.to_ne_bytes() of every count (models.rs:383-385), after segment D
+    if (L.body_len && !m.copy_body)
+        RDX_HIP(hipMemcpyAsync(out + L.body_off(), d_body, L.body_len, hipMemcpyDeviceToDevice, s));
+    if (L.count_raw && !m.copy_raw)   // c.to_ne_bytes() of every count (models.rs:383-385), after segment D
         RDX_HIP(hipMemcpyAsync(out + m.c_off + L.d.size(), d_counts, m.raw_len, hipMemcpyDeviceToDevice, s));
-    RDX_HIP(launch_cbor(m, s));
+    RDX_HIP(launch_cbor(m, blocks, s));
     return RDX_OK;
 }
 

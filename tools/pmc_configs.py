@@ -9,6 +9,7 @@ Infinity Cache, one kernel family per case so a dispatch's kernel name identifie
   axis0_cols   k_axis_cols    f32 [4096,4096] axis 0 sum                             (64 MiB read)
   axis1_rows   k_axis_rows    f32 [4096,4096] axis 1 sum                             (64 MiB read)
   mixed_multi  k_multi        10 x C1 + 10 x C3 requests in one launch               (97 MB read)
+  cbor_counts  k_cbor         32 Mi counts (0/1) -> CBOR integers, no body            (256 MiB read, 32 MiB written)
 
 tools/pmc_traffic.py turns the counter CSVs into profiles/r02_pmc_<case>.json."""
 import ctypes as C
@@ -69,6 +70,21 @@ a = [torch.rand(4096 * 4096, device="cuda", generator=g) for _ in range(6)]
 single(_abi.CRequest("sum", "float32", shape=[4096, 4096], axis=0), a, 64 << 20)
 single(_abi.CRequest("sum", "float32", shape=[4096, 4096], axis=1), a, 64 << 20)
 del a
+
+
+# cbor_counts: the count-array kernel alone (a body-less response layout)
+n = 512 * 256 * 256
+cts = torch.randint(0, 2, (n,), dtype=torch.int64, device="cuda", generator=g)
+info = _abi.rdx_response_info()
+info.dtype, info.ndim, info.shape[0], info.body_bytes, info.n_counts = _abi.DTYPES["int64"], 1, n, 0, n
+bound = lib.rdx_cbor_bound(C.byref(info), 0)
+dst = torch.empty(bound, dtype=torch.uint8, device="cuda")
+dlen = torch.zeros(1, dtype=torch.int64, device="cuda")
+for _ in range(K + 1):
+    assert lib.rdx_cbor_encode_device(ws.ws, C.byref(info), None, C.c_void_p(cts.data_ptr()), 0,
+                                      C.c_void_p(dst.data_ptr()), bound, C.c_void_p(dlen.data_ptr()), None, SH) == 0
+torch.cuda.synchronize()
+del cts, dst
 
 
 # mixed_multi (bench.leg_mixed's requests)
