@@ -216,12 +216,20 @@ rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req,
  * rdx_host_alloc buffers) is pipelined: the chunk's H2D and the response's D2H overlap. */
 typedef struct rdx_result {
     rdx_response_info info;
-    void *body;            /* info.body_bytes bytes (16-byte aligned) */
-    int64_t *counts;       /* info.n_counts values */
-    uint64_t reserved[2];
+    void *body;            /* rdx_execute_owned: info.body_bytes bytes (16-byte aligned);
+                              rdx_execute_cbor: the CBOR response body, cbor_bytes bytes */
+    int64_t *counts;       /* rdx_execute_owned: info.n_counts values; rdx_execute_cbor: NULL */
+    uint64_t cbor_bytes;   /* rdx_execute_cbor: length of the CBOR body; otherwise 0 */
+    uint64_t reserved;
 } rdx_result;
 rdx_status rdx_execute_owned(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len,
                              rdx_result **out);
+/* rdx_execute_owned whose response leaves the device already serialised: `body` holds the HTTP body of
+ * the reference's success response (serde_cbor::to_vec(&CBORResponse::new(&response)), app.rs:33-40;
+ * flags = RDX_CBOR_* from RequestData.option_*_as_bytes), packed on the device by the same encoder as
+ * rdx_cbor_encode_device — a large count vector never crosses PCIe as 8-byte integers. */
+rdx_status rdx_execute_cbor(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len,
+                            uint32_t flags, rdx_result **out);
 void rdx_result_free(rdx_context *ctx, rdx_result *result);
 
 /* Device-resident path: everything already in HBM, nothing copied, asynchronous on `stream`.

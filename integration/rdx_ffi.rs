@@ -19,6 +19,8 @@
 //!                                     new: device-resident, batched and heterogeneous entry points
 //!   rdx_decompress_batch_device       compression.rs:18-27 `decompress` for a batch of device streams
 //!   rdx_inflate_last_error / _string  the detail of RDX_E_DECOMPRESSION (error.rs:33-41)
+//!   rdx_execute_cbor                  app.rs:163-183 + app.rs:33-40: the response leaves the engine as
+//!                                     its CBOR body
 //!   rdx_cbor_bound / _encode / _encode_device
 //!                                     app.rs:33-40 `serde_cbor::to_vec(&CBORResponse::new(&self))`
 //!                                     (models.rs:355-416), host or device-resident outputs
@@ -127,7 +129,8 @@ pub struct RdxResult {
     pub info: RdxResponseInfo,
     pub body: *mut c_void,
     pub counts: *mut i64,
-    pub reserved: [u64; 2],
+    pub cbor_bytes: u64,
+    pub reserved: u64,
 }
 
 pub enum RdxContext {}
@@ -165,6 +168,14 @@ extern "C" {
         req: *const RdxRequest,
         chunk: *const c_void,
         chunk_len: u64,
+        out: *mut *mut RdxResult,
+    ) -> c_int;
+    pub fn rdx_execute_cbor(
+        ctx: *mut RdxContext,
+        req: *const RdxRequest,
+        chunk: *const c_void,
+        chunk_len: u64,
+        flags: u32,
         out: *mut *mut RdxResult,
     ) -> c_int;
     pub fn rdx_result_free(ctx: *mut RdxContext, result: *mut RdxResult);

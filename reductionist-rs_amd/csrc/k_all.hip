@@ -483,7 +483,7 @@ hipError_t RDX_KFN(launch_all_strided)(uint32_t op, const KAllStrided &a, uint32
 }  // namespace rdx
 // probe builds: the phase timeline of the last all-axes launch of this dtype (rdx_device.hpp RDX_STAMP)
 extern "C" int RDX_KFN(rdx_probe_read)(uint64_t *host, uint32_t n) {
-    if (n > 4 * 8192) n = 4 * 8192;
+    if (n > 8 * 8192) n = 8 * 8192;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(rdx::g_rdx_probe), n * sizeof(uint64_t)) == hipSuccess ? 0 : 1;
 }
 namespace rdx {

@@ -418,12 +418,16 @@ __device__ __forceinline__ constexpr int packed_words() {
 // min/max and sum: 5, integer sum: 3, count: 1.
 // Phase timeline of the all-axes kernels (probe builds only, make EXTRA=-DRDX_PROBES=1): per workgroup
 // [0] first instruction, [1] streaming done, [2] record published + counter added, [3] fold done (last
-// arriver), in wall-clock ticks (100 MHz).  Read back by rdx_probe_read_<dtype> (k_all.hip).
+// arriver), in wall-clock ticks (100 MHz); [4] the HW_ID register at the start (CU / SH / SE placement).
+// Read back by rdx_probe_read_<dtype> (k_all.hip).
 #if RDX_PROBES
-static __device__ uint64_t g_rdx_probe[4 * 8192];
-#define RDX_STAMP(slot)                                                              \
-    do {                                                                             \
-        if (threadIdx.x == 0 && blockIdx.x < 8192) g_rdx_probe[4 * blockIdx.x + (slot)] = wall_clock64(); \
+static __device__ uint64_t g_rdx_probe[8 * 8192];
+#define RDX_STAMP(slot)                                                                              \
+    do {                                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x < 8192) {                                                 \
+            g_rdx_probe[8 * blockIdx.x + (slot)] = wall_clock64();                                   \
+            if ((slot) == 0) g_rdx_probe[8 * blockIdx.x + 4] = __builtin_amdgcn_s_getreg(4 | (31 << 11)); \
+        }                                                                                            \
     } while (0)
 #else
 #define RDX_STAMP(slot) \

@@ -106,6 +106,9 @@ struct rdx_workspace {
     DevBuf<uint32_t> zerr;
     DevBuf<uint8_t> raw;
     std::vector<uint8_t> last_zptrs, last_zlens;
+    // rdx_execute_cbor: the encoded response and its length
+    DevBuf<uint8_t> cbor;
+    DevBuf<uint64_t> cbor_len;
     uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
@@ -580,6 +583,8 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->zout_len.p);
     fr(ws->zerr.p);
     fr(ws->raw.p);
+    fr(ws->cbor.p);
+    fr(ws->cbor_len.p);
     if (ws->aux_stream) {
         (void)hipStreamSynchronize(ws->aux_stream);
         (void)hipStreamDestroy(ws->aux_stream);
@@ -597,6 +602,63 @@ bool is_gfx950(int dev) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+// Response serialisation on the device (rdx_cbor_encode_device, k_cbor.hip), asynchronous on `s`.
+rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const void *d_body, const int64_t *d_counts,
+                       uint32_t flags, void *d_out, uint64_t out_cap, uint64_t *d_out_len, uint32_t *d_status,
+                       hipStream_t s) {
+    if (!ws || !info || !d_out || !d_out_len) return RDX_E_INVALID_ARGUMENT;
+    CborLayout L;
+    if (rdx_status st = cbor_layout(*info, flags, L)) return st;
+    if ((L.body_len && !d_body) || (L.n_counts && !d_counts)) return RDX_E_INVALID_ARGUMENT;
+    if (out_cap < L.fixed() + (L.count_array ? 9 * L.n_counts : 0)) return RDX_E_BUFFER_TOO_SMALL;
+    if (L.a.size() + L.b.size() > (size_t)kCborFixedMax || L.d.size() + L.f.size() > (size_t)kCborTailMax)
+        return RDX_E_UNSUPPORTED;   // cannot happen: ndim <= RDX_MAX_NDIM bounds both
+    KCbor m{};
+    uint8_t *out = static_cast<uint8_t *>(d_out);
+    m.out = out;
+    m.counts = d_counts;
+    m.n = L.count_array ? L.n_counts : 0;
+    const uint64_t tiles = (m.n + 2047) / 2048;   // k_cbor.hip kCborTile
+    if (tiles > 0xffffffffull) return RDX_E_UNSUPPORTED;
+    m.n_tiles = (uint32_t)tiles;
+    m.c_off = L.c_off();
+    m.b_off = L.b_off();
+    m.raw_len = L.count_raw ? 8 * L.n_counts : 0;
+    m.out_len = d_out_len;
+    m.vec = (reinterpret_cast<uintptr_t>(d_counts) % 16) == 0;
+    m.a_len = (uint32_t)L.a.size();
+    m.b_len = (uint32_t)L.b.size();
+    m.d_len = (uint32_t)L.d.size();
+    m.f_len = (uint32_t)L.f.size();
+    std::memcpy(m.fixed, L.a.data(), L.a.size());
+    std::memcpy(m.fixed + L.a.size(), L.b.data(), L.b.size());
+    std::memcpy(m.tail, L.d.data(), L.d.size());
+    std::memcpy(m.tail + L.d.size(), L.f.data(), L.f.size());
+    // the body / count_as_bytes payload copies ride in the same launch when 16-byte loads and
+    // dword-aligned 16-byte stores fit them (large bodies: the body head makes segment A 12 bytes)
+    const auto al = [](const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
+    m.body = static_cast<const uint8_t *>(d_body);
+    m.body_len = L.body_len;
+    m.copy_body = L.body_len && al(d_body, 16) && al(out + L.body_off(), 4);
+    m.copy_raw = L.count_raw && al(d_counts, 16) && al(out + m.c_off + L.d.size(), 4);
+    const uint64_t copy_bytes = (m.copy_body ? L.body_len : 0) + (m.copy_raw ? m.raw_len : 0);
+    const uint64_t copy_blocks = std::min<uint64_t>((copy_bytes + 65535) / 65536, (uint64_t)ws->cus * 8);
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>({1, tiles, copy_blocks});
+    rdx_status st;
+    if (m.n_tiles) {
+        if ((st = ensure(ws, ws->partials, m.n_tiles, s, true))) return st;
+        if ((st = next_epoch(ws, s, m.epoch))) return st;
+        m.records = ws->partials.p;
+    }
+    if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
+    if (L.body_len && !m.copy_body)
+        RDX_HIP(hipMemcpyAsync(out + L.body_off(), d_body, L.body_len, hipMemcpyDeviceToDevice, s));
+    if (L.count_raw && !m.copy_raw)   // c.to_ne_bytes() of every count (models.rs:383-385), after segment D
+        RDX_HIP(hipMemcpyAsync(out + m.c_off + L.d.size(), d_counts, m.raw_len, hipMemcpyDeviceToDevice, s));
+    RDX_HIP(launch_cbor(m, blocks, s));
+    return RDX_OK;
 }
 
 // ---- host-resident execution (rdx_execute / rdx_execute_owned) --------------------------------------
@@ -723,11 +785,22 @@ rdx_status map_pipelined(rdx_workspace *ws, const ExecPlan &p, const uint8_t *ch
     return RDX_OK;
 }
 
+// rdx_execute_cbor: the response leaves the device as its CBOR body (k_cbor), in a pooled
+// page-locked block.
+struct CborOut {
+    uint32_t flags = 0;
+    void *host = nullptr;   // pool block (rdx_result.body)
+    uint64_t len = 0;       // encoded bytes
+};
+constexpr uint64_t kCborOneTrip = 1ull << 20;   // bounds up to this come back whole, in one round trip
+
 // operation<T>() for a chunk in host memory (app.rs:163-183): plan, bind the response buffers
 // (caller-provided or pooled), H2D, kernels, D2H; blocks until the response is in host memory.
+// With `cb`, the response is serialised on the device (serde_cbor CBORResponse, app.rs:33-40) and only
+// its CBOR body comes back.
 rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t *chunk, uint64_t chunk_len,
                         const std::function<rdx_status(const rdx_response_info &, void **, int64_t **)> &bind,
-                        rdx_response_info *info) {
+                        rdx_response_info *info, CborOut *cb = nullptr) {
     const bool compressed = req.compression != RDX_COMPRESSION_NONE;
     ExecPlan p;
     rdx_status st;
@@ -761,7 +834,7 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
         RDX_HIP(hipSetDevice(ws->device));
         hipStream_t s = ws->own_stream;
         rdx_status r;
-        if (!compressed && p.mode == Mode::Map && p.unfused_es.empty() && !p.fused && p.map.view.ndim >= 1 &&
+        if (!cb && !compressed && p.mode == Mode::Map && p.unfused_es.empty() && !p.fused && p.map.view.ndim >= 1 &&
             p.map.view.count[p.map.view.ndim - 1] >= 2 && chunk_len >= (32ull << 20) && is_pinned(chunk) &&
             is_pinned(body) && (p.map.kind == 0 || is_pinned(counts))) {
             if ((r = ensure_aux(ws))) return r;
@@ -792,6 +865,28 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
         if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
             return r;
         uint32_t status = 0;
+        if (cb) {   // encode on the device; the length (and, for small bounds, the bytes) in one trip
+            const uint64_t bound = rdx_cbor_bound(&p.info, cb->flags);
+            if (!bound) return RDX_E_INVALID_ARGUMENT;
+            if ((r = ensure(ws, ws->cbor, bound, s))) return r;
+            if ((r = ensure(ws, ws->cbor_len, 1, s))) return r;
+            if ((r = pool_alloc(ctx, bound, &cb->host))) return r;
+            if ((r = cbor_device(ws, &p.info, ws->body.p, ws->counts.p, cb->flags, ws->cbor.p, bound, ws->cbor_len.p,
+                                 nullptr, s)))
+                return r;
+            uint64_t n = 0;
+            RDX_HIP(hipMemcpyAsync(&n, ws->cbor_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            if (bound <= kCborOneTrip) RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, bound, hipMemcpyDeviceToHost, s));
+            RDX_HIP(hipStreamSynchronize(s));
+            if (status) return (rdx_status)status;
+            if (bound > kCborOneTrip) {
+                RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, n, hipMemcpyDeviceToHost, s));
+                RDX_HIP(hipStreamSynchronize(s));
+            }
+            cb->len = n;
+            return RDX_OK;
+        }
         if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
         if (p.info.n_counts)
             RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -1177,59 +1272,10 @@ rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_mul
 rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *info, const void *d_body,
                                   const int64_t *d_counts, uint32_t flags, void *d_out, uint64_t out_cap,
                                   uint64_t *d_out_len, uint32_t *d_status, void *stream) {
-    if (!ws || !info || !d_out || !d_out_len) return RDX_E_INVALID_ARGUMENT;
-    CborLayout L;
-    if (rdx_status st = cbor_layout(*info, flags, L)) return st;
-    if ((L.body_len && !d_body) || (L.n_counts && !d_counts)) return RDX_E_INVALID_ARGUMENT;
-    if (out_cap < L.fixed() + (L.count_array ? 9 * L.n_counts : 0)) return RDX_E_BUFFER_TOO_SMALL;
-    if (L.a.size() + L.b.size() > (size_t)kCborFixedMax || L.d.size() + L.f.size() > (size_t)kCborTailMax)
-        return RDX_E_UNSUPPORTED;   // cannot happen: ndim <= RDX_MAX_NDIM bounds both
-    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!ws) return RDX_E_INVALID_ARGUMENT;
     RDX_HIP(hipSetDevice(ws->device));
-    KCbor m{};
-    uint8_t *out = static_cast<uint8_t *>(d_out);
-    m.out = out;
-    m.counts = d_counts;
-    m.n = L.count_array ? L.n_counts : 0;
-    const uint64_t tiles = (m.n + 2047) / 2048;   // k_cbor.hip kCborTile
-    if (tiles > 0xffffffffull) return RDX_E_UNSUPPORTED;
-    m.n_tiles = (uint32_t)tiles;
-    m.c_off = L.c_off();
-    m.b_off = L.b_off();
-    m.raw_len = L.count_raw ? 8 * L.n_counts : 0;
-    m.out_len = d_out_len;
-    m.vec = (reinterpret_cast<uintptr_t>(d_counts) % 16) == 0;
-    m.a_len = (uint32_t)L.a.size();
-    m.b_len = (uint32_t)L.b.size();
-    m.d_len = (uint32_t)L.d.size();
-    m.f_len = (uint32_t)L.f.size();
-    std::memcpy(m.fixed, L.a.data(), L.a.size());
-    std::memcpy(m.fixed + L.a.size(), L.b.data(), L.b.size());
-    std::memcpy(m.tail, L.d.data(), L.d.size());
-    std::memcpy(m.tail + L.d.size(), L.f.data(), L.f.size());
-    // the body / count_as_bytes payload copies ride in the same launch when 16-byte loads and
-    // dword-aligned 16-byte stores fit them (large bodies: the body head makes segment A 12 bytes)
-    const auto al = [](const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
-    m.body = static_cast<const uint8_t *>(d_body);
-    m.body_len = L.body_len;
-    m.copy_body = L.body_len && al(d_body, 16) && al(out + L.body_off(), 4);
-    m.copy_raw = L.count_raw && al(d_counts, 16) && al(out + m.c_off + L.d.size(), 4);
-    const uint64_t copy_bytes = (m.copy_body ? L.body_len : 0) + (m.copy_raw ? m.raw_len : 0);
-    const uint64_t copy_blocks = std::min<uint64_t>((copy_bytes + 65535) / 65536, (uint64_t)ws->cus * 8);
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>({1, tiles, copy_blocks});
-    rdx_status st;
-    if (m.n_tiles) {
-        if ((st = ensure(ws, ws->partials, m.n_tiles, s, true))) return st;
-        if ((st = next_epoch(ws, s, m.epoch))) return st;
-        m.records = ws->partials.p;
-    }
-    if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
-    if (L.body_len && !m.copy_body)
-        RDX_HIP(hipMemcpyAsync(out + L.body_off(), d_body, L.body_len, hipMemcpyDeviceToDevice, s));
-    if (L.count_raw && !m.copy_raw)   // c.to_ne_bytes() of every count (models.rs:383-385), after segment D
-        RDX_HIP(hipMemcpyAsync(out + m.c_off + L.d.size(), d_counts, m.raw_len, hipMemcpyDeviceToDevice, s));
-    RDX_HIP(launch_cbor(m, blocks, s));
-    return RDX_OK;
+    return cbor_device(ws, info, d_body, d_counts, flags, d_out, out_cap, d_out_len, d_status,
+                       static_cast<hipStream_t>(stream));
 }
 
 rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, uint64_t n,
@@ -1281,6 +1327,31 @@ rdx_status rdx_execute_owned(rdx_context *ctx, const rdx_request *req, const voi
         return RDX_OK;
     };
     const rdx_status st = execute_host(ctx, *req, static_cast<const uint8_t *>(chunk), chunk_len, bind, &r->info);
+    if (st) {
+        rdx_result_free(ctx, r);
+        return st;
+    }
+    *out = r;
+    return RDX_OK;
+}
+
+rdx_status rdx_execute_cbor(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len,
+                            uint32_t flags, rdx_result **out) {
+    if (!ctx || !req || !out || (!chunk && chunk_len) || (flags & ~(RDX_CBOR_SHAPE_AS_BYTES | RDX_CBOR_COUNT_AS_BYTES)))
+        return RDX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    auto *r = new (std::nothrow) rdx_result();
+    if (!r) return RDX_E_OUT_OF_MEMORY;
+    auto bind = [&](const rdx_response_info &, void **b, int64_t **c) -> rdx_status {
+        *b = nullptr;   // the response stays on the device until it is encoded
+        *c = nullptr;
+        return RDX_OK;
+    };
+    CborOut cb;
+    cb.flags = flags;
+    const rdx_status st = execute_host(ctx, *req, static_cast<const uint8_t *>(chunk), chunk_len, bind, &r->info, &cb);
+    r->body = cb.host;
+    r->cbor_bytes = cb.len;
     if (st) {
         rdx_result_free(ctx, r);
         return st;

@@ -83,7 +83,7 @@ class rdx_multi_item(C.Structure):
 
 class rdx_result(C.Structure):
     _fields_ = [("info", rdx_response_info), ("body", C.c_void_p), ("counts", C.POINTER(C.c_int64)),
-                ("reserved", C.c_uint64 * 2)]
+                ("cbor_bytes", C.c_uint64), ("reserved", C.c_uint64)]
 
 
 class CRequest:
@@ -167,6 +167,7 @@ def _declare(lib):
         "rdx_execute_multi_device": (C.c_int, [VP, U64, P(rdx_multi_item), VP, P(C.c_uint32), info_p]),
         "rdx_execute_owned": (C.c_int, [VP, req_p, VP, U64, P(P(rdx_result))]),
         "rdx_result_free": (None, [VP, P(rdx_result)]),
+        "rdx_execute_cbor": (C.c_int, [VP, req_p, VP, U64, C.c_uint32, P(P(rdx_result))]),
         "rdx_cbor_bound": (U64, [P(rdx_response_info), C.c_uint32]),
         "rdx_cbor_encode": (C.c_int, [P(rdx_response_info), VP, VP, C.c_uint32, VP, U64, P(U64)]),
         "rdx_cbor_encode_device": (C.c_int, [VP, P(rdx_response_info), VP, VP, C.c_uint32, VP, U64, VP, VP, VP]),
@@ -185,7 +186,8 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_workspace_create",
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
             "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
-            "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device"]
+            "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device",
+            "rdx_execute_cbor"]
 
 
 def lib():

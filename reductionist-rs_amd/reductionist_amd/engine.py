@@ -75,6 +75,23 @@ class Engine:
         self.lib.rdx_result_free(self.ctx, res)
         return st, info, body, counts
 
+    def execute_cbor(self, creq: _abi.CRequest, data, flags: int = 0):
+        """rdx_execute_cbor: the response as the reference's HTTP body (serde_cbor CBORResponse, app.rs:33-40),
+        serialised on the device.  Returns (status, info, cbor bytes)."""
+        if isinstance(data, tuple):
+            src, n = C.c_void_p(data[0]), data[1]
+        else:
+            src, n = (C.c_char_p(bytes(data)) if len(data) else None), len(data)
+        res = C.POINTER(_abi.rdx_result)()
+        st = self.lib.rdx_execute_cbor(self.ctx, creq.ref, src, n, flags, C.byref(res))
+        if st != _abi.OK:
+            return st, _abi.rdx_response_info(), b""
+        r = res.contents
+        info = _abi.rdx_response_info.from_buffer_copy(r.info)
+        body = C.string_at(r.body, r.cbor_bytes)
+        self.lib.rdx_result_free(self.ctx, res)
+        return st, info, body
+
     def host_alloc(self, nbytes: int):
         """Page-locked host buffer (rdx_host_alloc) as (pointer, numpy uint8 view); free with host_free."""
         import numpy as np

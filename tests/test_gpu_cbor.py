@@ -145,3 +145,41 @@ def test_device_encoder_full_size_axis_none(workspace):
     for flags in (0, 2):
         got = device_encode(workspace, info, body.data_ptr(), counts.data_ptr(), flags, torch)
         assert got == host_encode(info, hb, hc, flags), flags
+
+
+def test_execute_cbor_end_to_end(engine):
+    """rdx_execute_cbor: host chunk in, the reference's HTTP body out (app.rs:163-183 then app.rs:33-40),
+    equal to the oracle's response serialised by the oracle — exact ops bit-exact, float sums through the
+    engine's own response (rdx_execute_owned) — incl. a response past the one-trip bound (two D2H trips),
+    a gzip chunk and an error."""
+    import gzip
+    rng = np.random.default_rng(0xCB5)
+    cases = [
+        ("count", {"dtype": "int32", "shape": [64, 128, 64], "axis": [], "missing": {"missing_value": 3}},
+         rng.integers(0, 8, 64 * 128 * 64, dtype=np.int32).tobytes()),          # 512 Ki counts: 2 trips
+        ("max", {"dtype": "uint64", "shape": [30, 40], "axis": [1]},
+         rng.integers(0, 2 ** 63, 1200, dtype=np.uint64).tobytes()),
+        ("select", {"dtype": "float32", "shape": [50, 60], "selection": [[2, 50, 3], [0, 60, 1]]},
+         rng.random(3000, dtype=np.float32).tobytes()),
+        ("sum", {"dtype": "int64", "compression": "gzip"},
+         gzip.compress(rng.integers(-10 ** 6, 10 ** 6, 100_000, dtype=np.int64).tobytes(), compresslevel=1)),
+        ("min", {"dtype": "float64", "shape": [100, 100], "axis": [0, 1], "missing": {"valid_range": [0.1, 0.9]}},
+         rng.random(10_000).tobytes()),
+        ("sum", {"dtype": "float32", "shape": [200, 300], "axis": [0]}, rng.random(60_000, dtype=np.float32).tobytes()),
+    ]
+    for op, req, data in cases:
+        creq = make_request(op, req, oracle.convert)
+        for flags in range(4):
+            st, info, got = engine.execute_cbor(creq, data, flags)
+            ost, oinfo, obody, ocounts = oracle.execute(creq, data)
+            assert st == ost == 0, (op, req, st, ost)
+            if op == "sum" and req["dtype"].startswith("float"):
+                est, einfo, ebody, ecounts = engine.execute_owned(creq, data)
+                assert est == 0 and ecounts == ocounts
+                obody = ebody
+            want = cb.cbor_response(obody, _abi.DTYPE_NAMES[oinfo.dtype], oinfo.shape_list(), ocounts,
+                                    bool(flags & 1), bool(flags & 2))
+            assert got == want, (op, req, flags)
+    bad = make_request("sum", {"dtype": "float32", "shape": [7, 7]}, oracle.convert)
+    st, _, _ = engine.execute_cbor(bad, bytes(4 * 48), 0)
+    assert st == oracle.execute(bad, bytes(4 * 48))[0] != 0

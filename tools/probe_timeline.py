@@ -26,9 +26,9 @@ TICK_NS = 10.0   # wall_clock64: 100 MHz
 
 
 def timeline(lib, n_wg):
-    buf = (C.c_uint64 * (4 * 8192))()
-    assert lib.rdx_probe_read_f32(buf, 4 * 8192) == 0
-    rows = [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3]) for i in range(n_wg)]
+    buf = (C.c_uint64 * (8 * 8192))()
+    assert lib.rdx_probe_read_f32(buf, 8 * 8192) == 0
+    rows = [(buf[8 * i], buf[8 * i + 1], buf[8 * i + 2], buf[8 * i + 3], buf[8 * i + 4]) for i in range(n_wg)]
     t0 = min(r[0] for r in rows)
     us = lambda t: round((t - t0) * TICK_NS / 1e3, 3)  # noqa: E731
     folds = [r[3] for r in rows if r[3] >= r[2] and r[3] > t0]
@@ -37,7 +37,22 @@ def timeline(lib, n_wg):
             "first_stream_end_us": us(min(r[1] for r in rows)), "last_stream_end_us": us(max(r[1] for r in rows)),
             "last_arrival_us": us(max(r[2] for r in rows)), "fold_end_us": us(max(folds)) if folds else None,
             "stream_us_median": round(statistics.median(stream), 3), "stream_us_max": round(max(stream), 3),
-            "start_us_deciles": [us(sorted(r[0] for r in rows)[int(q * (n_wg - 1))]) for q in (0.1, 0.5, 0.9)]}
+            "start_us_deciles": [us(sorted(r[0] for r in rows)[int(q * (n_wg - 1))]) for q in (0.1, 0.5, 0.9)],
+            "stream_us_deciles": [round(sorted(stream)[int(q * (n_wg - 1))], 3) for q in (0.1, 0.25, 0.5, 0.75, 0.9)],
+            # per block % 8 (the XCD under round-robin dispatch): median streaming time
+            "stream_us_by_xcd": [round(statistics.median(stream[i::8]), 3) for i in range(8)],
+            # HW_ID placement: workgroups sharing a (SE, SH, CU) slot, and the streaming time of those
+            "hwid_shared_slots": sum(1 for c in _slot_counts(rows).values() if c > 1),
+            "per_wg": [[i, round(stream[i], 2), (rows[i][4] >> 8) & 0xF, (rows[i][4] >> 12) & 1, (rows[i][4] >> 13) & 7]
+                       for i in range(n_wg)]}
+
+
+def _slot_counts(rows):
+    cnt = {}
+    for i, r in enumerate(rows):
+        key = (i % 8, (r[4] >> 8) & 0xFF)   # (XCD under round-robin dispatch, CU_ID / SH_ID / SE_ID)
+        cnt[key] = cnt.get(key, 0) + 1
+    return cnt
 
 
 def main():
