@@ -435,7 +435,11 @@ static __device__ uint64_t g_rdx_probe[8 * 8192];
     } while (0)
 #endif
 
+#if RDX_PROBES
+constexpr uint32_t kSpinLimit = 1u << 12;   // probe builds: a missing record surfaces as RDX_E_DEVICE quickly
+#else
 constexpr uint32_t kSpinLimit = 1u << 22;
+#endif
 constexpr uint64_t kPayload = (1ull << 48) - 1;
 constexpr int kMaxGranules = 6;
 
@@ -635,10 +639,9 @@ __device__ __forceinline__ void block_reduce(Red<T, OP> &r) {
     __syncthreads();
 }
 
-// Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
-// partials in workgroup order and write the response (one launch, no second kernel).  One lane
-// publishes the record (tagged granules, above), then adds to an arrival counter; the workgroup whose
-// add completes the count collects every record.  The counter is sharded 8 ways by workgroup index
+// Arrival counting of the cross-workgroup hand-off: after publishing its record(s) (tagged granules,
+// above) one lane of each workgroup adds to an arrival counter; the workgroup whose add completes the
+// count collects every record.  The counter is sharded 8 ways by workgroup index
 // (b % 8 groups share an XCD under round-robin dispatch) so that arrivals do not serialise on one word
 // (~11 ns per atomic, MI355X_MICROARCH.md "fanin" row); the last arrival of each shard adds to the top
 // counter.  All counters self-reset for the next launch.
@@ -652,14 +655,17 @@ __device__ __forceinline__ bool arrive_last(uint32_t *tk, uint32_t n, uint32_t b
     return __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
 }
 
+// The hand-off's second half: this workgroup's records are published; count its arrival (8-way
+// sharded, `members` workgroups per chunk) and, if it is the last, fold records P[0 .. nrec) in index
+// order (deterministic) and write the chunk's response.  `pool_ctr` (may be NULL): a dynamic-piece
+// counter the last arriver resets for the next launch (every workgroup has stopped claiming by then).
 template <typename T, int OP>
-__device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
+__device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chunk, uint32_t members, uint32_t nrec,
+                                uint32_t b, uint32_t *pool_ctr = nullptr) {
     __shared__ uint32_t s_last, s_fault;
     constexpr int kR = granules<T, OP>();   // u64 granules per record
-    block_reduce(r);
     if (threadIdx.x == 0) {
-        publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
-        s_last = arrive_last(out.tickets + (uint64_t)chunk * kTicketWords, bpc, b);
+        s_last = arrive_last(out.tickets + (uint64_t)chunk * kTicketWords, members, b);
         s_fault = 0;
     }
     RDX_STAMP(2);
@@ -668,8 +674,7 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
     Red<T, OP> acc;
     acc.init();
     uint32_t fault = 0;
-    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kR;
-    for (uint32_t j = threadIdx.x; j < bpc; j += kBlock) {
+    for (uint32_t j = threadIdx.x; j < nrec; j += kBlock) {
         Red<T, OP> o;
         collect<T, OP>(P + (uint64_t)j * kR, o, out.epoch, fault);
         acc.merge(o);
@@ -691,8 +696,20 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
             else if (!Red<T, OP>::kRank && chunk == 0) out.status[0] = 0;   // nothing can fail
         }
         __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pool_ctr) __hip_atomic_store(pool_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     RDX_STAMP(3);
+}
+
+// Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
+// partials in workgroup order and write the response (one launch, no second kernel).
+template <typename T, int OP>
+__device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
+    constexpr int kR = granules<T, OP>();
+    block_reduce(r);
+    const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kR;
+    if (threadIdx.x == 0) publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
+    arrive_and_fold<T, OP>(out, P, chunk, bpc, bpc, b);
 }
 
 // Integer count across workgroups without a hot atomic: every workgroup publishes its count (one
