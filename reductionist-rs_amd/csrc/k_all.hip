@@ -228,17 +228,14 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
             consume<T, OP, MK>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
     }
     // vector body: full tiles split into contiguous per-workgroup ranges, UNR tiles in flight per
-    // lane; the one partial tile (if any) goes to workgroup 0 with the scalar head/tail; the last
-    // n_pieces * pt tiles form the dynamic pool (below).
+    // lane; the one partial tile (if any) goes to workgroup 0 with the scalar head/tail.  (A dynamic
+    // hand-out of the last tiles to the workgroups that finish first was measured slower: the claim
+    // round trips cost more than the imbalance, profiles/r02_pool_ab.jsonl.)
     const uint64_t te = tile_elems<T, FUSED>();
     const uint64_t nfull = (vb - va) / te;
-    const uint32_t pt = a.piece_tiles ? a.piece_tiles : 1;
-    uint64_t n_pieces = a.rec_stride > bpc ? a.pool_tiles / pt : 0;
-    if (n_pieces * pt > nfull / 2) n_pieces = nfull / 2 / pt;   // (a misaligned chunk has one tile less)
-    const uint64_t home = nfull - n_pieces * pt;
-    const uint64_t per = (home + bpc - 1) / bpc;
+    const uint64_t per = (nfull + bpc - 1) / bpc;
     const uint64_t t_begin = (uint64_t)b * per;
-    const uint64_t t_end = t_begin + per < home ? t_begin + per : home;
+    const uint64_t t_end = t_begin + per < nfull ? t_begin + per : nfull;
     uint64_t t = t_begin;
     // Float min/max (the heaviest per-element fold) are software pipelined: the next UNR tiles'
     // loads are issued before the current UNR tiles are consumed (two register sets, alternating),
@@ -290,65 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
         consume_tile<T, OP, FUSED, MK, false>(r, x0, a, va + nfull * te, vb, selA, selB);
     }
     RDX_STAMP(1);
-    if (a.rec_stride <= bpc) {   // no pool: one record per workgroup
-        finalize_all<T, OP>(r, a.out, chunk, bpc, b);
-        return;
-    }
-    constexpr int kR = granules<T, OP>();
-    uint64_t *P = a.out.partials + (uint64_t)chunk * a.rec_stride * kR;
-    block_reduce(r);
-    if (threadIdx.x == 0) publish<T, OP>(P + (uint64_t)b * kR, r, a.out.epoch);
-    uint32_t *ctr = a.pool_ctr + (uint64_t)chunk * kTicketStride;
-    __shared__ uint32_t s_piece;
-#if RDX_PROBES
-    if (threadIdx.x == 0 && blockIdx.x < 8192) g_rdx_probe[8 * blockIdx.x + 5] = 0;
-#endif
-    uint32_t next_static = b;   // (a.pad == 1: tuning probe, pieces b, b + bpc, ... without the counter)
-#if RDX_PROBES
-    uint32_t probe_iters = 0;
-#endif
-    while (n_pieces) {   // claim pieces of the pool until it is empty (a load first: no RMW once it is)
-        if (threadIdx.x == 0) {
-            if (a.pad == 1) {
-                s_piece = next_static < n_pieces ? next_static : (uint32_t)n_pieces;
-                next_static += bpc;
-            } else {
-                const uint32_t seen = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_piece = seen < n_pieces ? __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                          : (uint32_t)n_pieces;
-            }
-        }
-        __syncthreads();
-        const uint32_t piece = s_piece;
-        __syncthreads();
-#if RDX_PROBES
-        if (threadIdx.x == 0 && blockIdx.x < 8192) {
-            g_rdx_probe[8 * blockIdx.x + 5] += 1;                          // claims
-            g_rdx_probe[8 * blockIdx.x + 6] = ((uint64_t)piece << 32) | (uint32_t)n_pieces;
-        }
-        if (++probe_iters > 64) break;   // probe builds: a runaway claim loop ends (records go missing)
-#endif
-        if (piece >= n_pieces) break;
-        Red<T, OP> rp;
-        rp.init();
-        const uint64_t p0 = home + (uint64_t)piece * pt, p1 = p0 + pt;
-        uint64_t q = p0;
-        for (; q + UNR <= p1; q += UNR) {
-            Tile<T, FUSED> x[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, va + (q + u) * te, vb);
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(rp, x[u], a, va + (q + u) * te, vb, selA, selB);
-        }
-        for (; q < p1; ++q) {
-            Tile<T, FUSED> x0;
-            load_tile<T, FUSED, true>(x0, base, a.src.plane, va + q * te, vb);
-            consume_tile<T, OP, FUSED, MK, true>(rp, x0, a, va + q * te, vb, selA, selB);
-        }
-        block_reduce(rp);
-        if (threadIdx.x == 0) publish<T, OP>(P + ((uint64_t)bpc + piece) * kR, rp, a.out.epoch);
-    }
-    arrive_and_fold<T, OP>(a.out, P, chunk, bpc, bpc + (uint32_t)n_pieces, b, ctr);
+    finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
 
 // ---- strided views ---------------------------------------------------------------------------------

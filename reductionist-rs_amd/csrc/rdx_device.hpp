@@ -657,11 +657,10 @@ __device__ __forceinline__ bool arrive_last(uint32_t *tk, uint32_t n, uint32_t b
 
 // The hand-off's second half: this workgroup's records are published; count its arrival (8-way
 // sharded, `members` workgroups per chunk) and, if it is the last, fold records P[0 .. nrec) in index
-// order (deterministic) and write the chunk's response.  `pool_ctr` (may be NULL): a dynamic-piece
-// counter the last arriver resets for the next launch (every workgroup has stopped claiming by then).
+// order (deterministic) and write the chunk's response.
 template <typename T, int OP>
 __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chunk, uint32_t members, uint32_t nrec,
-                                uint32_t b, uint32_t *pool_ctr = nullptr) {
+                                uint32_t b) {
     __shared__ uint32_t s_last, s_fault;
     constexpr int kR = granules<T, OP>();   // u64 granules per record
     if (threadIdx.x == 0) {
@@ -696,7 +695,6 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
             else if (!Red<T, OP>::kRank && chunk == 0) out.status[0] = 0;   // nothing can fail
         }
         __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (pool_ctr) __hip_atomic_store(pool_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     RDX_STAMP(3);
 }

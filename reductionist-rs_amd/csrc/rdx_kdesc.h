@@ -70,15 +70,6 @@ struct KAllContig {
     int64_t r0, rs;
     uint32_t filter_semantics;  // Count(All) uses missing_filter (operations.rs:25-33)
     uint32_t blocks_per_chunk;
-    // Load balance: the last pool_tiles tiles of a chunk are handed out at run time in pieces of
-    // piece_tiles to whichever workgroup of the chunk finishes its static share first; every piece
-    // publishes its own record, so the fold (records in index order: workgroups, then pieces) does not
-    // depend on who computed what.
-    uint32_t pool_tiles;        // 0: static split only
-    uint32_t piece_tiles;
-    uint32_t rec_stride;        // records per chunk: blocks_per_chunk + pool_tiles / piece_tiles
-    uint32_t pad;
-    uint32_t *pool_ctr;         // [chunk * kTicketStride]: piece counters, zero between launches
 };
 
 // A strided view: dims innermost-first.  offset(e) = base_off + sum idx_k * vstride_k,

@@ -62,9 +62,6 @@ struct Tuning {
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
-    int pool_pct = env_int("RDX_POOL_PCT", 0);            // k_all_contig: % of a chunk's tiles handed out at run time (experimental: off)
-    int pool_piece = env_int("RDX_POOL_PIECE_TILES", 2);  // tiles per dynamic piece
-    int pool_static = env_int("RDX_POOL_STATIC", 0);      // tuning probe: pool pieces assigned statically
 };
 
 const Tuning &tuning() {
@@ -184,25 +181,6 @@ rdx_status ensure_aux(rdx_workspace *ws) {
     return RDX_OK;
 }
 
-// k_all_contig's load balance (KAllContig::pool_tiles): the last pool_pct % of a chunk's tiles go to
-// whichever workgroups finish their static share first, in pieces of pool_piece tiles; off when the
-// workgroups would keep fewer than 8 static tiles each.  Partials: n_chunks x rec_stride records;
-// tickets: n_chunks arrival blocks, then one 256 B piece counter per chunk.
-rdx_status set_pool(rdx_workspace *ws, KAllContig &a, uint64_t tiles, uint64_t n_chunks, hipStream_t s) {
-    const uint32_t pt = (uint32_t)std::max(1, tuning().pool_piece);
-    uint64_t pool = tuning().pool_pct > 0 ? tiles * (uint64_t)tuning().pool_pct / 100 / pt * pt : 0;
-    if (tiles < 8ull * a.blocks_per_chunk || pool / pt > (1u << 20)) pool = 0;
-    a.piece_tiles = pt;
-    a.pool_tiles = (uint32_t)pool;
-    a.rec_stride = a.blocks_per_chunk + (uint32_t)(pool / pt);
-    a.pad = tuning().pool_static ? 1u : 0u;
-    rdx_status st;
-    if ((st = ensure(ws, ws->partials, n_chunks * a.rec_stride * kRecordU64, s, true))) return st;
-    if ((st = ensure(ws, ws->tickets, n_chunks * (kTicketWords + kTicketStride), s, true))) return st;
-    a.pool_ctr = ws->tickets.p + n_chunks * kTicketWords;
-    return RDX_OK;
-}
-
 uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
     const uint64_t target = (uint64_t)cus * (uint64_t)tuning().blocks_per_cu;
     uint64_t bpc = (target + n_chunks - 1) / n_chunks;
@@ -303,7 +281,8 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             KAllContig a = p.all_contig;
             const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus);
-            if ((st = set_pool(ws, a, (a.n + te - 1) / te, n_chunks, s))) return st;
+            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kRecordU64, s, true))) return st;
+            if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
             out.tickets = ws->tickets.p;
             a.src = ksrc;
@@ -369,7 +348,8 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 if ((st = ensure(ws, ws->ptrs, a.n_out, s))) return st;
                 if ((st = upload(ws, (void *)ws->ptrs.p, rows.data(), a.n_out * sizeof(void *), ws->last_ptrs, s)))
                     return st;
-                if ((st = set_pool(ws, c, (c.n + te - 1) / te, a.n_out, s))) return st;
+                if ((st = ensure(ws, ws->partials, a.n_out * c.blocks_per_chunk * kRecordU64, s, true))) return st;
+                if ((st = ensure(ws, ws->tickets, a.n_out * kTicketWords, s, true))) return st;
                 c.src = ksrc;
                 c.src.base = nullptr;
                 c.src.ptrs = ws->ptrs.p;
