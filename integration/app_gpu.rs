@@ -56,6 +56,41 @@ pub fn operation_gpu<T: operation::Operation>(
     debug_span!("operation_gpu").in_scope(|| T::execute(&request_data, vec))
 }
 
+/// A handler variant whose response body the engine serialises (operations_gpu::execute_cbor): the same
+/// permits, chunk store and thread-pool choice as `operation_handler` (app.rs:123-153), then the CBOR
+/// bytes go out with the header `IntoResponse for models::Response` sets (app.rs:31-43).  Route e.g.
+/// `/v2/count` to `operation_handler_cbor::<0>` when responses carry large count vectors.
+pub async fn operation_handler_cbor<const OP: u32>(
+    axum::extract::State(state): axum::extract::State<crate::app_state::SharedAppState>,
+    auth: Option<axum_extra::TypedHeader<headers::Authorization<headers::authorization::Basic>>>,
+    crate::validated_json::ValidatedJson(request_data): crate::validated_json::ValidatedJson<models::RequestData>,
+) -> Result<axum::response::Response, ActiveStorageError> {
+    use axum::response::IntoResponse;
+    let memory = request_data.size.unwrap_or(0);
+    let mem_permits = state.resource_manager.memory(memory).await?;
+    let data = state.chunk_store.get(&auth, &request_data, &state.resource_manager, mem_permits).await?;
+    let run = move || -> Result<Bytes, ActiveStorageError> {
+        // a lone compressed chunk is inflated on the host, as in operation_gpu
+        let (request_data, data) = match request_data.compression {
+            Some(c) => {
+                let d = compression::decompress(c, &data)?;
+                let mut rd = request_data;
+                rd.compression = None;
+                (rd, d)
+            }
+            None => (request_data, data),
+        };
+        debug_span!("operation_gpu_cbor").in_scope(|| operations_gpu::execute_cbor::<OP>(&request_data, &data))
+    };
+    let body = if state.args.use_rayon {
+        tokio_rayon::spawn(run).await?
+    } else {
+        let _task_permit = state.resource_manager.task().await?;
+        run()?
+    };
+    Ok((axum::http::StatusCode::OK, [(axum::http::header::CONTENT_TYPE, "application/cbor")], body).into_response())
+}
+
 // `operation_handler` body change (app.rs:147-152):
 //
 //     if state.args.use_rayon {

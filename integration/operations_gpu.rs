@@ -73,6 +73,42 @@ impl<const OP: u32> Operation for Gpu<OP> {
     }
 }
 
+/// The response of `Gpu<OP>` as the reference's HTTP body — `serde_cbor::to_vec(&CBORResponse::new(..))`
+/// (app.rs:33-40, models.rs:355-416) — serialised by the engine on the device (`rdx_execute_cbor`):
+/// a large count vector (axis reductions with many outputs, `axis: []`) crosses PCIe as CBOR integers
+/// (1 byte for a 0 / 1 count) instead of 8-byte values, and no host-side serialisation runs.  The bytes
+/// live in the engine's page-locked block until the HTTP response is dropped.
+pub fn execute_cbor<const OP: u32>(rd: &models::RequestData, data: &[u8]) -> Result<Bytes, ActiveStorageError> {
+    let req = Marshalled::new(rd, OP)?;
+    let flags = if rd.option_shape_as_bytes.unwrap_or(false) { RDX_CBOR_SHAPE_AS_BYTES } else { 0 }
+        | if rd.option_count_as_bytes.unwrap_or(false) { RDX_CBOR_COUNT_AS_BYTES } else { 0 };
+    let mut res: *mut RdxResult = std::ptr::null_mut();
+    check(
+        unsafe {
+            rdx_execute_cbor(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, flags, &mut res)
+        },
+        rd.compression,
+    )?;
+    Ok(Bytes::from_owner(OwnedCbor(res)))
+}
+
+/// An `RdxResult` of rdx_execute_cbor owned by a `Bytes`.
+struct OwnedCbor(*mut RdxResult);
+unsafe impl Send for OwnedCbor {}
+unsafe impl Sync for OwnedCbor {}
+
+impl AsRef<[u8]> for OwnedCbor {
+    fn as_ref(&self) -> &[u8] {
+        unsafe { std::slice::from_raw_parts((*self.0).body as *const u8, (*self.0).cbor_bytes as usize) }
+    }
+}
+
+impl Drop for OwnedCbor {
+    fn drop(&mut self) {
+        unsafe { rdx_result_free(ctx(), self.0) }
+    }
+}
+
 /// An `RdxResult` owned by a `Bytes` (freed back to the engine's pool on drop).
 struct Owned(*mut RdxResult);
 unsafe impl Send for Owned {}
