@@ -3,8 +3,8 @@
  *
  * This is the boundary a Reductionist host (Rust, through `extern "C"`) binds to replace the
  * synchronous part of a request: `operation<T>()` in src/app.rs:163-183, i.e.
- *   filter_pipeline()            src/filter_pipeline.rs:19-34 (gzip / zlib decompression, byte unshuffle;
- *                                blosc2 is not on the device, see RDX_E_UNSUPPORTED)
+ *   filter_pipeline()            src/filter_pipeline.rs:19-34 (gzip / zlib / blosc2 decompression, byte
+ *                                unshuffle)
  *   validate_raw_size()          src/app.rs:169-172 -> src/models.rs:214-239
  *   T::execute(&RequestData,..)  src/operation.rs:53-96 -> src/operations.rs (Count/Max/Min/Select/Sum)
  *   build_array + slicing        src/array.rs:18-208 (byte-order swap, hyperslab)
@@ -41,17 +41,19 @@ typedef enum rdx_status {
     RDX_E_SHUFFLE_LENGTH = 6,      /* shuffle.rs:21 assert_eq!(len % element_size, 0) — reference panics    */
     RDX_E_NAN_UNORDERED = 7,       /* operations.rs:181-183,355-357 NaN in min/max — reference panics with
                                       "unexpected undefined order error for min"                            */
-    RDX_E_UNSUPPORTED = 8,         /* compression blosc2 (not on the device) / rank > 32                    */
+    RDX_E_UNSUPPORTED = 8,         /* a blosc2 codec / filter not decoded on the device (RDX_BLOSC2_UNSUPPORTED:
+                                      zstd, snappy, zlib-coded streams, dictionaries, delta) / rank > 32  */
     RDX_E_DEVICE = 9,              /* HIP runtime error                                                      */
     RDX_E_OUT_OF_MEMORY = 10,      /* device or pinned allocation failed                                     */
     RDX_E_BUFFER_TOO_SMALL = 11,   /* caller-provided output buffer smaller than rdx_plan() reported        */
     RDX_E_NO_DEVICE = 12,          /* no usable gfx950 device                                                */
-    RDX_E_DECOMPRESSION = 13       /* compression.rs:18-82 gzip/zlib stream invalid: ActiveStorageError::
-                                      DecompressionFlate2 / DecompressionZune (HTTP 400, error.rs:247-249);
-                                      the rdx_inflate_error detail: rdx_inflate_last_error()            */
+    RDX_E_DECOMPRESSION = 13       /* compression.rs:18-82 gzip/zlib/blosc2 stream invalid: ActiveStorageError::
+                                      DecompressionFlate2 / DecompressionZune / DecompressionBlosc2 (HTTP
+                                      400, error.rs:247-249); the rdx_inflate_error detail:
+                                      rdx_inflate_last_error()                                          */
 } rdx_status;
 
-/* Why a gzip / zlib stream failed to decompress (RDX_E_DECOMPRESSION).  The reference's messages are
+/* Why a gzip / zlib / blosc2 stream failed to decompress (RDX_E_DECOMPRESSION).  The reference's messages are
  * reproduced by rdx_inflate_error_string where its tests pin them (compression.rs:166-190). */
 typedef enum rdx_inflate_error {
     RDX_INFLATE_OK = 0,
@@ -65,7 +67,13 @@ typedef enum rdx_inflate_error {
     RDX_INFLATE_BAD_SYMBOL = 8,      /* a bit pattern with no code, or a length/distance symbol >= 286/30 */
     RDX_INFLATE_DISTANCE = 9,        /* back-reference before the start of the output                    */
     RDX_INFLATE_CHECKSUM = 10,       /* gzip CRC-32 / ISIZE or zlib Adler-32 mismatch                    */
-    RDX_INFLATE_OUTPUT_OVERFLOW = 11 /* more output than the capacity given (retry with a larger one)    */
+    RDX_INFLATE_OUTPUT_OVERFLOW = 11,/* more output than the capacity given (retry with a larger one)    */
+    /* blosc2 (compression.rs:29-57, ActiveStorageError::DecompressionBlosc2, HTTP 400) */
+    RDX_BLOSC2_INVALID = 12,         /* "invalid blosc2 compressed data": blosc2_cbuffer_sizes -> nbytes 0 */
+    RDX_BLOSC2_FAILED = 13,          /* "failed to decompress blosc2 data": blosc2_decompress <= 0        */
+    RDX_BLOSC2_SIZE = 14,            /* "unexpected decompressed size for blosc2 data"                     */
+    RDX_BLOSC2_UNSUPPORTED = 15      /* a codec / flag not decoded here (zstd, snappy, dictionaries,
+                                        user-defined codecs or filters, delta): status RDX_E_UNSUPPORTED */
 } rdx_inflate_error;
 
 /* ---- request enums (src/models.rs) ------------------------------------------------------------ */
@@ -140,8 +148,7 @@ typedef struct rdx_request {
     const rdx_slice *selection;    /* ndim entries or NULL */
     const uint64_t *axes;          /* n_axes entries or NULL */
     uint32_t n_filters;
-    uint32_t compression;          /* rdx_compression: GZIP/ZLIB decompressed on the device; BLOSC2 ->
-                                      RDX_E_UNSUPPORTED */
+    uint32_t compression;          /* rdx_compression: decompressed on the device (k_inflate / k_blosc2) */
     const rdx_filter *filters;     /* n_filters entries, in REQUEST order (decoded in reverse) */
     rdx_missing missing;
     uint32_t has_size;             /* RequestData.size is Some(..): app.rs:169 skips validate_raw_size */
@@ -186,6 +193,11 @@ rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out);
 /* Message for an rdx_inflate_error, and the detail of this thread's last RDX_E_DECOMPRESSION. */
 const char *rdx_inflate_error_string(uint32_t code);
 uint32_t rdx_inflate_last_error(void);
+/* blosc2_cbuffer_sizes (src/compression.rs:33, blusc 0.0.2 / c-blosc2): the sizes a blosc chunk's
+ * 16-byte header states; all three 0 when it is not a valid header (the reference's "invalid blosc2
+ * compressed data").  Host only: sizes the output of rdx_decompress_batch_device. */
+rdx_status rdx_blosc2_cbuffer_sizes(const void *src, uint64_t len, uint64_t *nbytes, uint64_t *cbytes,
+                                    uint64_t *blocksize);
 
 /* Page-locked host buffers: a host that downloads chunks straight into these (s3_client.rs:215-233
  * today copies into an 8-byte aligned Vec) lets rdx_execute DMA them without a staging copy, and
@@ -197,7 +209,7 @@ void rdx_host_free(rdx_context *ctx, void *p);
 /* ---- execution ------------------------------------------------------------------------------------ */
 /* Host-resident chunk in, host-resident response out (the drop-in for operation<T>()).
  * `chunk` is borrowed read-only; body/counts are caller-provided with capacities from rdx_plan.
- * Blocks until the response is in host memory.  A gzip/zlib chunk crosses PCIe compressed and is
+ * Blocks until the response is in host memory.  A gzip/zlib/blosc2 chunk crosses PCIe compressed and is
  * inflated on the device (k_inflate); info describes the response of the decompressed chunk. */
 rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req,
                        const void *chunk, uint64_t chunk_len,
@@ -240,7 +252,7 @@ typedef struct rdx_workspace rdx_workspace;
 rdx_status rdx_workspace_create(rdx_context *ctx, int device, rdx_workspace **out);
 void rdx_workspace_destroy(rdx_workspace *ws);
 
-/* A compressed request (gzip/zlib) is inflated into workspace scratch first; the call then waits on
+/* A compressed request (gzip/zlib/blosc2) is decompressed into workspace scratch first; the call then waits on
  * `stream` once for the decompressed length before launching the operation. */
 rdx_status rdx_execute_device(rdx_workspace *ws, const rdx_request *req,
                               const void *d_chunk, uint64_t chunk_len,
@@ -282,12 +294,14 @@ typedef struct rdx_multi_item {
 rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_multi_item *items, void *stream,
                                     uint32_t *statuses, rdx_response_info *infos);
 
-/* compression::decompress (src/compression.rs:18-27, gzip and zlib) for a batch of n device-resident
+/* compression::decompress (src/compression.rs:18-27: gzip, zlib, blosc2) for a batch of n device-resident
  * compressed streams, asynchronous on `stream`: stream i (h_in_ptrs[i] device pointer, h_in_lens[i]
  * bytes; HOST arrays) is inflated into d_out + i*out_capacity (out_capacity a multiple of 16, d_out
  * 16-byte aligned); d_out_lens[i] = bytes produced, d_errors[i] = rdx_inflate_error (device arrays).
  * RDX_INFLATE_OUTPUT_OVERFLOW means the stream needs more than out_capacity: the caller retries that
- * stream with a larger capacity.  rdx_execute / rdx_execute_device call this for a compressed
+ * stream with a larger capacity (for blosc2, d_out_lens[i] then holds the size the header states).
+ * gzip / zlib: one wavefront per stream (k_inflate); blosc2: one wavefront per block stream, every chunk
+ * spread over many (k_blosc2), so a lone blosc2 chunk decodes in parallel.  rdx_execute / rdx_execute_device call this for a compressed
  * request (then synchronise once to learn the decompressed length) before planning the operation. */
 rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, uint64_t n,
                                        const void *const *h_in_ptrs, const uint64_t *h_in_lens,

@@ -1,0 +1,123 @@
+"""This repo's own blosc2 chunk WRITER — test infrastructure only (fixtures for the blosc2 decoder).
+
+The reference only decompresses blosc2 (src/compression.rs:29-57, via the un-vendored blusc 0.0.2, a
+pure-Rust port of c-blosc2); its one test compresses b"hello world" with blusc itself
+(compression.rs:90-110).  With no blosc2 library in this image, chunks are assembled here from the
+published c-blosc2 chunk format (README_CHUNK_FORMAT): header (16 bytes, or 32 with the extended
+blosc2 fields when flags carry both shuffle bits), bstarts, per block `typesize` split streams (or one),
+each a signed 32-bit csize followed by a BloscLZ / LZ4 / zlib stream, a raw copy (csize == stream
+size), a zero run (csize 0) or a byte run (csize = -byte, token byte 1); memcpy'ed and special-value
+chunks.  Filters run forward per block (filters[0] first): byte shuffle, bitshuffle.  The LZ encoders
+are oracle_blosc2.cpp's (greedy, this repo's own), so a decoder matching these chunks is checked
+against the format description, not against c-blosc2's bytes ("parity unpinned").
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+
+import numpy as np
+
+from . import py_oracle
+
+BLOSCLZ, LZ4, ZLIB, ZSTD = 0, 1, 3, 4
+NOFILTER, SHUFFLE, BITSHUFFLE, DELTA, TRUNC = 0, 1, 2, 3, 4
+
+
+def shuffle_block(b: bytes, ts: int) -> bytes:
+    ne = len(b) // ts
+    if ts <= 1 or ne == 0:
+        return b
+    a = np.frombuffer(b[: ne * ts], np.uint8).reshape(ne, ts)
+    return a.T.tobytes() + b[ne * ts:]
+
+
+def bitshuffle_block(b: bytes, ts: int) -> bytes:
+    size = len(b) // ts
+    size -= size % 8
+    if size == 0:
+        return b
+    a = np.frombuffer(b[: size * ts], np.uint8).reshape(size, ts)
+    bits = np.unpackbits(a[:, :, None], axis=2, bitorder="little")      # [elem][byte][bit]
+    rows = np.packbits(bits.transpose(1, 2, 0), axis=2, bitorder="little")  # [byte][bit][elem / 8]
+    return rows.tobytes() + b[size * ts:]
+
+
+def _stream(codec: int, s: bytes, mode: str) -> bytes:
+    n = len(s)
+    if mode == "auto" and n and s.count(s[0]) == n:
+        return struct.pack("<i", 0) if s[0] == 0 else struct.pack("<iB", -s[0], 1)
+    if mode == "raw":
+        return struct.pack("<i", n) + s
+    if codec in (BLOSCLZ, LZ4):
+        c = py_oracle.blosc2_lz(codec, s)
+    elif codec == ZLIB:
+        c = zlib.compress(s, 6)
+    else:
+        raise ValueError(codec)
+    if len(c) >= n:
+        return struct.pack("<i", n) + s
+    return struct.pack("<i", len(c)) + c
+
+
+def build(data: bytes, typesize: int = 4, blocksize: int | None = None, codec: int = BLOSCLZ,
+          filters=(0, 0, 0, 0, 0, SHUFFLE), split: bool = True, version: int = 5, memcpyed: bool | None = None,
+          stream_mode: str = "auto", b2flags: int = 0) -> bytes:
+    """One chunk.  version 5: extended 32-byte header with the filter pipeline; version 2: the 16-byte
+    blosc1 header (filters from the flag bits).  memcpyed None: only when compressing does not pay."""
+    nbytes = len(data)
+    if blocksize is None:
+        blocksize = min(nbytes, 64 * 1024) or 1
+    blocksize = max(1, min(blocksize, max(nbytes, 1)))
+    ext = version >= 3
+    overhead = 32 if ext else 16
+    flags = codec << 5
+    fl = list(filters)
+    if ext:
+        flags |= 0x05
+    else:
+        if SHUFFLE in fl:
+            flags |= 0x01
+        if BITSHUFFLE in fl:
+            flags |= 0x04
+    if not split:
+        flags |= 0x10
+
+    def header(fl_, cbytes):
+        h = struct.pack("<BBBBiii", version, 1, fl_, typesize, nbytes, blocksize, cbytes)
+        if ext:
+            h += bytes(fl[:6]) + bytes([0, 0]) + bytes(6) + bytes([0, b2flags])
+        return h
+
+    nblocks = (nbytes + blocksize - 1) // blocksize
+    leftover = nbytes % blocksize
+    body = bytearray()
+    bstarts = []
+    base = overhead + 4 * nblocks
+    for j in range(nblocks):
+        left = leftover and j == nblocks - 1
+        blk = data[j * blocksize: j * blocksize + (leftover if left else blocksize)]
+        for f in fl:
+            if f == SHUFFLE:
+                blk = shuffle_block(blk, typesize)
+            elif f == BITSHUFFLE:
+                blk = bitshuffle_block(blk, typesize)
+        ns = typesize if (split and not left) else 1
+        ne = len(blk) // ns
+        bstarts.append(base + len(body))
+        for k in range(ns):
+            body += _stream(codec, blk[k * ne:(k + 1) * ne], stream_mode)
+    cbytes = base + len(body)
+    if memcpyed is None:
+        memcpyed = cbytes >= nbytes + overhead
+    if memcpyed:
+        return header(flags | 0x02, nbytes + overhead) + data
+    return header(flags, cbytes) + struct.pack(f"<{nblocks}i", *bstarts) + bytes(body)
+
+
+def special(nbytes: int, typesize: int, kind: int, value: bytes = b"") -> bytes:
+    """A special-value chunk (blosc2_flags bits 4-6: 1 zeros, 2 NaN, 3 a repeated value, 4 uninit)."""
+    cbytes = 32 + (len(value) if kind == 3 else 0)
+    h = struct.pack("<BBBBiii", 5, 1, 0x05, typesize, nbytes, max(1, min(nbytes, 1 << 16)), cbytes)
+    h += bytes(6) + bytes([0, 0]) + bytes(6) + bytes([0, kind << 4])
+    return h + (value if kind == 3 else b"")

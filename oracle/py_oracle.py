@@ -41,6 +41,12 @@ def lib():
         L.oracle_decompress.argtypes = [C.c_uint32, VP, U64, VP, U64, C.POINTER(C.c_uint64)]
         L.oracle_inflate_last_error.restype = C.c_uint32
         L.oracle_inflate_last_error.argtypes = []
+        L.oracle_blosc2_sizes.restype = None
+        L.oracle_blosc2_sizes.argtypes = [VP, U64, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]
+        L.oracle_blosc2_decompress.restype = C.c_uint32
+        L.oracle_blosc2_decompress.argtypes = [VP, U64, VP, U64, C.POINTER(U64)]
+        L.oracle_blosc2_lz_compress.restype = C.c_int64
+        L.oracle_blosc2_lz_compress.argtypes = [C.c_uint32, VP, U64, U64, VP, U64]
         L.oracle_missing_convert.restype = C.c_int
         L.oracle_missing_convert.argtypes = [C.c_uint32, C.c_uint32, C.c_int64, C.c_uint64, C.c_double, VP]
         _LIB = L
@@ -123,3 +129,32 @@ def decompress(compression: int, data: bytes, cap: int | None = None):
     src = C.create_string_buffer(bytes(data), max(1, len(data)))
     e = L.oracle_decompress(compression, src, len(data), out, cap, C.byref(got))
     return int(e), bytes(out)[: min(got.value, cap)]
+
+
+def blosc2_sizes(data: bytes):
+    """blosc2_cbuffer_sizes (compression.rs:33) restated (oracle_blosc2.cpp): (nbytes, cbytes, blocksize)."""
+    a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    lib().oracle_blosc2_sizes(src, len(data), C.byref(a), C.byref(b), C.byref(c))
+    return a.value, b.value, c.value
+
+
+def blosc2_decompress(data: bytes, cap: int | None = None):
+    """decompress_blusc_blosc2 (compression.rs:29-57) restated: (rdx_inflate_error, bytes)."""
+    if cap is None:
+        cap = max(blosc2_sizes(data)[0], 1)
+    out = (C.c_uint8 * max(1, cap))()
+    got = C.c_uint64(0)
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    e = lib().oracle_blosc2_decompress(src, len(data), out, cap, C.byref(got))
+    return int(e), bytes(out)[: min(got.value, cap)]
+
+
+def blosc2_lz(codec: int, data: bytes, max_dist: int = 8191 + 65535) -> bytes:
+    """This repo's own BloscLZ (codec 0) / LZ4 (codec 1) stream encoder (test fixtures only)."""
+    cap = 2 * len(data) + 64
+    out = (C.c_uint8 * cap)()
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    n = lib().oracle_blosc2_lz_compress(codec, src, len(data), max_dist, out, cap)
+    assert n >= 0
+    return bytes(out)[:n]

@@ -36,6 +36,10 @@
 #include <type_traits>
 #include <vector>
 
+extern "C" void oracle_blosc2_sizes(const uint8_t *src, uint64_t len, uint64_t *nbytes, uint64_t *cbytes,
+                                   uint64_t *blocksize);
+extern "C" uint32_t oracle_blosc2_decompress(const uint8_t *src, uint64_t len, uint8_t *out, uint64_t cap,
+                                             uint64_t *out_len);
 extern "C" uint32_t oracle_decompress(uint32_t compression, const uint8_t *in, uint64_t len, uint8_t *out,
                                       uint64_t cap, uint64_t *out_len);  // oracle_inflate.cpp
 
@@ -608,8 +612,18 @@ Response operation(const rdx_request &req, const uint8_t *chunk, u64 len) {
             data.resize(got);
             break;
         }
+    } else if (req.compression == RDX_COMPRESSION_BLOSC2) {   // compression.rs:29-57, oracle_blosc2.cpp
+        u64 nbytes = 0, cbytes = 0, bsize = 0, got = 0;
+        oracle_blosc2_sizes(chunk, len, &nbytes, &cbytes, &bsize);
+        data.resize(nbytes ? nbytes : 1);
+        const uint32_t e = nbytes ? oracle_blosc2_decompress(chunk, len, data.data(), nbytes, &got) : RDX_BLOSC2_INVALID;
+        if (e != RDX_INFLATE_OK) {
+            g_inflate_error = e;
+            throw OracleError{e == RDX_BLOSC2_UNSUPPORTED ? RDX_E_UNSUPPORTED : RDX_E_DECOMPRESSION};
+        }
+        data.resize(got);
     } else if (req.compression != RDX_COMPRESSION_NONE) {
-        throw OracleError{RDX_E_UNSUPPORTED};  // blosc2: no restatement (the blusc crate is un-vendored)
+        throw OracleError{RDX_E_INVALID_ARGUMENT};
     } else {
         data.assign(chunk, chunk + len);
     }

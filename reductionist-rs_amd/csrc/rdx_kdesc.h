@@ -181,6 +181,20 @@ struct KCbor {
     uint8_t tail[kCborTailMax];     // D then F
 };
 
+// blosc2 chunks (k_blosc2.hip): chunk i = in[i] (in_len[i] bytes) -> out + i * cap; the decode
+// scratch (same layout) holds the filtered blocks until k_blosc2_filter writes them into out.
+struct KBlosc2Args {
+    const uint8_t *const *in;   // device array of chunk pointers
+    const uint64_t *in_len;     // device array of chunk lengths
+    uint8_t *out;
+    uint8_t *scratch;           // n * cap bytes (may be null when no chunk has an active filter)
+    uint64_t cap;
+    uint64_t *out_len;          // nbytes (also on RDX_INFLATE_OUTPUT_OVERFLOW, so the caller can resize)
+    uint32_t *err;              // rdx_inflate_error; zeroed by the caller before the launch
+    uint32_t n;
+    uint32_t wg_per_chunk;      // workgroups (4 decoding waves each) per chunk
+};
+
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]
 // (operations.rs:188-210, :58-67).  out index g -> element offset via `view` (dims
 // innermost-first in OUTPUT order).

@@ -304,9 +304,8 @@ rdx_status make_plan(const rdx_request &req, uint64_t len, ExecPlan &p) {
     p.is_float = is_float_dtype(req.dtype);
     p.need_rank = p.is_float && (req.op == RDX_OP_MIN || req.op == RDX_OP_MAX);
 
-    // filter_pipeline.rs:23-25 — gzip/zlib are inflated on the device BEFORE planning (k_inflate.hip), so
-    // `len` is the decompressed length here; blosc2 is not on the device.
-    if (req.compression == RDX_COMPRESSION_BLOSC2) return RDX_E_UNSUPPORTED;
+    // filter_pipeline.rs:23-25 — gzip/zlib/blosc2 are decompressed on the device BEFORE planning
+    // (k_inflate.hip, k_blosc2.hip), so `len` is the decompressed length here.
     for (uint32_t k = 0; k < req.n_filters; ++k) {
         const uint64_t es = req.filters[k].element_size;
         if (es == 0 || len % es != 0) return RDX_E_SHUFFLE_LENGTH;  // shuffle.rs:21 assert

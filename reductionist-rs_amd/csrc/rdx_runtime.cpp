@@ -105,6 +105,7 @@ struct rdx_workspace {
     DevBuf<uint64_t> zout_len;
     DevBuf<uint32_t> zerr;
     DevBuf<uint8_t> raw;
+    DevBuf<uint8_t> zscratch;   // blosc2: decoded blocks before their filters (k_blosc2_filter)
     std::vector<uint8_t> last_zptrs, last_zlens;
     // rdx_execute_cbor: the encoded response and its length
     DevBuf<uint8_t> cbor;
@@ -492,6 +493,24 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
     if ((st = ensure(ws, ws->zlens, n, s))) return st;
     if ((st = upload(ws, (void *)ws->zptrs.p, h_ptrs, n * sizeof(void *), ws->last_zptrs, s))) return st;
     if ((st = upload(ws, ws->zlens.p, h_lens, n * sizeof(uint64_t), ws->last_zlens, s))) return st;
+    if (compression == RDX_COMPRESSION_BLOSC2) {
+        if (n > 0xffffffffull) return RDX_E_INVALID_ARGUMENT;
+        if ((st = ensure(ws, ws->zscratch, n * cap, s))) return st;
+        RDX_HIP(hipMemsetAsync(d_err, 0, n * sizeof(uint32_t), s));
+        KBlosc2Args a{};
+        a.in = ws->zptrs.p;
+        a.in_len = ws->zlens.p;
+        a.out = d_out;
+        a.scratch = ws->zscratch.p;
+        a.cap = cap;
+        a.out_len = d_out_len;
+        a.err = d_err;
+        a.n = (uint32_t)n;
+        // waves per chunk: enough for one chunk's streams to fill the chip (4 waves per workgroup)
+        a.wg_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(128, 1024 / n));
+        RDX_HIP(launch_blosc2(a, true, s));
+        return RDX_OK;
+    }
     RDX_HIP(launch_inflate(compression, ws->zptrs.p, ws->zlens.p, n, d_out, cap, d_out_len, d_err, s));
     return RDX_OK;
 }
@@ -504,8 +523,8 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
 rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const uint8_t *d_src, uint64_t len,
                               uint64_t size_hint, hipStream_t s, uint64_t *raw_len) {
     g_inflate_error = RDX_INFLATE_OK;
-    if (req.compression == RDX_COMPRESSION_BLOSC2) return RDX_E_UNSUPPORTED;
-    if (req.compression != RDX_COMPRESSION_GZIP && req.compression != RDX_COMPRESSION_ZLIB)
+    const bool blosc2 = req.compression == RDX_COMPRESSION_BLOSC2;
+    if (req.compression != RDX_COMPRESSION_GZIP && req.compression != RDX_COMPRESSION_ZLIB && !blosc2)
         return RDX_E_INVALID_ARGUMENT;
     uint64_t cap = size_hint;
     if (req.ndim && req.shape && req.dtype <= RDX_DTYPE_FLOAT64) {
@@ -514,6 +533,7 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
         for (uint32_t k = 0; k < req.ndim; ++k) ovf |= __builtin_mul_overflow(e, req.shape[k], &e);
         if (!ovf) cap = e;
     }
+    if (blosc2 && size_hint) cap = size_hint;   // the header's nbytes (read on the host)
     if (cap == 0) cap = 4 * len + 4096;
     rdx_status st;
     if ((st = ensure(ws, ws->zout_len, 1, s))) return st;
@@ -532,12 +552,13 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
         const uint32_t e = (uint32_t)ws->zback[1];
         if (e == RDX_INFLATE_OUTPUT_OVERFLOW) {
             if (cap >= (1ull << 40)) return RDX_E_OUT_OF_MEMORY;
-            cap *= 4;
+            // a blosc2 header states its size (k_blosc2 reports it with the overflow)
+            cap = blosc2 && ws->zback[0] > cap ? ws->zback[0] : cap * 4;
             continue;
         }
         if (e != RDX_INFLATE_OK) {
             g_inflate_error = e;
-            return RDX_E_DECOMPRESSION;
+            return e == RDX_BLOSC2_UNSUPPORTED ? RDX_E_UNSUPPORTED : RDX_E_DECOMPRESSION;
         }
         *raw_len = ws->zback[0];
         return RDX_OK;
@@ -813,8 +834,6 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
         if ((st = make_plan(req, chunk_len, p))) return st;
         *info = p.info;
         if ((st = bind(p.info, &body, &counts))) return st;
-    } else if (req.compression == RDX_COMPRESSION_BLOSC2) {
-        return RDX_E_UNSUPPORTED;
     }
 
     // take a workspace (round-robin device, then any free workspace of it)
@@ -855,6 +874,10 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             if (req.compression == RDX_COMPRESSION_GZIP && chunk_len >= 18) {  // RFC 1952 ISIZE
                 const uint8_t *t = chunk + chunk_len - 4;
                 hint = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+            }
+            if (req.compression == RDX_COMPRESSION_BLOSC2) {  // blosc2_cbuffer_sizes, compression.rs:33
+                uint64_t cb = 0, bs = 0;
+                rdx_blosc2_cbuffer_sizes(chunk, chunk_len, &hint, &cb, &bs);
             }
             if ((r = decompress_request(ws, req, ws->chunk.p, chunk_len, hint, s, &len))) return r;
             src = ws->raw.p;
@@ -947,11 +970,35 @@ const char *rdx_inflate_error_string(uint32_t code) {
         case RDX_INFLATE_DISTANCE: return "invalid distance too far back";
         case RDX_INFLATE_CHECKSUM: return "checksum mismatch";
         case RDX_INFLATE_OUTPUT_OVERFLOW: return "decompressed data larger than the output buffer";
+        case RDX_BLOSC2_INVALID: return "invalid blosc2 compressed data";                  // compression.rs:37
+        case RDX_BLOSC2_FAILED: return "failed to decompress blosc2 data";                 // compression.rs:47
+        case RDX_BLOSC2_SIZE: return "unexpected decompressed size for blosc2 data";       // compression.rs:52
+        case RDX_BLOSC2_UNSUPPORTED: return "blosc2 codec or filter not supported by the device engine";
     }
     return "unknown decompression error";
 }
 
 uint32_t rdx_inflate_last_error(void) { return g_inflate_error; }
+
+// blosc2_cbuffer_sizes (blusc 0.0.2 / c-blosc2 read_chunk_header on the first 16 bytes), as the
+// reference calls it (compression.rs:33): all zeros when the header is not a valid blosc chunk.
+rdx_status rdx_blosc2_cbuffer_sizes(const void *src, uint64_t len, uint64_t *nbytes, uint64_t *cbytes,
+                                    uint64_t *blocksize) {
+    if ((!src && len) || !nbytes || !cbytes || !blocksize) return RDX_E_INVALID_ARGUMENT;
+    *nbytes = *cbytes = *blocksize = 0;
+    if (len < 16) return RDX_OK;
+    const uint8_t *h = static_cast<const uint8_t *>(src);
+    auto rd = [&](int k) {
+        return (int32_t)((uint32_t)h[k] | (uint32_t)h[k + 1] << 8 | (uint32_t)h[k + 2] << 16 | (uint32_t)h[k + 3] << 24);
+    };
+    const int32_t nb = rd(4), bs = rd(8), cb = rd(12);
+    if (cb < 16 || h[0] == 0 || h[0] > 5 || bs <= 0 || (nb > 0 && bs > nb) || bs > 536866816 || h[3] == 0 || nb <= 0)
+        return RDX_OK;
+    *nbytes = (uint64_t)nb;
+    *cbytes = (uint64_t)cb;
+    *blocksize = (uint64_t)bs;
+    return RDX_OK;
+}
 
 int rdx_device_count(void) {
     int n = 0;
@@ -1284,8 +1331,9 @@ rdx_status rdx_cbor_encode_device(rdx_workspace *ws, const rdx_response_info *in
 rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, uint64_t n,
                                        const void *const *h_in_ptrs, const uint64_t *h_in_lens, void *d_out,
                                        uint64_t out_capacity, uint64_t *d_out_lens, uint32_t *d_errors, void *stream) {
-    if (compression == RDX_COMPRESSION_BLOSC2) return RDX_E_UNSUPPORTED;
-    if (!ws || (compression != RDX_COMPRESSION_GZIP && compression != RDX_COMPRESSION_ZLIB)) return RDX_E_INVALID_ARGUMENT;
+    if (!ws || (compression != RDX_COMPRESSION_GZIP && compression != RDX_COMPRESSION_ZLIB &&
+                compression != RDX_COMPRESSION_BLOSC2))
+        return RDX_E_INVALID_ARGUMENT;
     if (n == 0) return RDX_OK;
     if (!h_in_ptrs || !h_in_lens || !d_out || !d_out_lens || !d_errors || out_capacity % 16 ||
         (uintptr_t)d_out % 16)

@@ -25,7 +25,8 @@ OK, E_INVALID_ARGUMENT, E_REQUEST_VALIDATION, E_FROM_BYTES, E_SHAPE_INVALID, E_I
 # rdx_inflate_error (detail of E_DECOMPRESSION)
 INFLATE_OK, INFLATE_GZIP_HEADER, INFLATE_ZLIB_METHOD, INFLATE_ZLIB_HEADER, INFLATE_TRUNCATED, \
     INFLATE_BLOCK_TYPE, INFLATE_STORED_LENGTH, INFLATE_CODE_LENGTHS, INFLATE_BAD_SYMBOL, INFLATE_DISTANCE, \
-    INFLATE_CHECKSUM, INFLATE_OUTPUT_OVERFLOW = range(12)
+    INFLATE_CHECKSUM, INFLATE_OUTPUT_OVERFLOW, BLOSC2_INVALID, BLOSC2_FAILED, BLOSC2_SIZE, \
+    BLOSC2_UNSUPPORTED = range(16)
 
 OPS = {"count": 0, "max": 1, "min": 2, "select": 3, "sum": 4}
 DTYPES = {"int32": 0, "int64": 1, "uint32": 2, "uint64": 3, "float32": 4, "float64": 5}
@@ -164,6 +165,7 @@ def _declare(lib):
         "rdx_inflate_error_string": (C.c_char_p, [C.c_uint32]),
         "rdx_inflate_last_error": (C.c_uint32, []),
         "rdx_decompress_batch_device": (C.c_int, [VP, C.c_uint32, U64, P(VP), P(U64), VP, U64, VP, VP, VP]),
+        "rdx_blosc2_cbuffer_sizes": (C.c_int, [VP, U64, P(U64), P(U64), P(U64)]),
         "rdx_execute_multi_device": (C.c_int, [VP, U64, P(rdx_multi_item), VP, P(C.c_uint32), info_p]),
         "rdx_execute_owned": (C.c_int, [VP, req_p, VP, U64, P(P(rdx_result))]),
         "rdx_result_free": (None, [VP, P(rdx_result)]),
@@ -187,7 +189,7 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
             "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
             "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device",
-            "rdx_execute_cbor"]
+            "rdx_execute_cbor", "rdx_blosc2_cbuffer_sizes"]
 
 
 def lib():
@@ -214,3 +216,12 @@ def status_string(code: int) -> str:
 
 def inflate_error_string(code: int) -> str:
     return lib().rdx_inflate_error_string(code).decode()
+
+
+def blosc2_cbuffer_sizes(data: bytes):
+    """blosc2_cbuffer_sizes (compression.rs:33) through the C ABI: (nbytes, cbytes, blocksize)."""
+    a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    st = lib().rdx_blosc2_cbuffer_sizes(buf, len(data), C.byref(a), C.byref(b), C.byref(c))
+    assert st == OK
+    return a.value, b.value, c.value

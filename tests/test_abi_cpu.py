@@ -61,7 +61,6 @@ def test_plan_matches_oracle_random():
 def test_plan_error_order_matches_oracle():
     """operation<T>() raises its first error in a fixed order (app.rs:163-183)."""
     cases = [
-        ("sum", {"dtype": "int32", "compression": "blosc2", "size": 8}, 8, _abi.E_UNSUPPORTED),
         ("sum", {"dtype": "int32", "filters": [{"id": "shuffle", "element_size": 3}]}, 8, _abi.E_SHUFFLE_LENGTH),
         ("sum", {"dtype": "int32", "filters": [{"id": "shuffle", "element_size": 0}]}, 8, _abi.E_SHUFFLE_LENGTH),
         ("sum", {"dtype": "int32"}, 6, _abi.E_REQUEST_VALIDATION),              # validate_raw_size
@@ -84,6 +83,11 @@ def test_plan_error_order_matches_oracle():
     assert oracle.execute(creq, bytes(8))[0] == _abi.E_DECOMPRESSION
     assert lib.rdx_plan(creq.ref, 8, C.byref(_abi.rdx_response_info())) == 0
     assert lib.rdx_plan(creq.ref, 6, C.byref(_abi.rdx_response_info())) == _abi.E_REQUEST_VALIDATION
+    # blosc2 (compression.rs:29-57): 8 zero bytes are no blosc2 header -> "invalid blosc2 compressed data"
+    creq = make_request("sum", {"dtype": "int32", "compression": "blosc2", "size": 8}, oracle.convert)
+    assert oracle.execute(creq, bytes(8))[0] == _abi.E_DECOMPRESSION
+    assert oracle.lib().oracle_inflate_last_error() == _abi.BLOSC2_INVALID
+    assert lib.rdx_plan(creq.ref, 8, C.byref(_abi.rdx_response_info())) == 0
 
 
 def _random_validation_case(rng):

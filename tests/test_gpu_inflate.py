@@ -190,7 +190,8 @@ def test_execute_compression_errors(engine):
     st, info, body, counts = engine.execute_raw(creq, gz(big.tobytes(), 9))
     assert st == 0 and counts == [3 << 20]
     creq = make_request("sum", {"dtype": "int32", "compression": "blosc2"}, product_convert)
-    assert engine.execute_raw(creq, b"\0" * 64)[0] == _abi.E_UNSUPPORTED
+    assert engine.execute_raw(creq, b"\0" * 64)[0] == _abi.E_DECOMPRESSION
+    assert lib.rdx_inflate_last_error() == _abi.BLOSC2_INVALID
 
 
 def test_execute_device_with_compression(torch, workspace):

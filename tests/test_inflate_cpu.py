@@ -130,4 +130,4 @@ def test_operation_with_compression_and_filters():
     assert oracle.lib().oracle_inflate_last_error() == _abi.INFLATE_GZIP_HEADER
     creq = _abi.CRequest("sum", "int32", compression="blosc2")
     st, *_ = oracle.execute(creq, b"\0" * 64)
-    assert st == _abi.E_UNSUPPORTED
+    assert st == _abi.E_DECOMPRESSION and oracle.lib().oracle_inflate_last_error() == _abi.BLOSC2_INVALID
