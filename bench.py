@@ -22,6 +22,7 @@ extra (every number DESIGN.md quotes comes from here):
                          ranks (strong scaling of that batch)
   f64_64mib / f64_4mib   the north_star's f64 legs (shuffle es=8, big-endian, sum)
   c4z_inflate            the batch compressed with zlib, decompressed on the device
+  c4b_blosc2             the batch as blosc2 chunks (LZ4 / BloscLZ + shuffle), decoded on the device
   configs                (N=1) device-resident C1, C3 (min / max / valid_range) and C5 select launches
   mixed_requests         (N=1) 20 mixed C1/C3 requests in ONE heterogeneous launch (rdx_execute_multi_device)
   concurrent_native      (N=1) C1 / C2 / C3 requests from native C++ threads (rdx_conc_bench: own workspace
@@ -509,6 +510,86 @@ def leg_inflate(cx, with_cpu, n_total=1024, distinct=16, reps=3):
     return out
 
 
+def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
+    """The C4 batch shape as blosc2 chunks (compression.rs:29-57): 1024 x 4 MiB f32 chunks of a smooth
+    field quantized to 1/64 (the low mantissa bytes repeat, as in real model output), blosc2 chunks with
+    the SHUFFLE filter, typesize 4, 64 KiB blocks split into 4 streams, written by this repo's own writer
+    (datagen/blosc2_chunk.py; distinct chunks cycled), split over ranks; one rdx_decompress_batch_device
+    launch per rep, per codec.  Also one lone chunk per call (a single request).  GB/s of decompressed
+    output; CPU: the oracle's blosc2 decoder (scalar C++, oracle/oracle_blosc2.cpp) on a thread pool."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from datagen import blosc2_chunk as B
+    from reductionist_amd.sharding import shard_range
+    torch = cx.torch
+    lo, hi = shard_range(n_total, cx.rank, cx.world)
+    n = hi - lo
+    rng = np.random.default_rng(0x5EED2100)
+    raw_len = 4 * C4_ELEMS
+    raws = [(np.round(np.cumsum(rng.standard_normal(C4_ELEMS)) * 64) / 64).astype(np.float32).tobytes()
+            for _ in range(distinct)]
+    out = {"workload": "1024 x 4 MiB f32 chunks (random walk quantized to 1/64) as blosc2 chunks: SHUFFLE, "
+                       "typesize 4, 64 KiB blocks x 4 streams; batch split over ranks, one "
+                       "rdx_decompress_batch_device launch per codec; lone = one chunk per call",
+           "kernel": "k_blosc2_decode + k_blosc2_filter", "unit": "GB/s decompressed (this rank)",
+           "bound": "serial token chain per wavefront (one stream each), not HBM"}
+    d_out = torch.empty(max(1, n) * raw_len, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+    d_err = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
+    chunks_by_codec = {}
+    for name, codec in (("lz4", B.LZ4), ("blosclz", B.BLOSCLZ)):
+        chunks = [B.build(r, 4, 1 << 16, codec, (0, 0, 0, 0, 0, B.SHUFFLE), memcpyed=False) for r in raws]
+        chunks_by_codec[name] = chunks
+        offs, total = [], 0
+        for c in chunks:
+            offs.append(total)
+            total += (len(c) + 255) // 256 * 256
+        host = np.zeros(total, dtype=np.uint8)
+        for o, c in zip(offs, chunks):
+            host[o:o + len(c)] = np.frombuffer(c, dtype=np.uint8)
+        d_in = torch.from_numpy(host).cuda()
+        ptrs = [d_in.data_ptr() + offs[(lo + i) % distinct] for i in range(n)]
+        lens = [len(chunks[(lo + i) % distinct]) for i in range(n)]
+
+        def step(i, k=n):
+            cx.ws.decompress_batch_device("blosc2", ptrs[:k], lens[:k], d_out.data_ptr(), raw_len, d_len.data_ptr(),
+                                          d_err.data_ptr(), cx.stream.cuda_stream)
+
+        step(0)
+        torch.cuda.synchronize()
+        assert int(d_err.abs().sum()) == 0 and bool((d_len == raw_len).all())
+        assert d_out[:raw_len].cpu().numpy().tobytes() == raws[lo % distinct]
+        t = cx.dev_time(step, reps, warm=0)
+        t1 = cx.dev_time(lambda i: step(i, 1), 20, warm=2)
+        ratio = raw_len * distinct / sum(len(c) for c in chunks)
+        out[name] = {"ratio": round(ratio, 3), "value": round(n * raw_len / t / 1e9, 2), "ms_per_launch": round(t * 1e3, 3),
+                     "lone_chunk_us": round(t1 * 1e6, 1), "lone_chunk_GBs": round(raw_len / t1 / 1e9, 2)}
+    if with_cpu:
+        from oracle import py_oracle as oracle
+        import ctypes as C
+        threads = pool_threads()
+        L = oracle.lib()
+        chunks = chunks_by_codec["lz4"]
+        bufs = [C.create_string_buffer(c, len(c)) for c in chunks]
+        outs = [(C.c_uint8 * raw_len)() for _ in range(threads)]
+
+        def one(i):
+            got = C.c_uint64(0)
+            e = L.oracle_blosc2_decompress(bufs[i % distinct], len(chunks[i % distinct]), outs[i % threads], raw_len,
+                                           C.byref(got))
+            assert e == 0
+
+        with ThreadPoolExecutor(threads) as ex:   # ctypes releases the GIL during the call
+            list(ex.map(one, range(threads)))
+            c0 = time.perf_counter()
+            list(ex.map(one, range(n_total)))
+            tz = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": round(n_total * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
+                               "kind": "port", "sample": f"oracle_blosc2_decompress (scalar C++, g++ -O2) of all "
+                                                         f"{n_total} lz4 chunks on a {threads}-thread pool, {tz:.2f} s"}
+    return out
+
+
 def _c3_host():
     import numpy as np
     rng = np.random.default_rng(0x5EED0005)
@@ -977,6 +1058,8 @@ def main():
         extra["f64_4mib"] = leg_f64(cx, 512 * 1024, 128, steps)
     if not args.no_inflate:
         extra["c4z_inflate"] = leg_inflate(cx, solo and not args.no_cpu_baseline)
+    if not args.no_inflate:
+        extra["c4b_blosc2"] = leg_blosc2(cx, solo and not args.no_cpu_baseline)
     if world == 1 and not args.no_configs:
         extra["configs"] = leg_configs(cx)
         extra["mixed_requests"] = leg_mixed(cx)

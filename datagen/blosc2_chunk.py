@@ -1,4 +1,4 @@
-"""This repo's own blosc2 chunk WRITER — test infrastructure only (fixtures for the blosc2 decoder).
+"""This repo's own blosc2 chunk WRITER — synthetic inputs for tests and bench (neither product nor oracle).
 
 The reference only decompresses blosc2 (src/compression.rs:29-57, via the un-vendored blusc 0.0.2, a
 pure-Rust port of c-blosc2); its one test compresses b"hello world" with blusc itself
@@ -8,7 +8,7 @@ blosc2 fields when flags carry both shuffle bits), bstarts, per block `typesize`
 each a signed 32-bit csize followed by a BloscLZ / LZ4 / zlib stream, a raw copy (csize == stream
 size), a zero run (csize 0) or a byte run (csize = -byte, token byte 1); memcpy'ed and special-value
 chunks.  Filters run forward per block (filters[0] first): byte shuffle, bitshuffle.  The LZ encoders
-are oracle_blosc2.cpp's (greedy, this repo's own), so a decoder matching these chunks is checked
+are datagen/blosc2_writer.cpp's (greedy, this repo's own), so a decoder matching these chunks is checked
 against the format description, not against c-blosc2's bytes ("parity unpinned").
 """
 from __future__ import annotations
@@ -18,7 +18,36 @@ import zlib
 
 import numpy as np
 
-from . import py_oracle
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "libblosc2w.so"
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+        L = C.CDLL(str(LIB_PATH))
+        L.blosc2w_lz_compress.restype = C.c_int64
+        L.blosc2w_lz_compress.argtypes = [C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                                C.c_uint64]
+        _LIB = L
+    return _LIB
+
+
+def lz(codec: int, data: bytes, max_dist: int = 8191 + 65535) -> bytes:
+    """One BloscLZ (codec 0) / LZ4 (codec 1) stream by this repo's greedy encoder."""
+    cap = 2 * len(data) + 64
+    out = (C.c_uint8 * cap)()
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    n = lib().blosc2w_lz_compress(codec, src, len(data), max_dist, out, cap)
+    assert n >= 0
+    return bytes(out)[:n]
 
 BLOSCLZ, LZ4, ZLIB, ZSTD = 0, 1, 3, 4
 NOFILTER, SHUFFLE, BITSHUFFLE, DELTA, TRUNC = 0, 1, 2, 3, 4
@@ -50,7 +79,7 @@ def _stream(codec: int, s: bytes, mode: str) -> bytes:
     if mode == "raw":
         return struct.pack("<i", n) + s
     if codec in (BLOSCLZ, LZ4):
-        c = py_oracle.blosc2_lz(codec, s)
+        c = lz(codec, s)
     elif codec == ZLIB:
         c = zlib.compress(s, 6)
     else:

@@ -45,8 +45,6 @@ def lib():
         L.oracle_blosc2_sizes.argtypes = [VP, U64, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]
         L.oracle_blosc2_decompress.restype = C.c_uint32
         L.oracle_blosc2_decompress.argtypes = [VP, U64, VP, U64, C.POINTER(U64)]
-        L.oracle_blosc2_lz_compress.restype = C.c_int64
-        L.oracle_blosc2_lz_compress.argtypes = [C.c_uint32, VP, U64, U64, VP, U64]
         L.oracle_missing_convert.restype = C.c_int
         L.oracle_missing_convert.argtypes = [C.c_uint32, C.c_uint32, C.c_int64, C.c_uint64, C.c_double, VP]
         _LIB = L
@@ -149,12 +147,3 @@ def blosc2_decompress(data: bytes, cap: int | None = None):
     e = lib().oracle_blosc2_decompress(src, len(data), out, cap, C.byref(got))
     return int(e), bytes(out)[: min(got.value, cap)]
 
-
-def blosc2_lz(codec: int, data: bytes, max_dist: int = 8191 + 65535) -> bytes:
-    """This repo's own BloscLZ (codec 0) / LZ4 (codec 1) stream encoder (test fixtures only)."""
-    cap = 2 * len(data) + 64
-    out = (C.c_uint8 * cap)()
-    src = C.create_string_buffer(bytes(data), max(1, len(data)))
-    n = lib().oracle_blosc2_lz_compress(codec, src, len(data), max_dist, out, cap)
-    assert n >= 0
-    return bytes(out)[:n]

@@ -6,7 +6,7 @@ b"hello world" compressed by blosc2_compress(clevel 5, BLOSC_SHUFFLE, typesize 1
 buffer size blosc stores it memcpy'ed behind a 32-byte header, rebuilt here from the published chunk
 format; compression.rs:130-140 test_decompress_invalid_blosc: b"invalid format" ->
 "invalid blosc2 compressed data").  Everything else is PARITY UNPINNED (no blosc2 library in the
-image): chunks come from this repo's own writer (oracle/blosc2_chunk.py) and are checked for round
+image): chunks come from this repo's own writer (datagen/blosc2_chunk.py) and are checked for round
 trips, the frozen fixtures in tests/golden/blosc2_chunks.json, and the error taxonomy."""
 import hashlib
 import itertools
@@ -17,7 +17,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from oracle import blosc2_chunk as B
+from datagen import blosc2_chunk as B
 from oracle import py_oracle as oracle
 from reductionist_amd import _abi
 

@@ -2,14 +2,14 @@
 (oracle/oracle_blosc2.cpp, tests/test_blosc2_cpu.py) and the original bytes, through the C ABI:
 rdx_decompress_batch_device (batches and lone chunks) and rdx_execute / rdx_execute_device with a blosc2
 request (decompress -> filters -> operation, app.rs:163-183).  Chunks come from this repo's writer
-(oracle/blosc2_chunk.py): parity unpinned beyond the reference's two tests."""
+(datagen/blosc2_chunk.py): parity unpinned beyond the reference's two tests."""
 import itertools
 import struct
 
 import numpy as np
 import pytest
 
-from oracle import blosc2_chunk as B
+from datagen import blosc2_chunk as B
 from oracle import py_oracle as oracle
 from reductionist_amd import _abi
 
