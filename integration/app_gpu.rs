@@ -38,10 +38,20 @@ pub fn operation_gpu<T: operation::Operation>(
     request_data: models::RequestData,
     data: Bytes,
 ) -> Result<models::Response, ActiveStorageError> {
-    // One request = one DEFLATE stream, and a stream is serial: a wavefront decodes a 4 MiB chunk in
-    // ~100-220 ms, a CPU core in ~4-7 ms.  A lone compressed request therefore keeps the
-    // reference's host decompression (compression.rs:18-27); chunks are inflated on the device only in
-    // batches (rdx_decompress_batch_device).  blosc2 is decoded on the host always.
+    // gzip / zlib: one request = one DEFLATE stream, and a stream is serial: a wavefront decodes a 4 MiB
+    // chunk in ~100-220 ms, a CPU core in ~4-7 ms.  A lone gzip/zlib request therefore
+    // keeps the reference's host decompression (compression.rs:18-27); those chunks are inflated on the
+    // device only in batches (rdx_decompress_batch_device).
+    // blosc2: a chunk is hundreds of independent block streams, decoded in parallel on the device
+    // (k_blosc2), so the compressed chunk goes to the engine as it is; a codec the device
+    // does not decode comes back as UnsupportedOperation and is decompressed here instead.
+    if request_data.compression == Some(models::Compression::Blosc2) {
+        let vec: Vec<u8> = data.clone().into();
+        match debug_span!("operation_gpu").in_scope(|| T::execute(&request_data, vec)) {
+            Err(ActiveStorageError::UnsupportedOperation { .. }) => {}
+            other => return other,
+        }
+    }
     let (request_data, data) = match request_data.compression {
         Some(c) => {
             let d = compression::decompress(c, &data)?;
@@ -70,17 +80,26 @@ pub async fn operation_handler_cbor<const OP: u32>(
     let mem_permits = state.resource_manager.memory(memory).await?;
     let data = state.chunk_store.get(&auth, &request_data, &state.resource_manager, mem_permits).await?;
     let run = move || -> Result<Bytes, ActiveStorageError> {
-        // a lone compressed chunk is inflated on the host, as in operation_gpu
+        // a lone gzip / zlib chunk is inflated on the host, as in operation_gpu; blosc2 goes to the device
         let (request_data, data) = match request_data.compression {
-            Some(c) => {
+            Some(c) if c != models::Compression::Blosc2 => {
                 let d = compression::decompress(c, &data)?;
                 let mut rd = request_data;
                 rd.compression = None;
                 (rd, d)
             }
-            None => (request_data, data),
+            _ => (request_data, data),
         };
-        debug_span!("operation_gpu_cbor").in_scope(|| operations_gpu::execute_cbor::<OP>(&request_data, &data))
+        match debug_span!("operation_gpu_cbor").in_scope(|| operations_gpu::execute_cbor::<OP>(&request_data, &data)) {
+            // a blosc2 codec the device does not decode: decompress on the host and run again
+            Err(ActiveStorageError::UnsupportedOperation { .. }) if request_data.compression.is_some() => {
+                let d = compression::decompress(request_data.compression.unwrap(), &data)?;
+                let mut rd = request_data;
+                rd.compression = None;
+                operations_gpu::execute_cbor::<OP>(&rd, &d)
+            }
+            other => other,
+        }
     };
     let body = if state.args.use_rayon {
         tokio_rayon::spawn(run).await?

@@ -299,13 +299,22 @@ pub fn check(st: i32, compression: Option<Compression>) -> Result<(), ActiveStor
         E_SHUFFLE_LENGTH => panic!("assertion `left == right` failed"),
         // operations.rs:181-183,355-357: NaN in a min/max comparison panics in the reference; parity
         E_NAN_UNORDERED => panic!("unexpected undefined order error for min"),
-        // compression.rs:29-57 blosc2 is decoded on the host (compression::decompress) before the call
-        E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 on the GPU".into() }),
+        // a blosc2 codec / filter the device does not decode (zstd, snappy, zlib streams, dictionaries,
+        // delta): app_gpu::operation_gpu catches this variant and decompresses on the host instead
+        E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 codec on the GPU".into() }),
         // compression.rs:60-82 -> DecompressionFlate2 / DecompressionZune, 400 (error.rs:247-249)
         E_DECOMPRESSION => {
             let code = unsafe { rdx_inflate_last_error() };
             let msg = unsafe { std::ffi::CStr::from_ptr(rdx_inflate_error_string(code)) }.to_string_lossy().into_owned();
             Err(match compression {
+                // compression.rs:33-55: DecompressionBlosc2 carries one of three static messages
+                Some(Compression::Blosc2) => ActiveStorageError::DecompressionBlosc2 {
+                    error: match code {
+                        crate::rdx_ffi::blosc2::INVALID => "invalid blosc2 compressed data",
+                        crate::rdx_ffi::blosc2::SIZE => "unexpected decompressed size for blosc2 data",
+                        _ => "failed to decompress blosc2 data",
+                    },
+                },
                 // compression.rs:184 reads the message back from DecodeErrorStatus::GenericStr
                 Some(Compression::Zlib) => ActiveStorageError::DecompressionZune(
                     zune_inflate::errors::InflateDecodeErrors::new_with_error(

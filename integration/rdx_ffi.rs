@@ -54,6 +54,14 @@ pub mod status {
     pub const E_DECOMPRESSION: i32 = 13;
 }
 
+/// rdx_inflate_error values of a blosc2 chunk (include/rdx.h; compression.rs:29-57 messages)
+pub mod blosc2 {
+    pub const INVALID: u32 = 12;      // "invalid blosc2 compressed data"
+    pub const FAILED: u32 = 13;       // "failed to decompress blosc2 data"
+    pub const SIZE: u32 = 14;         // "unexpected decompressed size for blosc2 data"
+    pub const UNSUPPORTED: u32 = 15;  // zstd / snappy / zlib streams / dictionaries / delta: host fallback
+}
+
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
 pub struct RdxSlice {
@@ -150,6 +158,13 @@ extern "C" {
     pub fn rdx_missing_from_f64(dtype: u32, v: f64, out: *mut c_void) -> c_int;
     pub fn rdx_inflate_error_string(code: u32) -> *const c_char;
     pub fn rdx_inflate_last_error() -> u32;
+    pub fn rdx_blosc2_cbuffer_sizes(
+        src: *const c_void,
+        len: u64,
+        nbytes: *mut u64,
+        cbytes: *mut u64,
+        blocksize: *mut u64,
+    ) -> c_int;
     pub fn rdx_host_alloc(ctx: *mut RdxContext, bytes: u64, out: *mut *mut c_void) -> c_int;
     pub fn rdx_host_free(ctx: *mut RdxContext, p: *mut c_void);
     pub fn rdx_execute(

@@ -46,11 +46,11 @@ class DeviceError(ActiveStorageError):                # new with the device engi
     http_status = 500
 
 
-class Unsupported(ActiveStorageError):                # blosc2: decompress on the host first
+class Unsupported(ActiveStorageError):                # a blosc2 codec not decoded on the device: host fallback
     http_status = 500
 
 
-class Decompression(ActiveStorageError):              # error.rs DecompressionFlate2 / DecompressionZune, 400
+class Decompression(ActiveStorageError):              # error.rs DecompressionFlate2 / Zune / Blosc2, 400
     http_status = 400
 
 
@@ -73,7 +73,7 @@ _MAP = {
 def check(status: int) -> None:
     if status == _abi.OK:
         return
-    if status == _abi.E_DECOMPRESSION:  # the detail: compression.rs:166-190 messages
+    if status == _abi.E_DECOMPRESSION:  # the detail: compression.rs:35-53 (blosc2), :166-190 messages
         raise Decompression(_abi.inflate_error_string(_abi.lib().rdx_inflate_last_error()), status)
     cls, msg = _MAP.get(status, (DeviceError, f"rdx status {status}"))
     raise cls(msg, status)
