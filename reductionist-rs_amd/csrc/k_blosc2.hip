@@ -75,7 +75,7 @@ __device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b = 0;
     if (lane < 32 && lane < len) b = gld<uint8_t>(src + lane);
-    auto hb = [&](uint32_t k) { return (uint32_t)__shfl((int)b, (int)k, 64) & 0xffu; };
+    auto hb = [&](uint32_t k) { return rfl((uint32_t)__shfl((int)b, (int)k, 64) & 0xffu); };
     auto h32 = [&](uint32_t k) { return (int32_t)(hb(k) | hb(k + 1) << 8 | hb(k + 2) << 16 | hb(k + 3) << 24); };
     Hdr h{};
     const uint32_t version = hb(0);
@@ -190,38 +190,40 @@ struct LzStream {
     WaveLds &L;
     const uint32_t lane;
     const uint32_t *srcw;   // stream as dwords from its 4-byte aligned base
-    uint64_t end;           // skew + csize (aligned-stream coordinates)
-    uint64_t staged;        // [.., staged) is in the input ring
+    // positions are 32-bit: a stream is at most a block (BLOSC2_MAXBLOCKSIZE < 2^29), and the token
+    // chain is scalar code whose length per token sets the decode rate (64-bit adds cost two SALU ops)
+    uint32_t end;           // skew + csize (aligned-stream coordinates)
+    uint32_t staged;        // [.., staged) is in the input ring
     uint32_t pf[kStage / 4 / 64];
     uint8_t *dst;
-    uint64_t n, op, flushed;
+    uint32_t n, op, flushed;
 
-    __device__ __forceinline__ void load_unit(uint64_t start) {
-        const uint64_t w0 = start / 4 + (uint64_t)lane * (kStage / 4 / 64);
+    __device__ __forceinline__ void load_unit(uint32_t start) {
+        const uint32_t w0 = start / 4 + (uint32_t)lane * (kStage / 4 / 64);
 #pragma unroll
         for (int k = 0; k < (int)(kStage / 4 / 64); ++k) {
-            const uint64_t w = w0 + k;
+            const uint32_t w = w0 + k;
             pf[k] = 0;
             if (w * 4 < end) {
                 pf[k] = gld<uint32_t>(srcw + w);
-                const uint64_t valid = end - w * 4;
+                const uint32_t valid = end - w * 4;
                 if (valid < 4) pf[k] &= (1u << (8 * valid)) - 1;
             }
         }
     }
     __device__ __forceinline__ void stage() {
-        const uint32_t i0 = (uint32_t)(staged / 4 + (uint64_t)lane * (kStage / 4 / 64));
+        const uint32_t i0 = (uint32_t)(staged / 4 + (uint32_t)lane * (kStage / 4 / 64));
 #pragma unroll
         for (int k = 0; k < (int)(kStage / 4 / 64); ++k) L.in[(i0 + k) & (kInWords - 1)] = pf[k];
         staged += kStage;
         load_unit(staged);   // words past the stream load as zeros (no loads issued)
         wave_sync();
     }
-    __device__ __forceinline__ void ensure(uint64_t p) {
+    __device__ __forceinline__ void ensure(uint32_t p) {
         while (p > staged) stage();
     }
     // bytes p .. p+7 (aligned-stream coordinates), wave-uniform
-    __device__ __forceinline__ uint64_t peek8(uint64_t p) {
+    __device__ __forceinline__ uint64_t peek8(uint32_t p) {
         ensure(p + 12);
         const uint32_t i = (uint32_t)(p >> 2), sh = (uint32_t)(p & 3) * 8;
         const uint32_t a = L.in[i & (kInWords - 1)], b = L.in[(i + 1) & (kInWords - 1)],
@@ -230,7 +232,7 @@ struct LzStream {
         const uint64_t v = sh ? (lo >> sh) | ((uint64_t)c << (64 - sh)) : lo;
         return rfl64(v);
     }
-    __device__ __forceinline__ uint8_t in_byte(uint64_t p) const {
+    __device__ __forceinline__ uint8_t in_byte(uint32_t p) const {
         return (uint8_t)(L.in[(p >> 2) & (kInWords - 1)] >> ((p & 3) * 8));
     }
 
@@ -257,31 +259,31 @@ struct LzStream {
     __device__ __forceinline__ void room() {
         if (op - flushed > kRing - 64) flush(kFlush);
     }
-    __device__ __forceinline__ uint8_t far_byte(uint64_t q) const {
+    __device__ __forceinline__ uint8_t far_byte(uint32_t q) const {
         const uintptr_t a = (uintptr_t)(dst + q);
         const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
         return (uint8_t)(w >> (8 * (a & 3)));
     }
     // literal run of `run` bytes from input position ip
-    __device__ void literals(uint64_t ip, uint64_t run) {
-        for (uint64_t s = 0; s < run; s += 64) {
+    __device__ void literals(uint32_t ip, uint32_t run) {
+        for (uint32_t s = 0; s < run; s += 64) {
             ensure(ip + s + 64);
             room();
-            const uint64_t k = run - s < 64 ? run - s : 64;
+            const uint32_t k = run - s < 64 ? run - s : 64;
             if (lane < k) L.win[(op + lane) & kRingMask] = in_byte(ip + s + lane);
             op += k;
             asm volatile("" ::: "memory");
         }
     }
     // match of len bytes at distance dist (1 <= dist <= op)
-    __device__ void match(uint64_t len, uint64_t dist) {
-        for (uint64_t s = 0; s < len; s += 64) {
+    __device__ void match(uint32_t len, uint32_t dist) {
+        for (uint32_t s = 0; s < len; s += 64) {
             room();
-            const uint64_t k = len - s < 64 ? len - s : 64;
+            const uint32_t k = len - s < 64 ? len - s : 64;
             if (lane < k) {
                 const uint32_t m = dist < 64 ? lane % (uint32_t)dist : lane;
-                const uint64_t back = dist - m, q = op - back;
+                const uint32_t back = dist - m, q = op - back;
                 const uint8_t v = back <= kRing - 64 ? L.win[q & kRingMask] : far_byte(q);
                 L.win[(op + lane) & kRingMask] = v;
             }
@@ -294,13 +296,13 @@ struct LzStream {
     }
 
     // blosclz_decompress (oracle_blosc2.cpp blosclz_dec); returns false on a malformed stream
-    __device__ bool blosclz(uint64_t ip) {
+    __device__ bool blosclz(uint32_t ip) {
         uint32_t ctrl = (uint32_t)(peek8(ip) & 31u);
         ++ip;
         for (;;) {
             if (ctrl >= 32) {
-                uint64_t len = (ctrl >> 5) - 1;
-                uint64_t ofs = (uint64_t)(ctrl & 31u) << 8;
+                uint32_t len = (ctrl >> 5) - 1;
+                uint32_t ofs = (uint32_t)(ctrl & 31u) << 8;
                 if (len == 6) {
                     uint32_t c;
                     do {
@@ -308,6 +310,7 @@ struct LzStream {
                         c = (uint32_t)(peek8(ip) & 255u);
                         ++ip;
                         len += c;
+                        if (len > n) return false;   // (32-bit positions: no wrap on hostile input)
                     } while (c == 255);
                 } else if (ip + 1 >= end) {
                     return false;
@@ -316,7 +319,7 @@ struct LzStream {
                 const uint32_t code = (uint32_t)(w & 255u);
                 ++ip;
                 len += 3;
-                uint64_t dist = ofs + code + 1;
+                uint32_t dist = ofs + code + 1;
                 uint32_t nx = (uint32_t)((w >> 8) & 255u);
                 if (code == 255 && ofs == (31u << 8)) {
                     if (ip + 1 >= end) return false;
@@ -330,7 +333,7 @@ struct LzStream {
                 ++ip;
                 match(len, dist);
             } else {
-                const uint64_t run = ctrl + 1;
+                const uint32_t run = ctrl + 1;
                 if (op + run > n || ip + run > end) return false;
                 literals(ip, run);
                 ip += run;
@@ -343,14 +346,14 @@ struct LzStream {
     }
 
     // LZ4_decompress_safe (oracle_blosc2.cpp lz4_dec)
-    __device__ bool lz4(uint64_t ip) {
+    __device__ bool lz4(uint32_t ip) {
         if (ip >= end) return false;
         for (;;) {
             if (ip >= end) return false;
             uint64_t w = peek8(ip);
             const uint32_t token = (uint32_t)(w & 255u);
             ++ip;
-            uint64_t L = token >> 4;
+            uint32_t L = token >> 4;
             if (L == 15) {
                 uint32_t b;
                 do {
@@ -358,6 +361,7 @@ struct LzStream {
                     b = (uint32_t)(peek8(ip) & 255u);
                     ++ip;
                     L += b;
+                    if (L > n) return false;
                 } while (b == 255);
             }
             if (end - ip < L || n - op < L) return false;
@@ -367,11 +371,12 @@ struct LzStream {
                 if (ip != end) return false;
                 break;
             }
-            w = peek8(ip);
-            const uint64_t off = w & 0xffffu;
+            // a short literal run leaves the offset inside the token's 8-byte window: no second LDS trip
+            const uint32_t off = (uint32_t)((token >> 4) <= 5 ? (w >> (8 * (1 + (token >> 4)))) & 0xffffu
+                                                               : peek8(ip) & 0xffffu);
             ip += 2;
             if (off == 0 || off > op) return false;
-            uint64_t M = token & 15u;
+            uint32_t M = token & 15u;
             if (M == 15) {
                 uint32_t b;
                 do {
@@ -379,6 +384,7 @@ struct LzStream {
                     b = (uint32_t)(peek8(ip) & 255u);
                     ++ip;
                     M += b;
+                    if (M > n) return false;
                 } while (b == 255);
             }
             M += 4;
@@ -393,7 +399,9 @@ struct LzStream {
 
 __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args a) {
     __shared__ WaveLds LW[kWaves];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index made scalar: the compiler's uniformity analysis does not see threadIdx.x >> 6 as
+    // wave-uniform, and everything below (items, stream positions, the token chain) derives from it
+    const uint32_t wave = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t c = blockIdx.x / a.wg_per_chunk;
     if (c >= a.n) return;
     const uint64_t w0 = (uint64_t)(blockIdx.x % a.wg_per_chunk) * kWaves + wave;
@@ -470,10 +478,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args
             const uint32_t skew = (uint32_t)((uintptr_t)s & 3);
             LzStream z{LW[wave], lane};
             z.srcw = reinterpret_cast<const uint32_t *>(s - skew);
-            z.end = skew + (uint64_t)cb;
+            z.end = skew + (uint32_t)cb;
             z.staged = 0;
             z.dst = dst;
-            z.n = neblock;
+            z.n = (uint32_t)neblock;
             z.op = z.flushed = 0;
             z.load_unit(0);
             z.stage();
