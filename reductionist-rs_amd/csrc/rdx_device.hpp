@@ -414,8 +414,10 @@ __device__ __forceinline__ constexpr int packed_words() {
 //
 // Record fields -> granules: a 64-bit value / sum / compensation as two 32-bit halves; a 32-bit min/max
 // value as one; the count (< 2^47) with the NaN flag in bit 47 as one; each ±0 fold-order rank (48-bit
-// two's complement, INT64_MAX as 0x7fff_ffff_ffff) as one.  f32 sum: 3 granules, f32 min/max: 4, f64
-// min/max and sum: 5, integer sum: 3, count: 1.
+// two's complement, INT64_MAX as 0x7fff_ffff_ffff) as one.  Sums carry the count (< 2^32: the planner
+// refuses views of 2^32 elements or more) in the spare 16 bits of their two sum halves instead of a
+// granule of its own.  f32 / integer sum: 2 granules (16 B), f32 min/max: 4, f64 sum: 4, f64 min/max: 5,
+// count: 1.
 // Phase timeline of the all-axes kernels (probe builds only, make EXTRA=-DRDX_PROBES=1): per workgroup
 // [0] first instruction, [1] streaming done, [2] record published + counter added, [3] fold done (last
 // arriver), in wall-clock ticks (100 MHz); [4] the HW_ID register at the start (CU / SH / SE placement).
@@ -461,9 +463,9 @@ __device__ __attribute__((noinline)) uint64_t poll_granule(const uint64_t *g, ui
 template <typename T, int OP>
 __device__ __forceinline__ constexpr int granules() {
     constexpr bool kRank = Red<T, OP>::kRank;
+    if (OP == OP_SUM) return std::is_same_v<T, double> ? 4 : 2;          // sum (+ compensation), count packed
     int n = 0;
-    if (OP != OP_COUNT) n += (OP == OP_SUM || sizeof(T) == 8) ? 2 : 1;   // value / sum
-    if (OP == OP_SUM && std::is_same_v<T, double>) n += 2;                // compensation
+    if (OP != OP_COUNT) n += sizeof(T) == 8 ? 2 : 1;                      // value
     n += 1;                                                               // count (+ NaN flag)
     if (kRank) n += 2;                                                    // ±0 ranks
     return n;
@@ -482,18 +484,23 @@ template <typename T, int OP>
 __device__ __forceinline__ void encode(const Red<T, OP> &r, uint64_t (&g)[kMaxGranules]) {
     uint64_t w[kPartialWords];
     r.to_words(w);
+    if constexpr (OP == OP_SUM) {   // {sum lo32, count lo16}, {sum hi32, count hi16} [, compensation]
+        g[0] = (w[0] & 0xffffffffull) | (w[2] & 0xffffull) << 32;
+        g[1] = (w[0] >> 32) | ((w[2] >> 16) & 0xffffull) << 32;
+        if constexpr (std::is_same_v<T, double>) {
+            g[2] = w[1] & 0xffffffffull;
+            g[3] = w[1] >> 32;
+        }
+        return;
+    }
     int k = 0;
     if constexpr (OP != OP_COUNT) {
-        if constexpr (OP == OP_SUM || sizeof(T) == 8) {
+        if constexpr (sizeof(T) == 8) {
             g[k++] = w[0] & 0xffffffffull;
             g[k++] = w[0] >> 32;
         } else {
             g[k++] = w[0] & 0xffffffffull;
         }
-    }
-    if constexpr (OP == OP_SUM && std::is_same_v<T, double>) {
-        g[k++] = w[1] & 0xffffffffull;
-        g[k++] = w[1] >> 32;
     }
     g[k++] = (w[2] & ((1ull << 47) - 1)) | (Red<T, OP>::kRank && w[5] ? (1ull << 47) : 0ull);
     if constexpr (Red<T, OP>::kRank) {
@@ -508,18 +515,21 @@ __device__ __forceinline__ void decode(const uint64_t (&g)[kMaxGranules], Red<T,
     id.init();
     uint64_t w[kPartialWords];
     id.to_words(w);
+    if constexpr (OP == OP_SUM) {
+        w[0] = (g[0] & 0xffffffffull) | (g[1] & 0xffffffffull) << 32;
+        w[2] = ((g[0] >> 32) & 0xffffull) | ((g[1] >> 32) & 0xffffull) << 16;
+        if constexpr (std::is_same_v<T, double>) w[1] = (g[2] & 0xffffffffull) | (g[3] & 0xffffffffull) << 32;
+        r.from_words(w);
+        return;
+    }
     int k = 0;
     if constexpr (OP != OP_COUNT) {
-        if constexpr (OP == OP_SUM || sizeof(T) == 8) {
+        if constexpr (sizeof(T) == 8) {
             w[0] = (g[k] & 0xffffffffull) | ((g[k + 1] & 0xffffffffull) << 32);
             k += 2;
         } else {
             w[0] = g[k++] & 0xffffffffull;
         }
-    }
-    if constexpr (OP == OP_SUM && std::is_same_v<T, double>) {
-        w[1] = (g[k] & 0xffffffffull) | ((g[k + 1] & 0xffffffffull) << 32);
-        k += 2;
     }
     w[2] = g[k] & ((1ull << 47) - 1);
     if constexpr (Red<T, OP>::kRank) {
