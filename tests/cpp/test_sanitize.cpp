@@ -7,7 +7,10 @@
 //     the same response shape and sizes when both succeed (a NaN status is data-dependent: the planner
 //     must then succeed);
 //   * the oracle's inflate on random bytes, truncated and bit-flipped stored / fixed-Huffman streams
-//     with and without gzip / zlib framing.
+//     with and without gzip / zlib framing;
+//   * the oracle's blosc2 decoder (oracle/oracle_blosc2.cpp) on the golden chunks
+//     (tests/golden/blosc2_chunks.json, passed as a seed file) truncated, bit-flipped and with random
+//     header fields.
 // Any sanitizer report aborts the process (non-zero exit).
 #include <cstdint>
 #include <cstdio>
@@ -23,6 +26,10 @@ extern "C" int oracle_execute(const rdx_request *req, const void *chunk, uint64_
 extern "C" int oracle_validate_request(const rdx_request *req);
 extern "C" uint32_t oracle_decompress(uint32_t compression, const uint8_t *in, uint64_t len, uint8_t *out,
                                       uint64_t cap, uint64_t *out_len);
+extern "C" uint32_t oracle_blosc2_decompress(const uint8_t *src, uint64_t len, uint8_t *out, uint64_t cap,
+                                             uint64_t *out_len);
+extern "C" void oracle_blosc2_sizes(const uint8_t *src, uint64_t len, uint64_t *nbytes, uint64_t *cbytes,
+                                   uint64_t *blocksize);
 
 static int failures = 0;
 #define EXPECT(c, ...)                                                              \
@@ -223,10 +230,46 @@ static void inflate_fuzz(uint64_t seed, int count) {
     }
 }
 
+// seed file: records of {u32 length, bytes}
+static void blosc2_fuzz(const char *path, uint64_t seed, int count) {
+    std::vector<std::vector<uint8_t>> seeds;
+    if (FILE *f = std::fopen(path, "rb")) {
+        uint32_t n = 0;
+        while (std::fread(&n, 4, 1, f) == 1) {
+            std::vector<uint8_t> v(n);
+            if (n && std::fread(v.data(), 1, n, f) != n) break;
+            seeds.push_back(std::move(v));
+        }
+        std::fclose(f);
+    }
+    EXPECT(seeds.size() >= 10, "blosc2 seed file %s: %zu chunks", path, seeds.size());
+    Rng g(seed);
+    for (int i = 0; i < count && !seeds.empty(); ++i) {
+        std::vector<uint8_t> c = seeds[(size_t)uni(g, 0, (int64_t)seeds.size() - 1)];
+        const double kind = unif(g);
+        if (kind < 0.3 && c.size() > 1) c.resize((size_t)uni(g, 0, (int64_t)c.size() - 1));
+        const int flips = (int)uni(g, 0, 6);
+        for (int k = 0; k < flips && !c.empty(); ++k) c[(size_t)uni(g, 0, (int64_t)c.size() - 1)] ^= (uint8_t)(1u << uni(g, 0, 7));
+        if (kind > 0.8 && c.size() >= 32) {   // a random header field
+            const int at = (int)uni(g, 0, 31);
+            c[(size_t)at] = (uint8_t)g();
+        }
+        uint64_t nb = 0, cb = 0, bs = 0, got = 0;
+        oracle_blosc2_sizes(c.data(), c.size(), &nb, &cb, &bs);
+        const uint64_t cap = nb > (1u << 22) ? (1u << 22) : nb;
+        std::vector<uint8_t> out(cap ? cap : 1);
+        const uint32_t e = oracle_blosc2_decompress(c.data(), c.size(), out.data(), cap, &got);
+        EXPECT(e == 0 || e == RDX_INFLATE_OUTPUT_OVERFLOW || (e >= RDX_BLOSC2_INVALID && e <= RDX_BLOSC2_UNSUPPORTED),
+               "blosc2 case %d error code %u", i, e);
+        EXPECT(e != 0 || got == nb, "blosc2 case %d: %llu bytes of %llu", i, (unsigned long long)got, (unsigned long long)nb);
+    }
+}
+
 int main(int argc, char **argv) {
     const int n = argc > 1 ? std::atoi(argv[1]) : 4000;
     for (uint64_t seed = 1; seed <= 4 && failures == 0; ++seed) requests(seed * 7919, n);
     inflate_fuzz(99, n);
+    if (argc > 2) blosc2_fuzz(argv[2], 1234, n);
     if (failures) {
         std::fprintf(stderr, "%d failure(s)\n", failures);
         return 1;

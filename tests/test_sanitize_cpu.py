@@ -1,14 +1,17 @@
 """The host code under AddressSanitizer + UndefinedBehaviorSanitizer: the product planner
 (rdx_plan.cpp) and the oracle built with -fsanitize=address,undefined -fno-sanitize-recover=all, driven
-by tests/cpp/test_sanitize.cpp (random requests planner-vs-oracle, inflate on corrupted streams).  Any
+by tests/cpp/test_sanitize.cpp (random requests planner-vs-oracle, inflate on corrupted streams, the blosc2
+decoder on corrupted golden chunks).  Any
 sanitizer report fails the run."""
+import json
 import os
+import struct
 import subprocess
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 SRCS = [ROOT / "tests" / "cpp" / "test_sanitize.cpp", ROOT / "reductionist-rs_amd" / "csrc" / "rdx_plan.cpp",
-        ROOT / "oracle" / "rdx_oracle.cpp", ROOT / "oracle" / "oracle_inflate.cpp"]
+        ROOT / "oracle" / "rdx_oracle.cpp", ROOT / "oracle" / "oracle_inflate.cpp", ROOT / "oracle" / "oracle_blosc2.cpp"]
 DEPS = SRCS + [ROOT / "include" / "rdx.h", ROOT / "reductionist-rs_amd" / "csrc" / "rdx_plan.hpp",
                ROOT / "reductionist-rs_amd" / "csrc" / "rdx_kdesc.h"]
 
@@ -24,5 +27,9 @@ def _binary():
 
 def test_planner_and_oracle_under_asan_ubsan():
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
-    r = subprocess.run([str(_binary()), "4000"], capture_output=True, text=True, timeout=600, env=env)
+    seeds = ROOT / "tests" / "cpp" / "build" / "blosc2_seeds.bin"
+    chunks = json.loads((ROOT / "tests" / "golden" / "blosc2_chunks.json").read_text())["chunks"]
+    binary = _binary()
+    seeds.write_bytes(b"".join(struct.pack("<I", len(c)) + c for c in (bytes.fromhex(x["chunk"]) for x in chunks)))
+    r = subprocess.run([str(binary), "4000", str(seeds)], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0 and "sanitize: ok" in r.stdout, (r.stdout + r.stderr)[-4000:]
