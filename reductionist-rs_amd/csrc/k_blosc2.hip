@@ -198,25 +198,19 @@ struct LzStream {
     uint8_t *dst;
     uint32_t n, op, flushed;
 
+    // The next unit's words, in flight until stage() stores them: addresses are clamped to the stream's
+    // last word (no branch, so no wait right behind each load); bytes past the end are never parsed.
     __device__ __forceinline__ void load_unit(uint32_t start) {
-        const uint32_t w0 = start / 4 + (uint32_t)lane * (kStage / 4 / 64);
+        const uint32_t w0 = start / 4 + (uint32_t)lane * (kStage / 4 / 64), last = (end - 1) / 4;
 #pragma unroll
-        for (int k = 0; k < (int)(kStage / 4 / 64); ++k) {
-            const uint32_t w = w0 + k;
-            pf[k] = 0;
-            if (w * 4 < end) {
-                pf[k] = gld<uint32_t>(srcw + w);
-                const uint32_t valid = end - w * 4;
-                if (valid < 4) pf[k] &= (1u << (8 * valid)) - 1;
-            }
-        }
+        for (int k = 0; k < (int)(kStage / 4 / 64); ++k) pf[k] = gld<uint32_t>(srcw + (w0 + k < last ? w0 + k : last));
     }
     __device__ __forceinline__ void stage() {
         const uint32_t i0 = (uint32_t)(staged / 4 + (uint32_t)lane * (kStage / 4 / 64));
 #pragma unroll
         for (int k = 0; k < (int)(kStage / 4 / 64); ++k) L.in[(i0 + k) & (kInWords - 1)] = pf[k];
         staged += kStage;
-        load_unit(staged);   // words past the stream load as zeros (no loads issued)
+        load_unit(staged);
         wave_sync();
     }
     __device__ __forceinline__ void ensure(uint32_t p) {
@@ -282,7 +276,14 @@ struct LzStream {
             room();
             const uint32_t k = len - s < 64 ? len - s : 64;
             if (lane < k) {
-                const uint32_t m = dist < 64 ? lane % (uint32_t)dist : lane;
+                uint32_t m = lane;
+                if (dist < 64) {   // lane mod dist by a float reciprocal, exact after one correction
+                    const uint32_t q = (uint32_t)((float)lane * __builtin_amdgcn_rcpf((float)dist));
+                    int32_t r = (int32_t)(lane - q * (uint32_t)dist);
+                    r += r < 0 ? (int32_t)dist : 0;
+                    r -= r >= (int32_t)dist ? (int32_t)dist : 0;
+                    m = (uint32_t)r;
+                }
                 const uint32_t back = dist - m, q = op - back;
                 const uint8_t v = back <= kRing - 64 ? L.win[q & kRingMask] : far_byte(q);
                 L.win[(op + lane) & kRingMask] = v;
