@@ -276,14 +276,7 @@ struct LzStream {
             room();
             const uint32_t k = len - s < 64 ? len - s : 64;
             if (lane < k) {
-                uint32_t m = lane;
-                if (dist < 64) {   // lane mod dist by a float reciprocal, exact after one correction
-                    const uint32_t q = (uint32_t)((float)lane * __builtin_amdgcn_rcpf((float)dist));
-                    int32_t r = (int32_t)(lane - q * (uint32_t)dist);
-                    r += r < 0 ? (int32_t)dist : 0;
-                    r -= r >= (int32_t)dist ? (int32_t)dist : 0;
-                    m = (uint32_t)r;
-                }
+                const uint32_t m = dist < 64 ? lane % (uint32_t)dist : lane;
                 const uint32_t back = dist - m, q = op - back;
                 const uint8_t v = back <= kRing - 64 ? L.win[q & kRingMask] : far_byte(q);
                 L.win[(op + lane) & kRingMask] = v;
