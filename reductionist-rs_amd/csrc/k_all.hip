@@ -346,6 +346,7 @@ __device__ __forceinline__ void decompose(const KView &v, const DimRegs<ND> &d, 
 
 template <typename T, int OP, bool FUSED, int VW, int ND, int MK>
 __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
+    RDX_STAMP(0);
     constexpr int kU = VW > 1 ? 4 : 8;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
@@ -388,6 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
             }
         }
     }
+    RDX_STAMP(1);
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
 

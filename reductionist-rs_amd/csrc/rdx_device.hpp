@@ -550,6 +550,33 @@ __device__ __forceinline__ void publish(uint64_t *P, const Red<T, OP> &r, uint32
     for (int j = 0; j < granules<T, OP>(); ++j) put_granule(P + j * stride, g[j], tag);
 }
 
+// collect() in two halves, so that a folder can have several records' loads in flight before it waits
+// on the first: load_record issues the granule loads, accept_record checks their tags (polling a stale
+// one) and decodes.
+template <typename T, int OP>
+__device__ __forceinline__ void load_record(const uint64_t *P, uint64_t (&g)[kMaxGranules], uint64_t stride = 1) {
+#pragma unroll
+    for (int j = 0; j < granules<T, OP>(); ++j)
+        g[j] = __hip_atomic_load(P + j * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T, int OP>
+__device__ __forceinline__ void accept_record(const uint64_t *P, uint64_t (&g)[kMaxGranules], Red<T, OP> &r,
+                                              uint32_t tag, uint32_t &fault, uint64_t stride = 1) {
+    constexpr int kG = granules<T, OP>();
+    bool fresh = true;
+#pragma unroll
+    for (int j = 0; j < kG; ++j) fresh &= (uint32_t)(g[j] >> 48) == tag;
+    if (__builtin_expect(!fresh, 0)) {
+#pragma unroll
+        for (int j = 0; j < kG; ++j)
+            if ((uint32_t)(g[j] >> 48) != tag) {
+                g[j] = poll_granule(P + j * stride, tag);
+                fault |= (uint32_t)(g[j] >> 48) != tag;
+            }
+    }
+    decode(g, r);
+}
+
 template <typename T, int OP>
 __device__ __forceinline__ void collect(const uint64_t *P, Red<T, OP> &r, uint32_t tag, uint32_t &fault,
                                         uint64_t stride = 1) {
@@ -683,10 +710,20 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
     Red<T, OP> acc;
     acc.init();
     uint32_t fault = 0;
-    for (uint32_t j = threadIdx.x; j < nrec; j += kBlock) {
+    // records j = tid, tid + 256, ... merged in that order; two in flight per thread, so up to 512
+    // records (C3: 336) cost one load round trip instead of one per 256
+    for (uint32_t j0 = threadIdx.x; j0 < nrec; j0 += 2 * kBlock) {
+        const uint32_t j1 = j0 + kBlock;
+        uint64_t g0[kMaxGranules] = {}, g1[kMaxGranules] = {};
+        load_record<T, OP>(P + (uint64_t)j0 * kR, g0);
+        if (j1 < nrec) load_record<T, OP>(P + (uint64_t)j1 * kR, g1);
         Red<T, OP> o;
-        collect<T, OP>(P + (uint64_t)j * kR, o, out.epoch, fault);
+        accept_record<T, OP>(P + (uint64_t)j0 * kR, g0, o, out.epoch, fault);
         acc.merge(o);
+        if (j1 < nrec) {
+            accept_record<T, OP>(P + (uint64_t)j1 * kR, g1, o, out.epoch, fault);
+            acc.merge(o);
+        }
     }
     if (fault) s_fault = 1;   // benign race: every writer stores 1
     block_reduce(acc);

@@ -2,7 +2,7 @@
 """Phase timeline of one all-axes launch (probe build: make -C reductionist-rs_amd EXTRA=-DRDX_PROBES=1
 BUILD=build_probe OUT=librdx_probe.so; run with RDX_LIB_PATH=reductionist-rs_amd/librdx_probe.so).
 
-Each workgroup of k_all_contig stamps the wall clock (100 MHz) at its first instruction, when its
+Each workgroup of k_all_contig (and k_all_strided: the C3 hyperslab case) stamps the wall clock (100 MHz) at its first instruction, when its
 streaming ends, after its record is published and its arrival counted, and (last arriver) when the fold
 is done (rdx_device.hpp RDX_STAMP).  For the C2 single-chunk launch (64 MiB shuffled big-endian f32, one
 chunk) and the batched launch (8 chunks) this prints, relative to the first workgroup's start: the
@@ -25,9 +25,9 @@ from reductionist_amd import Engine, _abi  # noqa: E402
 TICK_NS = 10.0   # wall_clock64: 100 MHz
 
 
-def timeline(lib, n_wg):
+def timeline(lib, n_wg, dtype="f32"):
     buf = (C.c_uint64 * (8 * 8192))()
-    assert lib.rdx_probe_read_f32(buf, 8 * 8192) == 0
+    assert getattr(lib, f"rdx_probe_read_{dtype}")(buf, 8 * 8192) == 0
     rows = [(buf[8 * i], buf[8 * i + 1], buf[8 * i + 2], buf[8 * i + 3], buf[8 * i + 4]) for i in range(n_wg)]
     t0 = min(r[0] for r in rows)
     us = lambda t: round((t - t0) * TICK_NS / 1e3, 3)  # noqa: E731
@@ -78,6 +78,15 @@ def main():
                                 None, stream.cuda_stream)
     torch.cuda.synchronize()
     res["c2_batch8"] = timeline(lib, 256)   # 8 chunks x 32 workgroups (pick_bpc: one per CU in all)
+    # C3: f64 [128,128,128] hyperslab min with missing_value (k_all_strided, VW = 2: 1024 vectors per
+    # workgroup -> 336 workgroups)
+    v = torch.from_numpy(bench._c3_host()).cuda()
+    c3 = bench._c3_req(_abi, "min")
+    o8 = torch.zeros(2, dtype=torch.float64, device="cuda")
+    for k in range(12):
+        ws.execute_device(c3, v.data_ptr(), v.numel() * 8, o8.data_ptr(), cnt.data_ptr(), None, stream.cuda_stream)
+    torch.cuda.synchronize()
+    res["c3_min"] = timeline(lib, (bench.C3_NSEL // 2 + 1023) // 1024, "f64")
     print(json.dumps(res), flush=True)
 
 
