@@ -42,7 +42,7 @@ typedef enum rdx_status {
     RDX_E_NAN_UNORDERED = 7,       /* operations.rs:181-183,355-357 NaN in min/max — reference panics with
                                       "unexpected undefined order error for min"                            */
     RDX_E_UNSUPPORTED = 8,         /* a blosc2 codec / filter not decoded on the device (RDX_BLOSC2_UNSUPPORTED:
-                                      zstd, snappy, zlib-coded streams, dictionaries, delta) / rank > 32  */
+                                      zstd, snappy, dictionaries, delta) / rank > 32                     */
     RDX_E_DEVICE = 9,              /* HIP runtime error                                                      */
     RDX_E_OUT_OF_MEMORY = 10,      /* device or pinned allocation failed                                     */
     RDX_E_BUFFER_TOO_SMALL = 11,   /* caller-provided output buffer smaller than rdx_plan() reported        */

@@ -299,7 +299,7 @@ pub fn check(st: i32, compression: Option<Compression>) -> Result<(), ActiveStor
         E_SHUFFLE_LENGTH => panic!("assertion `left == right` failed"),
         // operations.rs:181-183,355-357: NaN in a min/max comparison panics in the reference; parity
         E_NAN_UNORDERED => panic!("unexpected undefined order error for min"),
-        // a blosc2 codec / filter the device does not decode (zstd, snappy, zlib streams, dictionaries,
+        // a blosc2 codec / filter the device does not decode (zstd, snappy, dictionaries,
         // delta): app_gpu::operation_gpu catches this variant and decompresses on the host instead
         E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 codec on the GPU".into() }),
         // compression.rs:60-82 -> DecompressionFlate2 / DecompressionZune, 400 (error.rs:247-249)

@@ -59,7 +59,7 @@ pub mod blosc2 {
     pub const INVALID: u32 = 12;      // "invalid blosc2 compressed data"
     pub const FAILED: u32 = 13;       // "failed to decompress blosc2 data"
     pub const SIZE: u32 = 14;         // "unexpected decompressed size for blosc2 data"
-    pub const UNSUPPORTED: u32 = 15;  // zstd / snappy / zlib streams / dictionaries / delta: host fallback
+    pub const UNSUPPORTED: u32 = 15;  // zstd / snappy / dictionaries / delta: host fallback
 }
 
 #[repr(C)]

@@ -23,8 +23,11 @@
 //                    filter are decoded straight into the output and skip this launch's work.
 // Memcpy'ed and special-value chunks (zeros, NaN, a repeated value, uninitialised) are copied / filled
 // by the decode launch in 4 KiB units.
-// Unsupported here (RDX_BLOSC2_UNSUPPORTED, as the oracle): zstd, snappy, zlib-coded streams,
-// dictionaries, delta, user-defined codecs / filters.
+// zlib-coded streams are not decoded here: each becomes a row of a stream table (source, length,
+// destination, expected size) that k_inflate decodes in the next launch, k_blosc2_zcheck folds their
+// results into the chunks' errors, then k_blosc2_filter runs.
+// Unsupported here (RDX_BLOSC2_UNSUPPORTED, as the oracle): zstd, snappy, dictionaries, delta,
+// user-defined codecs / filters (and more than 512 zlib-coded streams per chunk of a batch).
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
 
@@ -71,7 +74,7 @@ struct Hdr {
     uint64_t nbytes, bs, cbytes, nblocks, leftover, items;
 };
 
-__device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap) {
+__device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap, bool zlib) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b = 0;
     if (lane < 32 && lane < len) b = gld<uint8_t>(src + lane);
@@ -129,9 +132,12 @@ __device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap) {
     }
     h.mode = M_BLOCKS;
     h.codec = h.flags >> 5;
-    // zlib-coded streams: the oracle decodes them; on the device they are refused
-    if (h.codec == 2 || h.codec == 3 || h.codec == 4 || h.codec == 6) { h.code = RDX_BLOSC2_UNSUPPORTED; return h; }
-    if (h.codec > 1) { h.code = RDX_BLOSC2_FAILED; return h; }
+    // zlib-coded streams go to k_inflate through the stream table (refused when the caller gave none)
+    if (h.codec == 2 || h.codec == 4 || h.codec == 6 || (h.codec == 3 && !zlib)) {
+        h.code = RDX_BLOSC2_UNSUPPORTED;
+        return h;
+    }
+    if (h.codec > 1 && h.codec != 3) { h.code = RDX_BLOSC2_FAILED; return h; }
     for (int k = 0; k < 6; ++k)
         if (f[k] == 3 || f[k] > 4) { h.code = RDX_BLOSC2_UNSUPPORTED; return h; }
     h.filt = 0;
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args
     const uint64_t W = (uint64_t)a.wg_per_chunk * kWaves;
     const uint8_t *src = reinterpret_cast<const uint8_t *>(rfl64((uint64_t)gld<const uint8_t *>(a.in + c)));
     const uint64_t len = rfl64(gld<uint64_t>(a.in_len + c));
-    const Hdr h = parse(src, len, a.cap);
+    const Hdr h = parse(src, len, a.cap, a.z_in != nullptr);
     uint32_t *err = a.err + c;
     if (w0 == 0 && lane == 0) a.out_len[c] = h.code == 0 || h.code == RDX_INFLATE_OUTPUT_OVERFLOW ? h.nbytes : 0;
     if (h.code) {
@@ -467,6 +473,18 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args
             wave_fill(dst, neblock, (uint8_t)(-cb));
         } else if ((uint64_t)cb == neblock) {
             wave_copy(dst, src + pos, neblock);
+        } else if (h.codec == 3) {   // zlib: a row of the stream table, inflated by k_inflate next
+            uint32_t slot = 0;
+            if (lane == 0) slot = atomicAdd(a.z_count, 1u);
+            slot = rfl((uint32_t)__shfl((int)slot, 0, 64));
+            if (slot >= a.z_capacity) { fail(err, RDX_BLOSC2_UNSUPPORTED); return; }
+            if (lane == 0) {
+                a.z_in[slot] = src + pos;
+                a.z_len[slot] = (uint64_t)cb;
+                a.z_out[slot] = dst;
+                a.z_cap[slot] = neblock;
+                a.z_chunk[slot] = c;
+            }
         } else {
             const uint8_t *s = src + pos;
             const uint32_t skew = (uint32_t)((uintptr_t)s & 3);
@@ -493,7 +511,7 @@ __global__ __launch_bounds__(256) void k_blosc2_filter(const KBlosc2Args a) {
     if (gld<uint32_t>(a.err + c)) return;   // written by the decode launch before this one
     const uint8_t *src = reinterpret_cast<const uint8_t *>(gld<const uint8_t *>(a.in + c));
     const uint64_t len = gld<uint64_t>(a.in_len + c);
-    const Hdr h = parse(src, len, a.cap);
+    const Hdr h = parse(src, len, a.cap, a.z_in != nullptr);
     if (h.code || h.mode != M_BLOCKS || !h.nfilt) return;
     uint8_t *outc = a.out + (uint64_t)c * a.cap, *scr = a.scratch + (uint64_t)c * a.cap;
     const uint32_t ts = h.ts;
@@ -565,6 +583,26 @@ __global__ __launch_bounds__(256) void k_blosc2_filter(const KBlosc2Args a) {
             __syncthreads();
         }
     }
+}
+
+// Results of the zlib-coded streams (k_inflate over the table): a stream that failed or did not produce
+// exactly its block share fails its chunk, as blosc_d's size check.
+__global__ __launch_bounds__(256) void k_blosc2_zcheck(const KBlosc2Args a) {
+    const uint32_t n = __hip_atomic_load(a.z_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n && i < a.z_capacity;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        if (a.z_err[i] != 0 || a.z_out_len[i] != a.z_cap[i]) atomicCAS(a.err + a.z_chunk[i], 0u, (uint32_t)RDX_BLOSC2_FAILED);
+}
+
+hipError_t launch_blosc2_zcheck(const KBlosc2Args &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    if (a.z_in) {
+        hipLaunchKernelGGL(k_blosc2_zcheck, dim3(256), dim3(256), 0, s, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_blosc2_filter, dim3(a.n * a.wg_per_chunk), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_blosc2(const KBlosc2Args &a, bool filters, hipStream_t s) {

@@ -152,7 +152,12 @@ struct KInflateArgs {
     uint64_t *out_len;
     uint32_t *err;
     uint32_t format;           // RDX_COMPRESSION_GZIP / ZLIB
-    uint32_t n;                // streams
+    uint32_t n;                // streams (the grid's capacity when n_dev is set)
+    // stream tables filled on the device (blosc2 chunks with zlib-coded streams, k_blosc2.hip): the
+    // stream count in device memory, and per stream its own output pointer and capacity
+    const uint32_t *n_dev;
+    uint8_t *const *out_ptrs;
+    const uint64_t *caps;
 };
 
 template <uint32_t RING>
@@ -1045,6 +1050,10 @@ struct Inflater {
 template <uint32_t RING, uint32_t WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
     constexpr uint32_t kThreads = 64 * WAVES;
+    // a device-side stream count: workgroups past it leave before building their tables
+    uint32_t n = a.n;   // with a device-side count: never past the table (the grid covers a.n rows)
+    if (a.n_dev) n = min(n, rfl(__hip_atomic_load(a.n_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    if ((uint64_t)blockIdx.x * WAVES >= n) return;
     __shared__ InflateShared S;
     __shared__ InflateLds<RING> LW[WAVES];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1087,7 +1096,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
     if (t < 64) S.x_after[t] = x8n(S, (Inflater<RING>::kFlush / 64) * (63 - t));
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * WAVES + wave;
-    if (i >= a.n) return;
+    if (i >= n) return;
     InflateLds<RING> &L = LW[wave];
     // scalar: every lane reads the same descriptor, and the decode state derived from it must stay
     // wave-uniform (SGPRs) for the serial path to compile to scalar code
@@ -1103,8 +1112,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
     f.pos = 0;
     f.bb = 0;
     f.bc = 0;
-    f.dst = a.out + (uint64_t)i * a.cap;
-    f.cap = a.cap;
+    f.dst = a.out_ptrs ? reinterpret_cast<uint8_t *>(rfl64((uint64_t)gld<uint8_t *>(a.out_ptrs + i)))
+                       : a.out + (uint64_t)i * a.cap;
+    f.cap = a.caps ? rfl64(gld<uint64_t>(a.caps + i)) : a.cap;
     f.out = f.flushed = 0;
     f.crc = 0xffffffffu;  // raw CRC-32 register
     f.s1 = 0;
@@ -1191,7 +1201,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
 hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uint64_t *d_in_len, uint64_t n,
                           uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    KInflateArgs a{d_in, d_in_len, d_out, cap, d_out_len, d_err, format, (uint32_t)n};
+    KInflateArgs a{d_in, d_in_len, d_out, cap, d_out_len, d_err, format, (uint32_t)n, nullptr, nullptr, nullptr};
     // ring size from the batch size (InflateLds); RDX_INFLATE_RING=8192/16384/32768 forces one (tuning)
     static const int force = [] {
         const char *v = std::getenv("RDX_INFLATE_RING");
@@ -1205,6 +1215,19 @@ hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uin
     } else {
         hipLaunchKernelGGL((k_inflate<8192, 4>), dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+// Streams described by device tables (k_blosc2's zlib-coded block streams): up to max_n, the actual count
+// in *d_n; stream i -> d_out_ptrs[i] with capacity d_caps[i].  Many short streams: 8 KiB rings, 4 per
+// workgroup.
+hipError_t launch_inflate_table(const uint8_t *const *d_in, const uint64_t *d_in_len, uint8_t *const *d_out_ptrs,
+                                const uint64_t *d_caps, const uint32_t *d_n, uint64_t max_n, uint64_t *d_out_len,
+                                uint32_t *d_err, hipStream_t s) {
+    if (max_n == 0) return hipSuccess;
+    KInflateArgs a{d_in, d_in_len, nullptr, 0, d_out_len, d_err, RDX_COMPRESSION_ZLIB, (uint32_t)max_n, d_n, d_out_ptrs,
+                   d_caps};
+    hipLaunchKernelGGL((k_inflate<8192, 4>), dim3((uint32_t)((max_n + 3) / 4)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -193,6 +193,17 @@ struct KBlosc2Args {
     uint32_t *err;              // rdx_inflate_error; zeroed by the caller before the launch
     uint32_t n;
     uint32_t wg_per_chunk;      // workgroups (4 decoding waves each) per chunk
+    // zlib-coded block streams are not decoded here but appended to this table (slot = atomic counter)
+    // and inflated by k_inflate afterwards; null: such chunks fail with RDX_BLOSC2_UNSUPPORTED
+    const uint8_t **z_in;       // stream start
+    uint64_t *z_len;            // csize
+    uint8_t **z_out;            // destination (decode scratch or output)
+    uint64_t *z_cap;            // expected size (neblock)
+    uint32_t *z_chunk;          // chunk index
+    uint64_t *z_out_len;        // k_inflate: bytes produced
+    uint32_t *z_err;            // k_inflate: rdx_inflate_error
+    uint32_t *z_count;          // entries used (zeroed by the caller)
+    uint64_t z_capacity;
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

@@ -23,8 +23,14 @@ hipError_t launch_cbor(const KCbor &m, uint32_t blocks, hipStream_t s);
 // k_inflate.hip: gzip / zlib streams (format = rdx_compression), one wavefront per stream
 hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uint64_t *d_in_len, uint64_t n,
                           uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s);
+hipError_t launch_inflate_table(const uint8_t *const *d_in, const uint64_t *d_in_len, uint8_t *const *d_out_ptrs,
+                                const uint64_t *d_caps, const uint32_t *d_n, uint64_t max_n, uint64_t *d_out_len,
+                                uint32_t *d_err, hipStream_t s);
 // k_blosc2.hip: blosc2 chunks (decode launch, then the filter launch when `filters`)
 hipError_t launch_blosc2(const KBlosc2Args &a, bool filters, hipStream_t s);
+// after launch_blosc2(a, false) and the zlib-coded streams' inflate (launch_inflate_table): fold their
+// results into the chunks' errors, then the filter launch
+hipError_t launch_blosc2_zcheck(const KBlosc2Args &a, hipStream_t s);
 
 #define RDX_DECLARE_DTYPE(tn)                                                                                  \
     hipError_t launch_all_contig_##tn(uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s);    \

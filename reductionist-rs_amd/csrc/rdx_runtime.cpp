@@ -106,6 +106,11 @@ struct rdx_workspace {
     DevBuf<uint32_t> zerr;
     DevBuf<uint8_t> raw;
     DevBuf<uint8_t> zscratch;   // blosc2: decoded blocks before their filters (k_blosc2_filter)
+    // blosc2: the table of zlib-coded block streams k_blosc2_decode hands to k_inflate
+    DevBuf<const uint8_t *> zt_in;
+    DevBuf<uint64_t> zt_len, zt_cap, zt_out_len;
+    DevBuf<uint8_t *> zt_out;
+    DevBuf<uint32_t> zt_chunk, zt_err, zt_count;
     std::vector<uint8_t> last_zptrs, last_zlens;
     // rdx_execute_cbor: the encoded response and its length
     DevBuf<uint8_t> cbor;
@@ -508,7 +513,28 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
         a.n = (uint32_t)n;
         // waves per chunk: enough for one chunk's streams to fill the chip (4 waves per workgroup)
         a.wg_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(128, 1024 / n));
-        RDX_HIP(launch_blosc2(a, true, s));
+        // zlib-coded streams: up to 512 per chunk (at least 8192 in all) go through k_inflate, whose grid
+        // covers the table; a chunk with more fails with RDX_BLOSC2_UNSUPPORTED (the host decompresses it)
+        const uint64_t zcap = std::max<uint64_t>(8192, n * 512);
+        if ((st = ensure(ws, ws->zt_in, zcap, s)) || (st = ensure(ws, ws->zt_len, zcap, s)) ||
+            (st = ensure(ws, ws->zt_cap, zcap, s)) || (st = ensure(ws, ws->zt_out_len, zcap, s)) ||
+            (st = ensure(ws, ws->zt_out, zcap, s)) || (st = ensure(ws, ws->zt_chunk, zcap, s)) ||
+            (st = ensure(ws, ws->zt_err, zcap, s)) || (st = ensure(ws, ws->zt_count, 1, s)))
+            return st;
+        RDX_HIP(hipMemsetAsync(ws->zt_count.p, 0, sizeof(uint32_t), s));
+        a.z_in = ws->zt_in.p;
+        a.z_len = ws->zt_len.p;
+        a.z_out = ws->zt_out.p;
+        a.z_cap = ws->zt_cap.p;
+        a.z_chunk = ws->zt_chunk.p;
+        a.z_out_len = ws->zt_out_len.p;
+        a.z_err = ws->zt_err.p;
+        a.z_count = ws->zt_count.p;
+        a.z_capacity = zcap;
+        RDX_HIP(launch_blosc2(a, false, s));
+        RDX_HIP(launch_inflate_table(ws->zt_in.p, ws->zt_len.p, ws->zt_out.p, ws->zt_cap.p, ws->zt_count.p, zcap,
+                                     ws->zt_out_len.p, ws->zt_err.p, s));
+        RDX_HIP(launch_blosc2_zcheck(a, s));
         return RDX_OK;
     }
     RDX_HIP(launch_inflate(compression, ws->zptrs.p, ws->zlens.p, n, d_out, cap, d_out_len, d_err, s));
@@ -604,6 +630,15 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->zout_len.p);
     fr(ws->zerr.p);
     fr(ws->raw.p);
+    fr(ws->zscratch.p);
+    fr((void *)ws->zt_in.p);
+    fr(ws->zt_len.p);
+    fr(ws->zt_cap.p);
+    fr(ws->zt_out_len.p);
+    fr((void *)ws->zt_out.p);
+    fr(ws->zt_chunk.p);
+    fr(ws->zt_err.p);
+    fr(ws->zt_count.p);
     fr(ws->cbor.p);
     fr(ws->cbor_len.p);
     if (ws->aux_stream) {

@@ -54,8 +54,6 @@ def device_blosc2(torch, ws, chunks, cap, skew=0):
 
 def expected(c, cap):
     e, d = oracle.blosc2_decompress(c, cap=cap)
-    if e == 0 and c[2] >> 5 == B.ZLIB and not (c[2] & 2):
-        return _abi.BLOSC2_UNSUPPORTED, b""   # zlib-coded streams: oracle only (k_blosc2.hip header)
     return e, d if e == 0 else b""
 
 
