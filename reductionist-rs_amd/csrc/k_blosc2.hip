@@ -204,12 +204,18 @@ struct LzStream {
     uint8_t *dst;
     uint32_t n, op, flushed;
 
-    // The next unit's words, in flight until stage() stores them: addresses are clamped to the stream's
-    // last word (no branch, so no wait right behind each load); bytes past the end are never parsed.
     __device__ __forceinline__ void load_unit(uint32_t start) {
-        const uint32_t w0 = start / 4 + (uint32_t)lane * (kStage / 4 / 64), last = (end - 1) / 4;
+        const uint32_t w0 = start / 4 + (uint32_t)lane * (kStage / 4 / 64);
 #pragma unroll
-        for (int k = 0; k < (int)(kStage / 4 / 64); ++k) pf[k] = gld<uint32_t>(srcw + (w0 + k < last ? w0 + k : last));
+        for (int k = 0; k < (int)(kStage / 4 / 64); ++k) {
+            const uint32_t w = w0 + k;
+            pf[k] = 0;
+            if (w * 4 < end) {
+                pf[k] = gld<uint32_t>(srcw + w);
+                const uint32_t valid = end - w * 4;
+                if (valid < 4) pf[k] &= (1u << (8 * valid)) - 1;
+            }
+        }
     }
     __device__ __forceinline__ void stage() {
         const uint32_t i0 = (uint32_t)(staged / 4 + (uint32_t)lane * (kStage / 4 / 64));

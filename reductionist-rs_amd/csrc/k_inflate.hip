@@ -21,6 +21,7 @@
 //     combined (CRC-32: each slice CRC shifted past the bytes after it by one GF(2) multiplication
 //     and XOR-reduced, the running CRC folded into lane 0's slice; Adler-32: weighted sums).
 // LDS per wave ≈ ring + 8.5 KiB; ring and streams per workgroup chosen per launch (InflateLds).
+#include <algorithm>
 #include <cstdlib>
 
 #include "rdx_device.hpp"
@@ -1095,9 +1096,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
     }
     if (t < 64) S.x_after[t] = x8n(S, (Inflater<RING>::kFlush / 64) * (63 - t));
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * WAVES + wave;
-    if (i >= n) return;
     InflateLds<RING> &L = LW[wave];
+    // stream i = this wave's index, then every gridDim.x * WAVES further (a stream table's grid is smaller
+    // than the table: one workgroup's tables serve several streams)
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+    for (uint64_t i = (uint64_t)blockIdx.x * WAVES + wv; i < n; i += (uint64_t)gridDim.x * WAVES) {
     // scalar: every lane reads the same descriptor, and the decode state derived from it must stay
     // wave-uniform (SGPRs) for the serial path to compile to scalar code
     const uint8_t *src = reinterpret_cast<const uint8_t *>(rfl64((uint64_t)gld<const uint8_t *>(a.in + i)));
@@ -1194,6 +1197,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_inflate(const KInflateArgs a) {
         for (int k = 0; k < P_N; ++k) atomicAdd(&g_prof[k], (unsigned long long)f.prof[k]);
 #endif
     }
+    }
 }
 
 }  // namespace
@@ -1220,14 +1224,15 @@ hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uin
 
 // Streams described by device tables (k_blosc2's zlib-coded block streams): up to max_n, the actual count
 // in *d_n; stream i -> d_out_ptrs[i] with capacity d_caps[i].  Many short streams: 8 KiB rings, 4 per
-// workgroup.
+// workgroup, at most 1024 workgroups looping over the rows (an empty table costs one small launch).
 hipError_t launch_inflate_table(const uint8_t *const *d_in, const uint64_t *d_in_len, uint8_t *const *d_out_ptrs,
                                 const uint64_t *d_caps, const uint32_t *d_n, uint64_t max_n, uint64_t *d_out_len,
                                 uint32_t *d_err, hipStream_t s) {
     if (max_n == 0) return hipSuccess;
     KInflateArgs a{d_in, d_in_len, nullptr, 0, d_out_len, d_err, RDX_COMPRESSION_ZLIB, (uint32_t)max_n, d_n, d_out_ptrs,
                    d_caps};
-    hipLaunchKernelGGL((k_inflate<8192, 4>), dim3((uint32_t)((max_n + 3) / 4)), dim3(256), 0, s, a);
+    const uint64_t wgs = std::min<uint64_t>((max_n + 3) / 4, 1024);   // workgroups loop over the rows
+    hipLaunchKernelGGL((k_inflate<8192, 4>), dim3((uint32_t)wgs), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
