@@ -1034,7 +1034,15 @@ def main():
     if local_rank >= n_dev and not oversub:
         raise SystemExit(f"bench.py: rank {rank} (local {local_rank}) has no GPU of its own ({n_dev} visible)")
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo reports its connections on stdout; keep stdout for the one JSON line (rank 0)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     device = local_rank % n_dev
     torch.cuda.set_device(device)
     cx = Ctx(torch, dist, args, world, rank, device)
