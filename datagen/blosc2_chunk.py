@@ -61,8 +61,10 @@ def shuffle_block(b: bytes, ts: int) -> bytes:
     return a.T.tobytes() + b[ne * ts:]
 
 
-def bitshuffle_block(b: bytes, ts: int) -> bytes:
+def bitshuffle_block(b: bytes, ts: int, version: int = 5) -> bytes:
     size = len(b) // ts
+    if version == 2 and size % 8:
+        return b     # c-blosc 1.x (header version 2) stores such a block unshuffled
     size -= size % 8
     if size == 0:
         return b
@@ -130,7 +132,7 @@ def build(data: bytes, typesize: int = 4, blocksize: int | None = None, codec: i
             if f == SHUFFLE:
                 blk = shuffle_block(blk, typesize)
             elif f == BITSHUFFLE:
-                blk = bitshuffle_block(blk, typesize)
+                blk = bitshuffle_block(blk, typesize, version)
         ns = typesize if (split and not left) else 1
         ne = len(blk) // ns
         bstarts.append(base + len(body))

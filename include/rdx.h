@@ -42,7 +42,8 @@ typedef enum rdx_status {
     RDX_E_NAN_UNORDERED = 7,       /* operations.rs:181-183,355-357 NaN in min/max — reference panics with
                                       "unexpected undefined order error for min"                            */
     RDX_E_UNSUPPORTED = 8,         /* a blosc2 codec / filter not decoded on the device (RDX_BLOSC2_UNSUPPORTED:
-                                      zstd, snappy, dictionaries, delta) / rank > 32                     */
+                                      zstd, snappy, dictionaries, delta) / rank > 32 / views of >= 2^32
+                                      elements: the cause is rdx_last_unsupported_reason()             */
     RDX_E_DEVICE = 9,              /* HIP runtime error                                                      */
     RDX_E_OUT_OF_MEMORY = 10,      /* device or pinned allocation failed                                     */
     RDX_E_BUFFER_TOO_SMALL = 11,   /* caller-provided output buffer smaller than rdx_plan() reported        */
@@ -75,6 +76,19 @@ typedef enum rdx_inflate_error {
     RDX_BLOSC2_UNSUPPORTED = 15      /* a codec / flag not decoded here (zstd, snappy, dictionaries,
                                         user-defined codecs or filters, delta): status RDX_E_UNSUPPORTED */
 } rdx_inflate_error;
+
+/* Why this thread's last RDX_E_UNSUPPORTED was returned (rdx_last_unsupported_reason).  Only BLOSC2_CODEC
+ * concerns the chunk's encoding (decompress it on the host and call again); every other reason is a request
+ * the reference serves that this engine does not plan (run the reference's CPU path for it). */
+typedef enum rdx_unsupported_reason {
+    RDX_UNSUPPORTED_NONE = 0,
+    RDX_UNSUPPORTED_BLOSC2_CODEC = 1, /* RDX_BLOSC2_UNSUPPORTED: zstd, snappy, dictionaries, delta, user codecs */
+    RDX_UNSUPPORTED_RANK = 2,         /* request rank above RDX_MAX_NDIM                                    */
+    RDX_UNSUPPORTED_VIEW_SIZE = 3,    /* a view of 2^32 or more elements, or a dim of 2^32 or more            */
+    RDX_UNSUPPORTED_VIEW_DIMS = 4,    /* more than 16 dims left after canonicalisation                       */
+    RDX_UNSUPPORTED_MISSING_LIST = 5, /* a missing_values list of 2^32 or more entries                       */
+    RDX_UNSUPPORTED_CBOR_SIZE = 6     /* a CBOR count vector of 2^43 or more entries                          */
+} rdx_unsupported_reason;
 
 /* ---- request enums (src/models.rs) ------------------------------------------------------------ */
 typedef enum rdx_op { /* routes /v2/{count,max,min,select,sum}, src/app.rs:61-71 */
@@ -193,6 +207,8 @@ rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out);
 /* Message for an rdx_inflate_error, and the detail of this thread's last RDX_E_DECOMPRESSION. */
 const char *rdx_inflate_error_string(uint32_t code);
 uint32_t rdx_inflate_last_error(void);
+/* The rdx_unsupported_reason of this thread's last RDX_E_UNSUPPORTED. */
+uint32_t rdx_last_unsupported_reason(void);
 /* blosc2_cbuffer_sizes (src/compression.rs:33, blusc 0.0.2 / c-blosc2): the sizes a blosc chunk's
  * 16-byte header states; all three 0 when it is not a valid header (the reference's "invalid blosc2
  * compressed data").  Host only: sizes the output of rdx_decompress_batch_device. */

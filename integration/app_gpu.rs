@@ -53,17 +53,23 @@ pub fn operation_gpu<T: operation::Operation>(
         }
     }
     let (request_data, data) = match request_data.compression {
-        Some(c) => {
-            let d = compression::decompress(c, &data)?;
-            let mut rd = request_data;
-            rd.compression = None;
-            (rd, d)
-        }
+        Some(c) => (host_decompressed(request_data), compression::decompress(c, &data)?),
         None => (request_data, data),
     };
     // Bytes -> Vec<u8> without a copy, as the reference asserts (app.rs:173-181)
     let vec: Vec<u8> = data.into();
     debug_span!("operation_gpu").in_scope(|| T::execute(&request_data, vec))
+}
+
+/// The request that goes to the engine with a chunk this host has already decompressed.  `compression`
+/// is cleared and so is `size`: the reference runs validate_raw_size on the decompressed length whenever
+/// the request was compressed (app.rs:169-172), and the engine runs it exactly when `size` is absent
+/// (`size` of a compressed request is the compressed length, models.rs:244-249, and is no use to it).
+fn host_decompressed(request_data: models::RequestData) -> models::RequestData {
+    let mut rd = request_data;
+    rd.compression = None;
+    rd.size = None;
+    rd
 }
 
 /// A handler variant whose response body the engine serialises (operations_gpu::execute_cbor): the same
@@ -84,9 +90,7 @@ pub async fn operation_handler_cbor<const OP: u32>(
         let (request_data, data) = match request_data.compression {
             Some(c) if c != models::Compression::Blosc2 => {
                 let d = compression::decompress(c, &data)?;
-                let mut rd = request_data;
-                rd.compression = None;
-                (rd, d)
+                (host_decompressed(request_data), d)
             }
             _ => (request_data, data),
         };
@@ -94,9 +98,7 @@ pub async fn operation_handler_cbor<const OP: u32>(
             // a blosc2 codec the device does not decode: decompress on the host and run again
             Err(ActiveStorageError::UnsupportedOperation { .. }) if request_data.compression.is_some() => {
                 let d = compression::decompress(request_data.compression.unwrap(), &data)?;
-                let mut rd = request_data;
-                rd.compression = None;
-                operations_gpu::execute_cbor::<OP>(&rd, &d)
+                operations_gpu::execute_cbor::<OP>(&host_decompressed(request_data), &d)
             }
             other => other,
         }

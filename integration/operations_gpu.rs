@@ -29,7 +29,7 @@ static CTX: OnceLock<Ctx> = OnceLock::new();
 
 pub fn init(devices: &[i32]) -> Result<(), ActiveStorageError> {
     let mut ctx = std::ptr::null_mut();
-    check(unsafe { rdx_context_create(devices.as_ptr(), devices.len() as i32, &mut ctx) }, None)?;
+    check(unsafe { rdx_context_create(devices.as_ptr(), devices.len() as i32, &mut ctx) }, None, DType::Float64)?;
     let _ = CTX.set(Ctx(ctx));
     Ok(())
 }
@@ -52,10 +52,11 @@ impl<const OP: u32> Operation for Gpu<OP> {
         let mut res: *mut RdxResult = std::ptr::null_mut();
         // One call, any request (compressed chunks included): the engine sizes and allocates the
         // response in page-locked memory (include/rdx.h rdx_execute_owned).
-        check(
-            unsafe { rdx_execute_owned(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, &mut res) },
-            rd.compression,
-        )?;
+        let st = unsafe { rdx_execute_owned(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, &mut res) };
+        if planned_on_cpu(st) {
+            return cpu_operation::<OP>(rd, data);
+        }
+        check(st, rd.compression, rd.dtype)?;
         let owner = Owned(res);
         let info = unsafe { (*res).info };
         let shape: Vec<usize> = info.shape[..info.ndim as usize].iter().map(|&s| s as usize).collect();
@@ -73,6 +74,28 @@ impl<const OP: u32> Operation for Gpu<OP> {
     }
 }
 
+/// RDX_E_UNSUPPORTED for a reason other than the chunk's blosc2 codec: a request the reference serves
+/// that the engine does not plan (rank above 32, views of 2^32 or more elements; include/rdx.h
+/// rdx_unsupported_reason).  It runs on the reference's own CPU path instead of failing.
+fn planned_on_cpu(st: i32) -> bool {
+    st == status::E_UNSUPPORTED && unsafe { rdx_last_unsupported_reason() } != unsupported::BLOSC2_CODEC
+}
+
+/// The reference's synchronous path for this route, unchanged: `operation::<T>` (app.rs:163-183: the
+/// filter pipeline, validate_raw_size, then the CPU plugin of operations.rs).  `app::operation` becomes
+/// `pub(crate)` for this.
+fn cpu_operation<const OP: u32>(rd: &models::RequestData, data: Vec<u8>) -> Result<models::Response, ActiveStorageError> {
+    use crate::operations;
+    let (rd, data) = (rd.clone(), Bytes::from(data));
+    match OP {
+        0 => crate::app::operation::<operations::Count>(rd, data),
+        1 => crate::app::operation::<operations::Max>(rd, data),
+        2 => crate::app::operation::<operations::Min>(rd, data),
+        3 => crate::app::operation::<operations::Select>(rd, data),
+        _ => crate::app::operation::<operations::Sum>(rd, data),
+    }
+}
+
 /// The response of `Gpu<OP>` as the reference's HTTP body — `serde_cbor::to_vec(&CBORResponse::new(..))`
 /// (app.rs:33-40, models.rs:355-416) — serialised by the engine on the device (`rdx_execute_cbor`):
 /// a large count vector (axis reductions with many outputs, `axis: []`) crosses PCIe as CBOR integers
@@ -83,12 +106,13 @@ pub fn execute_cbor<const OP: u32>(rd: &models::RequestData, data: &[u8]) -> Res
     let flags = if rd.option_shape_as_bytes.unwrap_or(false) { RDX_CBOR_SHAPE_AS_BYTES } else { 0 }
         | if rd.option_count_as_bytes.unwrap_or(false) { RDX_CBOR_COUNT_AS_BYTES } else { 0 };
     let mut res: *mut RdxResult = std::ptr::null_mut();
-    check(
-        unsafe {
-            rdx_execute_cbor(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, flags, &mut res)
-        },
-        rd.compression,
-    )?;
+    let st = unsafe { rdx_execute_cbor(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, flags, &mut res) };
+    if planned_on_cpu(st) {
+        // the reference's path and its own serialisation (app.rs:31-43)
+        let response = cpu_operation::<OP>(rd, data.to_vec())?;
+        return Ok(Bytes::from(serde_cbor::to_vec(&models::CBORResponse::new(&response)).unwrap()));
+    }
+    check(st, rd.compression, rd.dtype)?;
     Ok(Bytes::from_owner(OwnedCbor(res)))
 }
 
@@ -258,6 +282,18 @@ fn marshal_missing(dtype: DType, m: &Missing<crate::types::DValue>) -> Result<(u
     }
 }
 
+/// `std::any::type_name::<T>()` of the element type, as array.rs:22-24 reports it in `FromBytes`.
+fn type_name_of(d: DType) -> &'static str {
+    match d {
+        DType::Int32 => std::any::type_name::<i32>(),
+        DType::Int64 => std::any::type_name::<i64>(),
+        DType::Uint32 => std::any::type_name::<u32>(),
+        DType::Uint64 => std::any::type_name::<u64>(),
+        DType::Float32 => std::any::type_name::<f32>(),
+        DType::Float64 => std::any::type_name::<f64>(),
+    }
+}
+
 fn dtype_code(d: DType) -> u32 {
     match d {
         DType::Int32 => 0,
@@ -281,7 +317,7 @@ fn dtype_of(code: u32) -> DType {
 }
 
 /// rdx_status -> the ActiveStorageError the reference raises for the same condition (error.rs:242-376).
-pub fn check(st: i32, compression: Option<Compression>) -> Result<(), ActiveStorageError> {
+pub fn check(st: i32, compression: Option<Compression>, dtype: DType) -> Result<(), ActiveStorageError> {
     use status::*;
     match st {
         OK => Ok(()),
@@ -290,7 +326,7 @@ pub fn check(st: i32, compression: Option<Compression>) -> Result<(), ActiveStor
             validator::ValidationError::new("request data is not valid"),
         )),
         // array.rs:18-27 zerocopy length / alignment -> 500 (error.rs:271)
-        E_FROM_BYTES => Err(ActiveStorageError::FromBytes { type_name: "T" }),
+        E_FROM_BYTES => Err(ActiveStorageError::FromBytes { type_name: type_name_of(dtype) }),
         // array.rs:58-63 ndarray from_shape -> 400
         E_SHAPE_INVALID => {
             Err(ActiveStorageError::ShapeInvalid(ndarray::ShapeError::from_kind(ndarray::ErrorKind::OutOfBounds)))
@@ -299,8 +335,9 @@ pub fn check(st: i32, compression: Option<Compression>) -> Result<(), ActiveStor
         E_SHUFFLE_LENGTH => panic!("assertion `left == right` failed"),
         // operations.rs:181-183,355-357: NaN in a min/max comparison panics in the reference; parity
         E_NAN_UNORDERED => panic!("unexpected undefined order error for min"),
-        // a blosc2 codec / filter the device does not decode (zstd, snappy, dictionaries,
-        // delta): app_gpu::operation_gpu catches this variant and decompresses on the host instead
+        // a blosc2 codec / filter the device does not decode (zstd, snappy, dictionaries, delta):
+        // app_gpu::operation_gpu catches this variant and decompresses on the host instead.  The other
+        // reasons never get here: Gpu<OP> serves them on the reference CPU path (planned_on_cpu).
         E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 codec on the GPU".into() }),
         // compression.rs:60-82 -> DecompressionFlate2 / DecompressionZune, 400 (error.rs:247-249)
         E_DECOMPRESSION => {

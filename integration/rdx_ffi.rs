@@ -19,6 +19,8 @@
 //!                                     new: device-resident, batched and heterogeneous entry points
 //!   rdx_decompress_batch_device       compression.rs:18-27 `decompress` for a batch of device streams
 //!   rdx_inflate_last_error / _string  the detail of RDX_E_DECOMPRESSION (error.rs:33-41)
+//!   rdx_last_unsupported_reason       the cause of RDX_E_UNSUPPORTED: a blosc2 codec (host decompression)
+//!                                     or a request only the reference CPU path plans (operations.rs)
 //!   rdx_execute_cbor                  app.rs:163-183 + app.rs:33-40: the response leaves the engine as
 //!                                     its CBOR body
 //!   rdx_cbor_bound / _encode / _encode_device
@@ -60,6 +62,17 @@ pub mod blosc2 {
     pub const FAILED: u32 = 13;       // "failed to decompress blosc2 data"
     pub const SIZE: u32 = 14;         // "unexpected decompressed size for blosc2 data"
     pub const UNSUPPORTED: u32 = 15;  // zstd / snappy / dictionaries / delta: host fallback
+}
+
+/// rdx_unsupported_reason (include/rdx.h): why the last RDX_E_UNSUPPORTED of this thread was returned.
+pub mod unsupported {
+    pub const NONE: u32 = 0;
+    pub const BLOSC2_CODEC: u32 = 1;  // decompress on the host, then call the engine again
+    pub const RANK: u32 = 2;          // every other reason: serve the request on the reference CPU path
+    pub const VIEW_SIZE: u32 = 3;
+    pub const VIEW_DIMS: u32 = 4;
+    pub const MISSING_LIST: u32 = 5;
+    pub const CBOR_SIZE: u32 = 6;
 }
 
 #[repr(C)]
@@ -158,6 +171,7 @@ extern "C" {
     pub fn rdx_missing_from_f64(dtype: u32, v: f64, out: *mut c_void) -> c_int;
     pub fn rdx_inflate_error_string(code: u32) -> *const c_char;
     pub fn rdx_inflate_last_error() -> u32;
+    pub fn rdx_last_unsupported_reason() -> u32;
     pub fn rdx_blosc2_cbuffer_sizes(
         src: *const c_void,
         len: u64,

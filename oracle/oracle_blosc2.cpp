@@ -179,8 +179,15 @@ void unshuffle(uint32_t ts, uint64_t bsize, const uint8_t *src, uint8_t *dst) {
 
 // bitunshuffle: over size = bsize / ts elements rounded down to a multiple of 8, row r = 8 * byte + bit
 // holds that bit of every element (element e at byte e / 8, bit e % 8 of the row); the rest copied.
-void bitunshuffle(uint32_t ts, uint64_t bsize, const uint8_t *src, uint8_t *dst) {
+// Chunks of header version 2 (written by c-blosc 1.x, e.g. numcodecs' Blosc) follow the older rule of
+// c-blosc2's bitunshuffle(..., format_version): a block whose element count is not a multiple of 8 was
+// stored unshuffled and is copied whole.
+void bitunshuffle(uint32_t ts, uint64_t bsize, const uint8_t *src, uint8_t *dst, uint32_t version) {
     uint64_t size = bsize / ts;
+    if (version == 2 && size % 8 != 0) {
+        std::memcpy(dst, src, bsize);
+        return;
+    }
     size -= size % 8;
     const uint64_t rowb = size / 8;
     std::memset(dst, 0, size * ts);
@@ -306,7 +313,7 @@ uint64_t decompress(const uint8_t *s, uint64_t len, uint8_t *out, uint64_t cap) 
                 unshuffle(h.typesize, bsize, cur, nxt);
                 std::swap(cur, nxt);
             } else if (h.filters[f] == FLT_BITSHUFFLE) {
-                bitunshuffle(h.typesize, bsize, cur, nxt);
+                bitunshuffle(h.typesize, bsize, cur, nxt, h.version);
                 std::swap(cur, nxt);
             }
         }

@@ -71,6 +71,7 @@ struct Hdr {
     uint32_t mode, flags, ts, codec, special, vts, overhead, nstreams;
     uint32_t filt;        // active decode filters, filters[5] first: 2 bits each (1 shuffle, 2 bitshuffle)
     uint32_t nfilt;
+    uint32_t version;     // header byte 0: version 2 (c-blosc 1.x) keeps the old bitshuffle leftover rule
     uint64_t nbytes, bs, cbytes, nblocks, leftover, items;
 };
 
@@ -86,6 +87,7 @@ __device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap, bool zlib) 
     h.ts = hb(3);
     const int32_t nb = h32(4), bs = h32(8), cb = h32(12);
     h.code = 0;
+    h.version = version;
     if (len < 16 || cb < 16 || version == 0 || version > 5 || bs <= 0 || (nb > 0 && bs > nb) || bs > 536866816 ||
         h.ts == 0 || nb <= 0) {
         h.code = RDX_BLOSC2_INVALID;
@@ -553,8 +555,11 @@ __global__ __launch_bounds__(256) void k_blosc2_filter(const KBlosc2Args a) {
                 }
                 for (uint64_t i = ne * ts + threadIdx.x; i < bsize; i += blockDim.x) B[i] = rd(A + i);
             } else {
+                // elements rounded down to a multiple of 8, the rest copied; a version-2 chunk's block
+                // whose element count is not a multiple of 8 was stored unshuffled and is copied whole
+                // (c-blosc2 bitunshuffle(..., format_version); oracle_blosc2.cpp bitunshuffle)
                 uint64_t size = bsize / ts;
-                size -= size % 8;
+                size = (h.version == 2 && size % 8) ? 0 : size - size % 8;
                 const uint64_t rowb = size / 8;
                 for (uint64_t g = threadIdx.x; g < rowb; g += blockDim.x) {
                     for (uint32_t k = 0; k < ts; ++k) {

@@ -48,7 +48,10 @@ __global__ __launch_bounds__(kBlock) void k_map(const KMap a) {
         }
         return o;
     };
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;  // nothing here can fail
+    // nothing here can fail, except the hand-off of Select's count: there the folding workgroup alone writes
+    // the status (finalize_count), so a detected fault is never overwritten by this store
+    constexpr bool kCountHandoff = KIND == 0 && MK != MK_NONE;
+    if (!kCountHandoff && blockIdx.x == 0 && threadIdx.x == 0 && a.out.status) *a.out.status = 0;
     for (uint64_t g0 = g_begin + threadIdx.x; g0 < g_end; g0 += stride * kU) {
         int64_t off[kU];
         bool ok[kU];

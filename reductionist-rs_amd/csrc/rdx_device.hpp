@@ -797,7 +797,7 @@ __device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint32_t *statu
         int64_t tot = 0;
         for (int k = 0; k < kBlock / 64; ++k) tot += part[k];
         *dst = tot;
-        if (s_fault && status) *status = RDX_E_DEVICE;
+        if (status) *status = s_fault ? (uint32_t)RDX_E_DEVICE : 0u;
         __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }

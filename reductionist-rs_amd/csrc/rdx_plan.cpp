@@ -16,6 +16,17 @@ uint32_t dtype_size(uint32_t dtype) {
     }
 }
 
+namespace {
+thread_local uint32_t g_unsupported = RDX_UNSUPPORTED_NONE;
+}
+
+rdx_status unsupported(uint32_t reason) {
+    g_unsupported = reason;
+    return RDX_E_UNSUPPORTED;
+}
+
+uint32_t last_unsupported() { return g_unsupported; }
+
 Div make_div(uint32_t d) {
     Div v{};
     v.d = d;
@@ -33,7 +44,7 @@ rdx_status basic_checks(const rdx_request &req) {
         req.order > RDX_ORDER_F || req.axes_kind > RDX_AXES_MULTI || req.compression > RDX_COMPRESSION_BLOSC2 ||
         req.missing.kind > RDX_MISSING_VALID_RANGE)
         return RDX_E_INVALID_ARGUMENT;
-    if (req.ndim > RDX_MAX_NDIM) return RDX_E_UNSUPPORTED;
+    if (req.ndim > RDX_MAX_NDIM) return unsupported(RDX_UNSUPPORTED_RANK);
     if (req.ndim && !req.shape) return RDX_E_INVALID_ARGUMENT;
     if (req.axes_kind == RDX_AXES_ONE && !req.axes) return RDX_E_INVALID_ARGUMENT;
     if (req.axes_kind == RDX_AXES_MULTI && req.n_axes && !req.axes) return RDX_E_INVALID_ARGUMENT;
@@ -146,7 +157,7 @@ rdx_status build_missing(const rdx_request &req, ExecPlan &p) {
                     case RDX_DTYPE_FLOAT32: p.miss_list = sorted_list<float>(m); break;
                     case RDX_DTYPE_FLOAT64: p.miss_list = sorted_list<double>(m); break;
                 }
-                if (p.miss_list.size() > 0xffffffffull) return RDX_E_UNSUPPORTED;
+                if (p.miss_list.size() > 0xffffffffull) return unsupported(RDX_UNSUPPORTED_MISSING_LIST);
                 km.n = (uint32_t)p.miss_list.size();
                 if (km.n <= (uint32_t)kInlineMissing) {  // collapsed by de-duplication
                     for (uint32_t i = 0; i < km.n; ++i) km.inl[i] = p.miss_list[i];
@@ -234,15 +245,15 @@ void fold_rank_strides(const std::vector<SDim> &sd, int64_t base_off, std::vecto
 }
 
 rdx_status fill_view(KView &v, const std::vector<CDim> &inner_first, int64_t base_off, int64_t r0, uint64_t n) {
-    if (inner_first.size() > (size_t)kMaxKDims) return RDX_E_UNSUPPORTED;
-    if (n > 0xffffffffull) return RDX_E_UNSUPPORTED;
+    if (inner_first.size() > (size_t)kMaxKDims) return unsupported(RDX_UNSUPPORTED_VIEW_DIMS);
+    if (n > 0xffffffffull) return unsupported(RDX_UNSUPPORTED_VIEW_SIZE);
     v = KView{};
     v.ndim = (int32_t)inner_first.size();
     v.base_off = base_off;
     v.r0 = r0;
     v.n = n;
     for (size_t k = 0; k < inner_first.size(); ++k) {
-        if (inner_first[k].count > 0xffffffffull) return RDX_E_UNSUPPORTED;
+        if (inner_first[k].count > 0xffffffffull) return unsupported(RDX_UNSUPPORTED_VIEW_SIZE);
         v.count[k] = (uint32_t)inner_first[k].count;
         v.div[k] = make_div((uint32_t)inner_first[k].count);
         v.vstride[k] = inner_first[k].vs;

@@ -36,6 +36,9 @@ rdx_status validate_request(const rdx_request &req);
 rdx_status make_plan(const rdx_request &req, uint64_t chunk_len, ExecPlan &plan);
 
 uint32_t dtype_size(uint32_t dtype);
+// RDX_E_UNSUPPORTED with its rdx_unsupported_reason recorded for this thread (rdx_last_unsupported_reason).
+rdx_status unsupported(uint32_t reason);
+uint32_t last_unsupported();
 Div make_div(uint32_t d);
 
 }  // namespace rdx

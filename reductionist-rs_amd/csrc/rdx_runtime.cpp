@@ -490,17 +490,22 @@ thread_local uint32_t g_inflate_error = RDX_INFLATE_OK;
 
 // compression::decompress (compression.rs:18-27) of n device-resident streams into d_out (stream i at
 // d_out + i*cap), asynchronous on s.
+// blosc2: `may_zlib` false when the caller has read every chunk's header on the host and none is
+// zlib-coded: no stream table, no k_inflate / zcheck launches.
+constexpr uint64_t kZTableMaxRows = 1ull << 20;   // 48 B per row: <= 48 MiB of HBM
+
 rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n, const uint8_t *const *h_ptrs,
                              const uint64_t *h_lens, uint8_t *d_out, uint64_t cap, uint64_t *d_out_len,
-                             uint32_t *d_err, hipStream_t s) {
+                             uint32_t *d_err, hipStream_t s, bool may_zlib = true) {
     rdx_status st;
     if ((st = ensure(ws, ws->zptrs, n, s))) return st;
     if ((st = ensure(ws, ws->zlens, n, s))) return st;
     if ((st = upload(ws, (void *)ws->zptrs.p, h_ptrs, n * sizeof(void *), ws->last_zptrs, s))) return st;
     if ((st = upload(ws, ws->zlens.p, h_lens, n * sizeof(uint64_t), ws->last_zlens, s))) return st;
     if (compression == RDX_COMPRESSION_BLOSC2) {
-        if (n > 0xffffffffull) return RDX_E_INVALID_ARGUMENT;
-        if ((st = ensure(ws, ws->zscratch, n * cap, s))) return st;
+        uint64_t scratch_bytes = 0;
+        if (n > 0xffffffffull || __builtin_mul_overflow(n, cap, &scratch_bytes)) return RDX_E_INVALID_ARGUMENT;
+        if ((st = ensure(ws, ws->zscratch, scratch_bytes, s))) return st;
         RDX_HIP(hipMemsetAsync(d_err, 0, n * sizeof(uint32_t), s));
         KBlosc2Args a{};
         a.in = ws->zptrs.p;
@@ -513,9 +518,16 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
         a.n = (uint32_t)n;
         // waves per chunk: enough for one chunk's streams to fill the chip (4 waves per workgroup)
         a.wg_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(128, 1024 / n));
-        // zlib-coded streams: up to 512 per chunk (at least 8192 in all) go through k_inflate, whose grid
-        // covers the table; a chunk with more fails with RDX_BLOSC2_UNSUPPORTED (the host decompresses it)
-        const uint64_t zcap = std::max<uint64_t>(8192, n * 512);
+        if (!may_zlib) {
+            RDX_HIP(launch_blosc2(a, false, s));
+            RDX_HIP(launch_blosc2_zcheck(a, s));   // (filters only: the table is absent)
+            return RDX_OK;
+        }
+        // zlib-coded streams go through k_inflate, whose grid covers the table: 512 rows per chunk of the
+        // batch, at least 8192 and at most kZTableMaxRows in all, handed out in arrival order across the
+        // batch; a stream that finds the table full fails its chunk with RDX_BLOSC2_UNSUPPORTED (the host
+        // decompresses that chunk)
+        const uint64_t zcap = std::min<uint64_t>(kZTableMaxRows, std::max<uint64_t>(8192, n * 512));
         if ((st = ensure(ws, ws->zt_in, zcap, s)) || (st = ensure(ws, ws->zt_len, zcap, s)) ||
             (st = ensure(ws, ws->zt_cap, zcap, s)) || (st = ensure(ws, ws->zt_out_len, zcap, s)) ||
             (st = ensure(ws, ws->zt_out, zcap, s)) || (st = ensure(ws, ws->zt_chunk, zcap, s)) ||
@@ -547,7 +559,7 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
 // RDX_INFLATE_OUTPUT_OVERFLOW, so a stream longer than the shape implies still decodes to its end and
 // meets validate_raw_size (app.rs:169-172) exactly like the reference.
 rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const uint8_t *d_src, uint64_t len,
-                              uint64_t size_hint, hipStream_t s, uint64_t *raw_len) {
+                              uint64_t size_hint, hipStream_t s, uint64_t *raw_len, const uint8_t *h_src = nullptr) {
     g_inflate_error = RDX_INFLATE_OK;
     const bool blosc2 = req.compression == RDX_COMPRESSION_BLOSC2;
     if (req.compression != RDX_COMPRESSION_GZIP && req.compression != RDX_COMPRESSION_ZLIB && !blosc2)
@@ -570,7 +582,10 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
         if ((st = ensure(ws, ws->raw, cap, s))) return st;
         const uint8_t *ptrs[1] = {d_src};
         const uint64_t lens[1] = {len};
-        if ((st = decompress_launch(ws, req.compression, 1, ptrs, lens, ws->raw.p, cap, ws->zout_len.p, ws->zerr.p, s)))
+        // a blosc2 chunk in host memory: its header says whether any stream can be zlib-coded (codec 3)
+        const bool may_zlib = !(blosc2 && h_src && len >= 16 && (h_src[2] >> 5) != 3);
+        if ((st = decompress_launch(ws, req.compression, 1, ptrs, lens, ws->raw.p, cap, ws->zout_len.p, ws->zerr.p, s,
+                                    may_zlib)))
             return st;
         RDX_HIP(hipMemcpyAsync(&ws->zback[0], ws->zout_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         RDX_HIP(hipMemcpyAsync(&ws->zback[1], ws->zerr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -584,7 +599,7 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
         }
         if (e != RDX_INFLATE_OK) {
             g_inflate_error = e;
-            return e == RDX_BLOSC2_UNSUPPORTED ? RDX_E_UNSUPPORTED : RDX_E_DECOMPRESSION;
+            return e == RDX_BLOSC2_UNSUPPORTED ? unsupported(RDX_UNSUPPORTED_BLOSC2_CODEC) : RDX_E_DECOMPRESSION;
         }
         *raw_len = ws->zback[0];
         return RDX_OK;
@@ -670,14 +685,14 @@ rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const v
     if ((L.body_len && !d_body) || (L.n_counts && !d_counts)) return RDX_E_INVALID_ARGUMENT;
     if (out_cap < L.fixed() + (L.count_array ? 9 * L.n_counts : 0)) return RDX_E_BUFFER_TOO_SMALL;
     if (L.a.size() + L.b.size() > (size_t)kCborFixedMax || L.d.size() + L.f.size() > (size_t)kCborTailMax)
-        return RDX_E_UNSUPPORTED;   // cannot happen: ndim <= RDX_MAX_NDIM bounds both
+        return unsupported(RDX_UNSUPPORTED_RANK);   // cannot happen: ndim <= RDX_MAX_NDIM bounds both
     KCbor m{};
     uint8_t *out = static_cast<uint8_t *>(d_out);
     m.out = out;
     m.counts = d_counts;
     m.n = L.count_array ? L.n_counts : 0;
     const uint64_t tiles = (m.n + 2047) / 2048;   // k_cbor.hip kCborTile
-    if (tiles > 0xffffffffull) return RDX_E_UNSUPPORTED;
+    if (tiles > 0xffffffffull) return unsupported(RDX_UNSUPPORTED_CBOR_SIZE);
     m.n_tiles = (uint32_t)tiles;
     m.c_off = L.c_off();
     m.b_off = L.b_off();
@@ -914,7 +929,7 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
                 uint64_t cb = 0, bs = 0;
                 rdx_blosc2_cbuffer_sizes(chunk, chunk_len, &hint, &cb, &bs);
             }
-            if ((r = decompress_request(ws, req, ws->chunk.p, chunk_len, hint, s, &len))) return r;
+            if ((r = decompress_request(ws, req, ws->chunk.p, chunk_len, hint, s, &len, chunk))) return r;
             src = ws->raw.p;
             if ((r = make_plan(req, len, p))) return r;
             *info = p.info;
@@ -1014,6 +1029,8 @@ const char *rdx_inflate_error_string(uint32_t code) {
 }
 
 uint32_t rdx_inflate_last_error(void) { return g_inflate_error; }
+
+uint32_t rdx_last_unsupported_reason(void) { return last_unsupported(); }
 
 // blosc2_cbuffer_sizes (blusc 0.0.2 / c-blosc2 read_chunk_header on the first 16 bytes), as the
 // reference calls it (compression.rs:33): all zeros when the header is not a valid blosc chunk.

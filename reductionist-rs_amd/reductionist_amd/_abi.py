@@ -28,6 +28,10 @@ INFLATE_OK, INFLATE_GZIP_HEADER, INFLATE_ZLIB_METHOD, INFLATE_ZLIB_HEADER, INFLA
     INFLATE_CHECKSUM, INFLATE_OUTPUT_OVERFLOW, BLOSC2_INVALID, BLOSC2_FAILED, BLOSC2_SIZE, \
     BLOSC2_UNSUPPORTED = range(16)
 
+# rdx_unsupported_reason (cause of E_UNSUPPORTED)
+UNSUPPORTED_NONE, UNSUPPORTED_BLOSC2_CODEC, UNSUPPORTED_RANK, UNSUPPORTED_VIEW_SIZE, UNSUPPORTED_VIEW_DIMS, \
+    UNSUPPORTED_MISSING_LIST, UNSUPPORTED_CBOR_SIZE = range(7)
+
 OPS = {"count": 0, "max": 1, "min": 2, "select": 3, "sum": 4}
 DTYPES = {"int32": 0, "int64": 1, "uint32": 2, "uint64": 3, "float32": 4, "float64": 5}
 DTYPE_SIZE = {"int32": 4, "int64": 8, "uint32": 4, "uint64": 8, "float32": 4, "float64": 8}
@@ -164,6 +168,7 @@ def _declare(lib):
         "rdx_execute_batch_device": (C.c_int, [VP, req_p, U64, P(VP), U64, VP, VP, VP, VP, info_p]),
         "rdx_inflate_error_string": (C.c_char_p, [C.c_uint32]),
         "rdx_inflate_last_error": (C.c_uint32, []),
+        "rdx_last_unsupported_reason": (C.c_uint32, []),
         "rdx_decompress_batch_device": (C.c_int, [VP, C.c_uint32, U64, P(VP), P(U64), VP, U64, VP, VP, VP]),
         "rdx_blosc2_cbuffer_sizes": (C.c_int, [VP, U64, P(U64), P(U64), P(U64)]),
         "rdx_execute_multi_device": (C.c_int, [VP, U64, P(rdx_multi_item), VP, P(C.c_uint32), info_p]),
@@ -189,7 +194,7 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
             "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
             "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device",
-            "rdx_execute_cbor", "rdx_blosc2_cbuffer_sizes"]
+            "rdx_execute_cbor", "rdx_blosc2_cbuffer_sizes", "rdx_last_unsupported_reason"]
 
 
 def lib():

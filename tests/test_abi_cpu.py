@@ -172,3 +172,44 @@ def test_no_device_fails_loudly():
     from reductionist_amd.errors import DeviceError
     with pytest.raises(DeviceError):
         Engine()
+
+
+def test_host_decompressed_request_runs_validate_raw_size():
+    """app.rs:169-172: a compressed request has its DECOMPRESSED length checked against the shape, whatever
+    `size` says (for a compressed request `size` is the compressed length, models.rs:244-249).  The Rust
+    plugin that inflates a lone gzip/zlib chunk on the host hands it to the engine with `compression` and
+    `size` both cleared (integration/app_gpu.rs host_decompressed); the engine runs validate_raw_size
+    exactly when `size` is absent, so the mismatch is still a 400."""
+    import gzip
+
+    lib = _abi.lib()
+    raw = np.arange(6, dtype=np.int32).tobytes()          # 6 elements behind a shape of 4
+    stream = gzip.compress(raw)
+    as_sent = _abi.CRequest("sum", "int32", shape=[4], compression="gzip", size=len(stream))
+    assert oracle.execute(as_sent, stream)[0] == _abi.E_REQUEST_VALIDATION   # the reference's answer
+    cleared = _abi.CRequest("sum", "int32", shape=[4])
+    info = _abi.rdx_response_info()
+    assert lib.rdx_plan(cleared.ref, len(raw), C.byref(info)) == _abi.E_REQUEST_VALIDATION
+    # keeping `size` would skip the check and reduce the first 4 elements (round-2 shim defect)
+    kept = _abi.CRequest("sum", "int32", shape=[4], size=len(stream))
+    assert lib.rdx_plan(kept.ref, len(raw), C.byref(info)) == 0
+    # a decompressed length that matches passes either way
+    assert lib.rdx_plan(cleared.ref, 16, C.byref(info)) == 0 and info.shape_list() == []
+
+
+def test_unsupported_carries_its_reason():
+    """RDX_E_UNSUPPORTED says why (rdx_last_unsupported_reason): only a blosc2 codec sends the plugin to host
+    decompression; a rank above 32 or a view of 2^32 elements sends it to the reference CPU path."""
+    lib = _abi.lib()
+    info = _abi.rdx_response_info()
+    deep = _abi.CRequest("sum", "int32", shape=[1] * 33)
+    assert lib.rdx_plan(deep.ref, 4, C.byref(info)) == _abi.E_UNSUPPORTED
+    assert lib.rdx_last_unsupported_reason() == _abi.UNSUPPORTED_RANK
+    # planning only (no data): a strided view of 2^32 f32 elements over a 32 GiB chunk
+    big = _abi.CRequest("sum", "float32", shape=[1 << 31, 4], selection=[[0, 1 << 31, 1], [0, 4, 2]])
+    assert lib.rdx_plan(big.ref, (1 << 31) * 16, C.byref(info)) == _abi.E_UNSUPPORTED
+    assert lib.rdx_last_unsupported_reason() == _abi.UNSUPPORTED_VIEW_SIZE
+    # the reason is per thread and only read after E_UNSUPPORTED: a good plan leaves it alone
+    ok = _abi.CRequest("sum", "int32")
+    assert lib.rdx_plan(ok.ref, 16, C.byref(info)) == 0
+    assert lib.rdx_last_unsupported_reason() == _abi.UNSUPPORTED_VIEW_SIZE

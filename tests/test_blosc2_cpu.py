@@ -143,3 +143,39 @@ def test_execute_blosc2_request_oracle():
                          filters=[{"id": "shuffle", "element_size": 4}])
     st, info, body, counts = oracle.execute(creq, c)
     assert st == 0 and struct.unpack("<f", body)[0] == float(vals.astype(np.float64).sum()) and counts == [30000]
+
+
+def v2_bitshuffle_chunks():
+    """Hand-built c-blosc 1.x chunks (header version 2, 16-byte header, BITSHUFFLE flag, BloscLZ codec id,
+    every stream stored raw: csize == stream size) -> (chunk, decoded bytes).  c-blosc 1.x bitshuffles a
+    block only when its element count is a multiple of 8 and stores any other block unshuffled; c-blosc2
+    decodes version-2 chunks by the same rule (bitunshuffle(..., format_version)).  Version 3+ instead
+    bitshuffles the first floor(n/8)*8 elements and leaves the tail."""
+    rng = np.random.default_rng(0xB175)
+    out = []
+    # (a) one block of 1001 f32 elements, one stream (DONTSPLIT): stored as it is
+    d = rng.integers(0, 1 << 31, 1001, dtype=np.uint32).tobytes()
+    h = struct.pack("<BBBBiii", 2, 1, 0x04 | 0x10, 4, len(d), len(d), 16 + 4 + 4 + len(d))
+    out.append((h + struct.pack("<i", 20) + struct.pack("<i", len(d)) + d, d))
+    # (b) a 2000-element block (bitshuffled, split into 4 raw streams) + a 1001-element leftover block
+    d = rng.integers(0, 1 << 31, 3001, dtype=np.uint32).tobytes()
+    blk0 = B.bitshuffle_block(d[:8000], 4)
+    assert blk0 != d[:8000]
+    streams0 = b"".join(struct.pack("<i", 2000) + blk0[k * 2000:(k + 1) * 2000] for k in range(4))
+    b0 = 16 + 8
+    b1 = b0 + len(streams0)
+    body = streams0 + struct.pack("<i", 4004) + d[8000:]
+    h = struct.pack("<BBBBiii", 2, 1, 0x04, 4, len(d), 8000, b0 + len(body))
+    out.append((h + struct.pack("<ii", b0, b1) + body, d))
+    return out
+
+
+def test_version2_bitshuffle_leftover_rule():
+    for c, d in v2_bitshuffle_chunks():
+        assert oracle.blosc2_decompress(c) == (0, d)
+        # the writer follows the same rule for version 2
+        assert B.bitshuffle_block(d[-4004:], 4, version=2) == d[-4004:]
+        # the same bytes read as a version-3 chunk take the newer rule: the odd block is bit-unshuffled
+        c3 = bytes([3]) + c[1:]
+        e3, d3 = oracle.blosc2_decompress(c3)
+        assert e3 == 0 and d3 != d and d3[-4:] == d[-4:]

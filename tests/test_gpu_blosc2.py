@@ -202,3 +202,17 @@ def test_execute_device_blosc2(torch, workspace):
     assert ost == 0 and int(status[0]) == 0
     assert body.cpu().numpy().tobytes()[:info.body_bytes] == obody
     assert counts.cpu().tolist()[:info.n_counts] == ocounts
+
+
+def test_version2_bitshuffle_leftover_rule(torch, workspace):
+    """c-blosc 1.x chunks (header version 2) with a block whose element count is not a multiple of 8: stored
+    unshuffled, copied whole (test_blosc2_cpu.v2_bitshuffle_chunks); read as version 3 they take the newer
+    rule.  Device == oracle == the original bytes."""
+    from test_blosc2_cpu import v2_bitshuffle_chunks
+    cases = v2_bitshuffle_chunks()
+    chunks = [c for c, _ in cases] + [bytes([3]) + c[1:] for c, _ in cases]
+    got = device_blosc2(torch, workspace, chunks, 16384)
+    for c, (e, out) in zip(chunks, got):
+        assert (e, out) == expected(c, 16384)
+    for (c, d), (e, out) in zip(cases, got):
+        assert e == 0 and out == d

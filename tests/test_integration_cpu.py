@@ -138,3 +138,31 @@ def test_plugins_cover_every_route_and_status():
         assert f"{code} =>" in ops, code
     assert "ChunkCacheError" not in ops
     assert "GpuEngine" in (ROOT / "integration" / "error_gpu.rs").read_text()
+
+
+def test_shim_clears_size_after_host_decompression():
+    """app.rs:169-172 validates the decompressed length of a compressed request; the engine does that only
+    when `size` is absent, so every host-decompressed request goes in with compression AND size cleared."""
+    app = (ROOT / "integration" / "app_gpu.rs").read_text()
+    fn = app[app.index("fn host_decompressed"):]
+    fn = fn[: fn.index("\n}\n")]
+    assert "rd.compression = None;" in fn and "rd.size = None;" in fn
+    # every host decompression hands its request through host_decompressed, and nothing else clears it
+    assert app.count("compression::decompress(") == 3
+    assert app.count("host_decompressed(") == 4          # the definition + three call sites
+    assert app.count("compression = None") == 1
+
+
+def test_shim_error_details_match_the_reference():
+    ops = (ROOT / "integration" / "operations_gpu.rs").read_text()
+    # array.rs:22-24: FromBytes carries std::any::type_name::<T>() of the element type
+    assert 'type_name: "T"' not in ops
+    assert "FromBytes { type_name: type_name_of(dtype) }" in ops
+    for t in ("i32", "i64", "u32", "u64", "f32", "f64"):
+        assert f"std::any::type_name::<{t}>()" in ops
+    # RDX_E_UNSUPPORTED: only the blosc2-codec reason becomes UnsupportedOperation (host decompression);
+    # the others run the reference's own operation::<T> on the CPU, in both plugin entry points
+    assert "rdx_last_unsupported_reason() } != unsupported::BLOSC2_CODEC" in ops
+    assert ops.count("if planned_on_cpu(st)") == 2
+    for op in ("Count", "Max", "Min", "Select", "Sum"):
+        assert f"crate::app::operation::<operations::{op}>(rd, data)" in ops
