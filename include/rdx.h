@@ -185,13 +185,44 @@ const char *rdx_status_string(rdx_status status);
 /* Number of visible gfx950 devices (0 when none / no driver). Never initialises anything else. */
 int rdx_device_count(void);
 
-/* A context is a pool over one or more devices (one chunk per device at a time, round-robin),
- * each with its own stream(s), pinned staging and workspace.  Thread-safe: rdx_execute may be
- * called concurrently from any number of host threads (src/app.rs:147-152 runs requests on
- * Tokio/Rayon worker threads).  devices == NULL / n_devices == 0 => device 0. */
+/* A context is a pool over one or more devices — the in-process multi-GPU server of app_state.rs:21-37
+ * (one process, requests on worker threads, src/app.rs:147-152).  Every entry of `devices` is one pool
+ * entry (a device listed twice is two entries on one GPU).  Thread-safe: rdx_execute* may be called
+ * concurrently from any number of host threads.  Each request goes to the entry with the fewest bytes
+ * of requests in flight; an entry holds up to max_workspaces workspaces (stream, buffers) and a caller
+ * that finds all of them busy waits for one (back-pressure, as the reference's resource manager
+ * semaphores, resource_manager.rs:54-89).  Concurrent small all-axes requests on one entry are coalesced:
+ * queued, and issued by whichever caller finds a launch lane free as ONE heterogeneous k_multi launch +
+ * one result copy; each caller returns when its own result is in host memory.
+ * devices == NULL / n_devices == 0 => device 0. */
 typedef struct rdx_context rdx_context;
 rdx_status rdx_context_create(const int *devices, int n_devices, rdx_context **out);
 void rdx_context_destroy(rdx_context *ctx);
+
+typedef struct rdx_context_config {
+    uint32_t max_workspaces;        /* per pool entry (0: 16); requests beyond it wait for a free one           */
+    uint32_t coalesce;              /* 1 (default): coalesce small all-axes requests into k_multi launches; 0: off */
+    uint32_t coalesce_lanes;        /* k_multi launches in flight per pool entry (0: 2)                        */
+    uint32_t reserved;
+    uint64_t coalesce_max_bytes;    /* rdx_execute_resident chunks up to this many bytes coalesce (0: 64 MiB)  */
+    uint64_t coalesce_host_max_bytes; /* rdx_execute / _owned host chunks up to this many (0: 1 MiB)           */
+} rdx_context_config;
+/* Applies to requests issued after it returns (call it before the context is shared). */
+rdx_status rdx_context_configure(rdx_context *ctx, const rdx_context_config *cfg);
+
+/* Bookkeeping of pool entry `index` (0 .. n_devices-1). */
+typedef struct rdx_device_stats {
+    int32_t device;                 /* HIP ordinal of the entry                                              */
+    uint32_t workspaces;            /* workspaces created (<= max_workspaces)                                */
+    uint32_t workspaces_busy;       /* held by a request right now                                            */
+    uint32_t max_workspaces;
+    uint64_t requests;              /* requests placed on this entry                                          */
+    uint64_t coalesced_requests;    /* of which served through a coalesced k_multi launch                     */
+    uint64_t coalesced_launches;    /* k_multi launches issued by the coalescer                               */
+    uint64_t outstanding_bytes;     /* chunk bytes of the requests in flight on this entry now                */
+    uint64_t waits;                 /* requests that waited for a free workspace                              */
+} rdx_device_stats;
+rdx_status rdx_context_stats(rdx_context *ctx, uint32_t index, rdx_device_stats *out);
 
 /* ---- host logic (no device needed) -------------------------------------------------------------- */
 /* models.rs:242-313 validate_request_data (+ missing validation, missing.rs:47-80, with typed values). */
@@ -259,6 +290,17 @@ rdx_status rdx_execute_owned(rdx_context *ctx, const rdx_request *req, const voi
 rdx_status rdx_execute_cbor(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len,
                             uint32_t flags, rdx_result **out);
 void rdx_result_free(rdx_context *ctx, rdx_result *result);
+
+/* rdx_execute for a chunk already resident in HBM of device `device` (a HIP ordinal of the context's pool):
+ * a device-side chunk cache (chunk_cache.rs keeps chunks in host memory; on the GPU server they can stay
+ * in HBM), or a chunk an earlier call left there.  Response into HOST buffers, synchronously, exactly as
+ * rdx_execute; the chunk is borrowed read-only.  Small all-axes requests are coalesced with concurrent
+ * callers' (rdx_context). */
+rdx_status rdx_execute_resident(rdx_context *ctx, int device, const rdx_request *req,
+                                const void *d_chunk, uint64_t chunk_len,
+                                void *body, uint64_t body_capacity,
+                                int64_t *counts, uint64_t counts_capacity,
+                                rdx_response_info *info);
 
 /* Device-resident path: everything already in HBM, nothing copied, asynchronous on `stream`.
  * A workspace holds the per-stream scratch (partials, arrival tickets, unshuffle buffers); use one

@@ -15,6 +15,9 @@
 //!   rdx_missing_from_{i64,u64,f64}    types/dvalue.rs:43-83 `TryFromDValue` (optional)
 //!   rdx_context_create / _destroy     new: device pool, built in `app::init` / `AppState::new`
 //!                                     (app.rs:46-53, app_state.rs:21-37)
+//!   rdx_context_configure / _stats    pool limits (resource_manager.rs:54-89's role on the device) and
+//!                                     request coalescing; per-device bookkeeping for metrics.rs
+//!   rdx_execute_resident              rdx_execute for a chunk kept in HBM (a device-side chunk_cache.rs)
 //!   rdx_execute_device / _batch_device / _multi_device, rdx_workspace_*
 //!                                     new: device-resident, batched and heterogeneous entry points
 //!   rdx_decompress_batch_device       compression.rs:18-27 `decompress` for a batch of device streams
@@ -154,6 +157,33 @@ pub struct RdxResult {
     pub reserved: u64,
 }
 
+/// `rdx_context_config` (include/rdx.h): pool limits and request coalescing.
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct RdxContextConfig {
+    pub max_workspaces: u32,
+    pub coalesce: u32,
+    pub coalesce_lanes: u32,
+    pub reserved: u32,
+    pub coalesce_max_bytes: u64,
+    pub coalesce_host_max_bytes: u64,
+}
+
+/// `rdx_device_stats` (include/rdx.h): one pool entry's bookkeeping.
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct RdxDeviceStats {
+    pub device: i32,
+    pub workspaces: u32,
+    pub workspaces_busy: u32,
+    pub max_workspaces: u32,
+    pub requests: u64,
+    pub coalesced_requests: u64,
+    pub coalesced_launches: u64,
+    pub outstanding_bytes: u64,
+    pub waits: u64,
+}
+
 pub enum RdxContext {}
 pub enum RdxWorkspace {}
 
@@ -164,6 +194,8 @@ extern "C" {
     pub fn rdx_device_count() -> c_int;
     pub fn rdx_context_create(devices: *const c_int, n_devices: c_int, out: *mut *mut RdxContext) -> c_int;
     pub fn rdx_context_destroy(ctx: *mut RdxContext);
+    pub fn rdx_context_configure(ctx: *mut RdxContext, cfg: *const RdxContextConfig) -> c_int;
+    pub fn rdx_context_stats(ctx: *mut RdxContext, index: u32, out: *mut RdxDeviceStats) -> c_int;
     pub fn rdx_validate_request(req: *const RdxRequest) -> c_int;
     pub fn rdx_plan(req: *const RdxRequest, chunk_len: u64, info: *mut RdxResponseInfo) -> c_int;
     pub fn rdx_missing_from_i64(dtype: u32, v: i64, out: *mut c_void) -> c_int;
@@ -208,6 +240,18 @@ extern "C" {
         out: *mut *mut RdxResult,
     ) -> c_int;
     pub fn rdx_result_free(ctx: *mut RdxContext, result: *mut RdxResult);
+    pub fn rdx_execute_resident(
+        ctx: *mut RdxContext,
+        device: c_int,
+        req: *const RdxRequest,
+        d_chunk: *const c_void,
+        chunk_len: u64,
+        body: *mut c_void,
+        body_capacity: u64,
+        counts: *mut i64,
+        counts_capacity: u64,
+        info: *mut RdxResponseInfo,
+    ) -> c_int;
     pub fn rdx_workspace_create(ctx: *mut RdxContext, device: c_int, out: *mut *mut RdxWorkspace) -> c_int;
     pub fn rdx_workspace_destroy(ws: *mut RdxWorkspace);
     pub fn rdx_execute_device(
@@ -285,6 +329,10 @@ const _: () = assert!(size_of::<RdxRequest>() == 112);
 const _: () = assert!(size_of::<RdxResponseInfo>() == 280);
 const _: () = assert!(size_of::<RdxMultiItem>() == 48);
 const _: () = assert!(size_of::<RdxResult>() == 312);
+const _: () = assert!(size_of::<RdxContextConfig>() == 32);
+const _: () = assert!(size_of::<RdxDeviceStats>() == 56);
+const _: () = assert!(offset_of!(RdxContextConfig, coalesce_max_bytes) == 16);
+const _: () = assert!(offset_of!(RdxDeviceStats, requests) == 16);
 const _: () = assert!(offset_of!(RdxRequest, op) == 4);
 const _: () = assert!(offset_of!(RdxRequest, shape) == 32);
 const _: () = assert!(offset_of!(RdxRequest, selection) == 40);

@@ -6,6 +6,10 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -121,12 +125,54 @@ struct rdx_workspace {
     hipEvent_t piece_ev[8] = {};
 };
 
-struct rdx_context {
-    std::vector<int> devices;
-    std::mutex mu;
-    std::vector<std::vector<rdx_workspace *>> free_ws;  // per device index
+namespace {
+
+// One in-flight k_multi launch of the coalescer: its own workspace (stream, hand-off records) and a
+// result slot per request (device, then page-locked host) filled by one copy per launch.
+constexpr uint64_t kSlotBytes = 32;   // [0, 8) body (value / i64 count), [8, 16) count, [16, 20) status
+struct Lane {
+    rdx_workspace *ws = nullptr;
+    uint8_t *d_res = nullptr;
+    uint8_t *h_res = nullptr;
+    hipEvent_t done = nullptr;
+};
+
+rdx_context_config effective_config(const rdx_context_config &c);
+void destroy_lane(Lane *L);
+
+// A request waiting for (or in) a coalesced launch.
+struct Job {
+    KMultiReq q{};                 // chunk / view / op; outputs are bound to the lane's slots at launch
+    uint64_t body_bytes = 0, n_counts = 0;
+    void *h_body = nullptr;        // host destinations
+    int64_t *h_counts = nullptr;
+    rdx_status st = RDX_OK;
+    bool done = false;
+};
+
+// One entry of the context's device pool.
+struct PoolEntry {
+    int device = 0;
+    std::mutex mu;                               // everything below but `outstanding`
+    std::condition_variable ws_cv;               // a workspace was released
+    std::vector<rdx_workspace *> free_ws;
     std::vector<rdx_workspace *> all_ws;
-    std::atomic<uint64_t> rr{0};
+    uint32_t busy = 0, creating = 0;
+    std::condition_variable job_cv;              // a coalesced launch finished
+    std::deque<Job *> jobs;                      // FIFO of queued requests
+    std::vector<Lane *> idle_lanes, all_lanes;
+    std::atomic<uint64_t> outstanding{0};        // chunk bytes in flight (placement key)
+    uint64_t requests = 0, coalesced = 0, launches = 0, waits = 0;
+};
+
+}  // namespace
+
+struct rdx_context {
+    std::vector<int> devices;                    // per pool entry
+    std::vector<std::unique_ptr<PoolEntry>> entries;
+    rdx_context_config cfg{};
+    std::mutex mu;                               // the pinned response pool
+    std::atomic<uint64_t> rr{0};                 // tie-break start of the placement scan
     // page-locked response buffers of rdx_execute_owned (size class -> free blocks; block -> class)
     std::map<uint64_t, std::vector<void *>> pinned_free;
     std::map<void *, uint64_t> pinned_class;
@@ -859,126 +905,6 @@ rdx_status map_pipelined(rdx_workspace *ws, const ExecPlan &p, const uint8_t *ch
     return RDX_OK;
 }
 
-// rdx_execute_cbor: the response leaves the device as its CBOR body (k_cbor), in a pooled
-// page-locked block.
-struct CborOut {
-    uint32_t flags = 0;
-    void *host = nullptr;   // pool block (rdx_result.body)
-    uint64_t len = 0;       // encoded bytes
-};
-constexpr uint64_t kCborOneTrip = 1ull << 20;   // bounds up to this come back whole, in one round trip
-
-// operation<T>() for a chunk in host memory (app.rs:163-183): plan, bind the response buffers
-// (caller-provided or pooled), H2D, kernels, D2H; blocks until the response is in host memory.
-// With `cb`, the response is serialised on the device (serde_cbor CBORResponse, app.rs:33-40) and only
-// its CBOR body comes back.
-rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t *chunk, uint64_t chunk_len,
-                        const std::function<rdx_status(const rdx_response_info &, void **, int64_t **)> &bind,
-                        rdx_response_info *info, CborOut *cb = nullptr) {
-    const bool compressed = req.compression != RDX_COMPRESSION_NONE;
-    ExecPlan p;
-    rdx_status st;
-    void *body = nullptr;
-    int64_t *counts = nullptr;
-    if (!compressed) {
-        if ((st = make_plan(req, chunk_len, p))) return st;
-        *info = p.info;
-        if ((st = bind(p.info, &body, &counts))) return st;
-    }
-
-    // take a workspace (round-robin device, then any free workspace of it)
-    rdx_workspace *ws = nullptr;
-    size_t di = 0;
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        di = (size_t)(ctx->rr++ % ctx->devices.size());
-        if (!ctx->free_ws[di].empty()) {
-            ws = ctx->free_ws[di].back();
-            ctx->free_ws[di].pop_back();
-        }
-    }
-    if (!ws) {
-        if ((st = create_workspace(ctx->devices[di], &ws))) return st;
-        std::lock_guard<std::mutex> g(ctx->mu);
-        ctx->all_ws.push_back(ws);
-    }
-    auto run = [&]() -> rdx_status {
-        RDX_HIP(hipSetDevice(ws->device));
-        hipStream_t s = ws->own_stream;
-        rdx_status r;
-        if (!cb && !compressed && p.mode == Mode::Map && p.unfused_es.empty() && !p.fused && p.map.view.ndim >= 1 &&
-            p.map.view.count[p.map.view.ndim - 1] >= 2 && chunk_len >= (32ull << 20) && is_pinned(chunk) &&
-            is_pinned(body) && (p.map.kind == 0 || is_pinned(counts))) {
-            if ((r = ensure_aux(ws))) return r;
-            return map_pipelined(ws, p, chunk, chunk_len, static_cast<uint8_t *>(body), counts);
-        }
-        if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
-        if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
-        if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
-        if ((r = ensure(ws, ws->status, 1, s))) return r;
-        if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
-        const uint8_t *src = ws->chunk.p;
-        uint64_t len = chunk_len;
-        if (compressed) {  // the chunk crossed PCIe compressed; inflate it in HBM, then plan on its size
-            uint64_t hint = 0;
-            if (req.compression == RDX_COMPRESSION_GZIP && chunk_len >= 18) {  // RFC 1952 ISIZE
-                const uint8_t *t = chunk + chunk_len - 4;
-                hint = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
-            }
-            if (req.compression == RDX_COMPRESSION_BLOSC2) {  // blosc2_cbuffer_sizes, compression.rs:33
-                uint64_t cb = 0, bs = 0;
-                rdx_blosc2_cbuffer_sizes(chunk, chunk_len, &hint, &cb, &bs);
-            }
-            if ((r = decompress_request(ws, req, ws->chunk.p, chunk_len, hint, s, &len, chunk))) return r;
-            src = ws->raw.p;
-            if ((r = make_plan(req, len, p))) return r;
-            *info = p.info;
-            if ((r = bind(p.info, &body, &counts))) return r;
-            if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
-            if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
-        }
-        RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
-        if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
-            return r;
-        uint32_t status = 0;
-        if (cb) {   // encode on the device; the length (and, for small bounds, the bytes) in one trip
-            const uint64_t bound = rdx_cbor_bound(&p.info, cb->flags);
-            if (!bound) return RDX_E_INVALID_ARGUMENT;
-            if ((r = ensure(ws, ws->cbor, bound, s))) return r;
-            if ((r = ensure(ws, ws->cbor_len, 1, s))) return r;
-            if ((r = pool_alloc(ctx, bound, &cb->host))) return r;
-            if ((r = cbor_device(ws, &p.info, ws->body.p, ws->counts.p, cb->flags, ws->cbor.p, bound, ws->cbor_len.p,
-                                 nullptr, s)))
-                return r;
-            uint64_t n = 0;
-            RDX_HIP(hipMemcpyAsync(&n, ws->cbor_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-            RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            if (bound <= kCborOneTrip) RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, bound, hipMemcpyDeviceToHost, s));
-            RDX_HIP(hipStreamSynchronize(s));
-            if (status) return (rdx_status)status;
-            if (bound > kCborOneTrip) {
-                RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, n, hipMemcpyDeviceToHost, s));
-                RDX_HIP(hipStreamSynchronize(s));
-            }
-            cb->len = n;
-            return RDX_OK;
-        }
-        if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
-        if (p.info.n_counts)
-            RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        RDX_HIP(hipStreamSynchronize(s));
-        if (status) return (rdx_status)status;
-        return RDX_OK;
-    };
-    st = run();
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        ctx->free_ws[di].push_back(ws);
-    }
-    return st;
-}
-
 }  // namespace
 
 // ====================================== C ABI ========================================================
@@ -1075,14 +1001,26 @@ rdx_status rdx_context_create(const int *devices, int n_devices, rdx_context **o
             return RDX_E_NO_DEVICE;
         }
     }
-    ctx->free_ws.resize(ctx->devices.size());
+    ctx->cfg = effective_config(rdx_context_config{0, 1, 0, 0, 0, 0});
+    for (int d : ctx->devices) {
+        auto e = std::unique_ptr<PoolEntry>(new (std::nothrow) PoolEntry());
+        if (!e) {
+            delete ctx;
+            return RDX_E_OUT_OF_MEMORY;
+        }
+        e->device = d;
+        ctx->entries.push_back(std::move(e));
+    }
     *out = ctx;
     return RDX_OK;
 }
 
 void rdx_context_destroy(rdx_context *ctx) {
     if (!ctx) return;
-    for (rdx_workspace *ws : ctx->all_ws) destroy_workspace(ws);
+    for (auto &e : ctx->entries) {
+        for (rdx_workspace *ws : e->all_ws) destroy_workspace(ws);
+        for (Lane *l : e->all_lanes) destroy_lane(l);
+    }
     for (auto &kv : ctx->pinned_free)
         for (void *p : kv.second) (void)hipHostFree(p);
     delete ctx;
@@ -1223,6 +1161,8 @@ rdx_status rdx_execute_batch_device(rdx_workspace *ws, const rdx_request *req, u
                       static_cast<uint8_t *>(d_bodies), d_counts, d_status, static_cast<hipStream_t>(stream));
 }
 
+}  // extern "C"
+
 namespace {
 
 bool fits_i32(int64_t v) { return v >= INT32_MIN && v <= INT32_MAX; }
@@ -1325,6 +1265,377 @@ rdx_status launch_multi_group(rdx_workspace *ws, const KMultiReq *reqs, uint32_t
 }
 
 }  // namespace
+
+namespace {
+
+// ---- the device pool: placement, workspaces with back-pressure, request coalescing ---------------------
+// The server runs every request as its own synchronous operation<T>() call on a worker thread
+// (app.rs:147-152, app_state.rs:21-37); the pool turns those concurrent calls into few, full launches.
+
+rdx_context_config effective_config(const rdx_context_config &c) {
+    rdx_context_config e = c;
+    if (!e.max_workspaces) e.max_workspaces = 16;
+    if (!e.coalesce_lanes) e.coalesce_lanes = 2;
+    if (e.coalesce_lanes > 16) e.coalesce_lanes = 16;
+    if (!e.coalesce_max_bytes) e.coalesce_max_bytes = 64ull << 20;
+    if (!e.coalesce_host_max_bytes) e.coalesce_host_max_bytes = 1ull << 20;
+    return e;
+}
+
+// A request's claim on a pool entry: its weight counts as in flight there until the request returns.
+struct Placement {
+    PoolEntry *e = nullptr;
+    uint64_t weight = 0;
+    Placement() = default;
+    Placement(const Placement &) = delete;
+    ~Placement() {
+        if (e) e->outstanding.fetch_sub(weight, std::memory_order_relaxed);
+    }
+};
+
+// Least outstanding bytes: the entry, among those on `device` (-1: any), with the fewest
+// chunk bytes in flight; the scan starts at a rotating index so that ties spread over the pool.  A
+// request weighs its chunk bytes plus 64 KiB (its fixed cost: launch, hand-off, round trip).
+bool place(rdx_context *ctx, uint64_t bytes, int device, Placement &pl) {
+    const size_t n = ctx->entries.size();
+    const size_t start = (size_t)(ctx->rr.fetch_add(1, std::memory_order_relaxed) % n);
+    size_t best = n;
+    uint64_t best_load = 0;
+    for (size_t k = 0; k < n; ++k) {
+        const size_t i = (start + k) % n;
+        const PoolEntry &e = *ctx->entries[i];
+        if (device >= 0 && e.device != device) continue;
+        const uint64_t load = e.outstanding.load(std::memory_order_relaxed);
+        if (best == n || load < best_load) {
+            best = i;
+            best_load = load;
+        }
+    }
+    if (best == n) return false;
+    pl.e = ctx->entries[best].get();
+    pl.weight = bytes + (64u << 10);
+    pl.e->outstanding.fetch_add(pl.weight, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> g(pl.e->mu);
+    ++pl.e->requests;
+    return true;
+}
+
+// A workspace of the entry for the duration of one request: a free one, a new one below the cap, or —
+// with max_workspaces busy — the next one released (back-pressure, resource_manager.rs:54-89).
+struct WsLease {
+    PoolEntry *e = nullptr;
+    rdx_workspace *ws = nullptr;
+    WsLease() = default;
+    WsLease(const WsLease &) = delete;
+    ~WsLease() {
+        if (!ws) return;
+        {
+            std::lock_guard<std::mutex> g(e->mu);
+            e->free_ws.push_back(ws);
+            --e->busy;
+        }
+        e->ws_cv.notify_one();
+    }
+};
+
+rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease) {
+    std::unique_lock<std::mutex> lk(e.mu);
+    bool waited = false;
+    while (e.free_ws.empty() && e.all_ws.size() + e.creating >= ctx->cfg.max_workspaces) {
+        if (!waited) ++e.waits;
+        waited = true;
+        e.ws_cv.wait(lk);
+    }
+    ++e.busy;
+    if (!e.free_ws.empty()) {
+        lease.ws = e.free_ws.back();
+        e.free_ws.pop_back();
+        lease.e = &e;
+        return RDX_OK;
+    }
+    ++e.creating;   // counts against the cap while it is created outside the lock
+    lk.unlock();
+    rdx_workspace *ws = nullptr;
+    const rdx_status st = create_workspace(e.device, &ws);
+    lk.lock();
+    --e.creating;
+    if (st) {
+        --e.busy;
+        lk.unlock();
+        e.ws_cv.notify_one();
+        return st;
+    }
+    e.all_ws.push_back(ws);
+    lease.ws = ws;
+    lease.e = &e;
+    return RDX_OK;
+}
+
+void destroy_lane(Lane *L) {
+    if (!L) return;
+    if (L->ws) destroy_workspace(L->ws);   // synchronises its stream first
+    if (L->d_res) (void)hipFree(L->d_res);
+    if (L->h_res) (void)hipHostFree(L->h_res);
+    if (L->done) (void)hipEventDestroy(L->done);
+    delete L;
+}
+
+rdx_status create_lane(int device, Lane **out) {
+    auto *L = new (std::nothrow) Lane();
+    if (!L) return RDX_E_OUT_OF_MEMORY;
+    rdx_status st = create_workspace(device, &L->ws);
+    if (!st) {
+        hipError_t e = hipMalloc((void **)&L->d_res, kMultiMaxItems * kSlotBytes);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&L->h_res, kMultiMaxItems * kSlotBytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&L->done, hipEventDisableTiming);
+        st = map_err(e);
+    }
+    if (st) {
+        destroy_lane(L);
+        return st;
+    }
+    *out = L;
+    return RDX_OK;
+}
+
+// Completion of a launch the caller needs before it can answer: poll the event (a blocking
+// synchronisation sleeps on an interrupt and wakes tens of microseconds late; only lane holders poll).
+rdx_status wait_done(hipEvent_t ev) {
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return RDX_OK;
+        if (e != hipErrorNotReady) return map_err(e);
+        std::this_thread::yield();
+    }
+}
+
+// One coalesced launch: the queued requests' descriptors with their outputs bound to the lane's result
+// slots, one k_multi launch, one copy of the slots to page-locked memory, then each request's result into
+// its caller's buffers.
+rdx_status run_lane(Lane &L, Job *const *batch, uint32_t n) {
+    rdx_workspace *ws = L.ws;
+    RDX_HIP(hipSetDevice(ws->device));
+    const hipStream_t s = ws->own_stream;
+    KMultiReq g[kMultiMaxItems];
+    for (uint32_t i = 0; i < n; ++i) {
+        g[i] = batch[i]->q;
+        uint8_t *slot = L.d_res + (uint64_t)i * kSlotBytes;
+        g[i].body = slot;
+        g[i].counts = reinterpret_cast<int64_t *>(slot + 8);
+        g[i].status = reinterpret_cast<uint32_t *>(slot + 16);
+    }
+    rdx_status st;
+    if ((st = launch_multi_group(ws, g, n, s))) return st;
+    RDX_HIP(hipMemcpyAsync(L.h_res, L.d_res, (uint64_t)n * kSlotBytes, hipMemcpyDeviceToHost, s));
+    RDX_HIP(hipEventRecord(L.done, s));
+    if ((st = wait_done(L.done))) return st;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *slot = L.h_res + (uint64_t)i * kSlotBytes;
+        Job &j = *batch[i];
+        uint32_t status = 0;
+        std::memcpy(&status, slot + 16, sizeof status);
+        j.st = (rdx_status)status;
+        if (j.body_bytes) std::memcpy(j.h_body, slot, j.body_bytes);
+        if (j.n_counts) std::memcpy(j.h_counts, slot + 8, sizeof(int64_t));
+    }
+    return RDX_OK;
+}
+
+// Queue the request on its entry and wait for its result.  Whoever finds a lane free (an idle one, or a
+// new one below coalesce_lanes) takes everything queued (up to kMultiMaxItems, oldest first) into one
+// launch — its own request among them or not — and loops until its own request is done.  Under load the
+// queue grows while the lanes are busy, so launches fill up by themselves; alone, a request launches at
+// once.
+rdx_status coalesce(rdx_context *ctx, PoolEntry &e, Job &job) {
+    std::unique_lock<std::mutex> lk(e.mu);
+    e.jobs.push_back(&job);
+    ++e.coalesced;
+    while (!job.done) {
+        Lane *lane = nullptr;
+        if (!e.jobs.empty()) {
+            if (!e.idle_lanes.empty()) {
+                lane = e.idle_lanes.back();
+                e.idle_lanes.pop_back();
+            } else if (e.all_lanes.size() < ctx->cfg.coalesce_lanes) {
+                const rdx_status st = create_lane(e.device, &lane);   // under the lock: once per lane
+                if (st) {
+                    lane = nullptr;
+                    if (e.all_lanes.empty()) {   // nothing can serve the queue: fail it
+                        for (Job *j : e.jobs) {
+                            j->st = st;
+                            j->done = true;
+                        }
+                        e.jobs.clear();
+                        e.job_cv.notify_all();
+                        break;
+                    }
+                } else {
+                    e.all_lanes.push_back(lane);
+                }
+            }
+        }
+        if (!lane) {
+            e.job_cv.wait(lk);
+            continue;
+        }
+        Job *batch[kMultiMaxItems];
+        uint32_t n = 0;
+        while (n < (uint32_t)kMultiMaxItems && !e.jobs.empty()) {
+            batch[n++] = e.jobs.front();
+            e.jobs.pop_front();
+        }
+        ++e.launches;
+        lk.unlock();
+        const rdx_status st = run_lane(*lane, batch, n);
+        lk.lock();
+        for (uint32_t i = 0; i < n; ++i) {
+            if (st) batch[i]->st = st;
+            batch[i]->done = true;
+        }
+        e.idle_lanes.push_back(lane);
+        e.job_cv.notify_all();
+    }
+    return job.st;
+}
+
+// rdx_execute_cbor: the response leaves the device as its CBOR body (k_cbor), in a pooled
+// page-locked block.
+struct CborOut {
+    uint32_t flags = 0;
+    void *host = nullptr;   // pool block (rdx_result.body)
+    uint64_t len = 0;       // encoded bytes
+};
+constexpr uint64_t kCborOneTrip = 1ull << 20;   // bounds up to this come back whole, in one round trip
+
+// operation<T>() for a chunk in host memory (app.rs:163-183): plan, bind the response buffers
+// (caller-provided or pooled), H2D, kernels, D2H; blocks until the response is in host memory.
+// With `cb`, the response is serialised on the device (serde_cbor CBORResponse, app.rs:33-40) and only
+// its CBOR body comes back.
+// `resident_device` >= 0: the chunk is in HBM of that device (rdx_execute_resident), nothing crosses PCIe
+// but the response.
+rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t *chunk, uint64_t chunk_len,
+                        const std::function<rdx_status(const rdx_response_info &, void **, int64_t **)> &bind,
+                        rdx_response_info *info, CborOut *cb = nullptr, int resident_device = -1) {
+    const bool resident = resident_device >= 0;
+    const bool compressed = req.compression != RDX_COMPRESSION_NONE;
+    ExecPlan p;
+    rdx_status st;
+    void *body = nullptr;
+    int64_t *counts = nullptr;
+    if (!compressed) {
+        if ((st = make_plan(req, chunk_len, p))) return st;
+        *info = p.info;
+        if ((st = bind(p.info, &body, &counts))) return st;
+    }
+
+    Placement pl;
+    if (!place(ctx, chunk_len, resident_device, pl)) return resident ? RDX_E_INVALID_ARGUMENT : RDX_E_NO_DEVICE;
+    PoolEntry &entry = *pl.e;
+    // a small all-axes request joins the entry's coalesced k_multi launches (chunk at d_base in HBM)
+    auto coalescible = [&](const uint8_t *d_base, Job &job) -> bool {
+        if (compressed || cb || !ctx->cfg.coalesce) return false;
+        if (chunk_len > (resident ? ctx->cfg.coalesce_max_bytes : ctx->cfg.coalesce_host_max_bytes)) return false;
+        rdx_multi_item it{};
+        it.req = &req;
+        it.d_chunk = d_base;
+        it.chunk_len = chunk_len;
+        if (!multi_req(p, it, job.q)) return false;
+        job.body_bytes = p.info.body_bytes;
+        job.n_counts = p.info.n_counts;
+        job.h_body = body;
+        job.h_counts = counts;
+        return true;
+    };
+    if (resident) {
+        Job job;
+        if (coalescible(chunk, job)) return coalesce(ctx, entry, job);
+    }
+    WsLease lease;
+    if ((st = acquire_ws(ctx, entry, lease))) return st;
+    rdx_workspace *ws = lease.ws;
+    auto run = [&]() -> rdx_status {
+        RDX_HIP(hipSetDevice(ws->device));
+        hipStream_t s = ws->own_stream;
+        rdx_status r;
+        if (!resident && !cb && !compressed && p.mode == Mode::Map && p.unfused_es.empty() && !p.fused && p.map.view.ndim >= 1 &&
+            p.map.view.count[p.map.view.ndim - 1] >= 2 && chunk_len >= (32ull << 20) && is_pinned(chunk) &&
+            is_pinned(body) && (p.map.kind == 0 || is_pinned(counts))) {
+            if ((r = ensure_aux(ws))) return r;
+            return map_pipelined(ws, p, chunk, chunk_len, static_cast<uint8_t *>(body), counts);
+        }
+        const uint8_t *src = chunk;
+        if (!resident) {
+            if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
+            if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
+            src = ws->chunk.p;
+            Job job;
+            if (coalescible(src, job)) {   // the chunk is in HBM once the copy completes
+                RDX_HIP(hipStreamSynchronize(s));
+                return coalesce(ctx, entry, job);
+            }
+        }
+        if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
+        if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
+        if ((r = ensure(ws, ws->status, 1, s))) return r;
+        uint64_t len = chunk_len;
+        if (compressed) {  // the chunk crossed PCIe compressed; inflate it in HBM, then plan on its size
+            uint64_t hint = 0;
+            if (!resident && req.compression == RDX_COMPRESSION_GZIP && chunk_len >= 18) {  // RFC 1952 ISIZE
+                const uint8_t *t = chunk + chunk_len - 4;
+                hint = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+            }
+            if (!resident && req.compression == RDX_COMPRESSION_BLOSC2) {  // blosc2_cbuffer_sizes, compression.rs:33
+                uint64_t cb = 0, bs = 0;
+                rdx_blosc2_cbuffer_sizes(chunk, chunk_len, &hint, &cb, &bs);
+            }
+            if ((r = decompress_request(ws, req, src, chunk_len, hint, s, &len, resident ? nullptr : chunk))) return r;
+            src = ws->raw.p;
+            if ((r = make_plan(req, len, p))) return r;
+            *info = p.info;
+            if ((r = bind(p.info, &body, &counts))) return r;
+            if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
+            if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
+        }
+        RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
+        if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
+            return r;
+        uint32_t status = 0;
+        if (cb) {   // encode on the device; the length (and, for small bounds, the bytes) in one trip
+            const uint64_t bound = rdx_cbor_bound(&p.info, cb->flags);
+            if (!bound) return RDX_E_INVALID_ARGUMENT;
+            if ((r = ensure(ws, ws->cbor, bound, s))) return r;
+            if ((r = ensure(ws, ws->cbor_len, 1, s))) return r;
+            if ((r = pool_alloc(ctx, bound, &cb->host))) return r;
+            if ((r = cbor_device(ws, &p.info, ws->body.p, ws->counts.p, cb->flags, ws->cbor.p, bound, ws->cbor_len.p,
+                                 nullptr, s)))
+                return r;
+            uint64_t n = 0;
+            RDX_HIP(hipMemcpyAsync(&n, ws->cbor_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            if (bound <= kCborOneTrip) RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, bound, hipMemcpyDeviceToHost, s));
+            RDX_HIP(hipStreamSynchronize(s));
+            if (status) return (rdx_status)status;
+            if (bound > kCborOneTrip) {
+                RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, n, hipMemcpyDeviceToHost, s));
+                RDX_HIP(hipStreamSynchronize(s));
+            }
+            cb->len = n;
+            return RDX_OK;
+        }
+        if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
+        if (p.info.n_counts)
+            RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipStreamSynchronize(s));
+        if (status) return (rdx_status)status;
+        return RDX_OK;
+    };
+    return run();
+}
+
+}  // namespace
+
+extern "C" {
 
 rdx_status rdx_execute_multi_device(rdx_workspace *ws, uint64_t n, const rdx_multi_item *items, void *stream,
                                     uint32_t *statuses, rdx_response_info *infos) {
@@ -1467,6 +1778,43 @@ void rdx_result_free(rdx_context *ctx, rdx_result *r) {
     if (!r) return;
     if (r->body) pool_free(ctx, r->body);
     delete r;
+}
+
+rdx_status rdx_execute_resident(rdx_context *ctx, int device, const rdx_request *req, const void *d_chunk,
+                                uint64_t chunk_len, void *body, uint64_t body_capacity, int64_t *counts,
+                                uint64_t counts_capacity, rdx_response_info *info) {
+    if (!ctx || !req || !info || device < 0 || (!d_chunk && chunk_len)) return RDX_E_INVALID_ARGUMENT;
+    auto bind = [&](const rdx_response_info &inf, void **b, int64_t **c) -> rdx_status {
+        if (body_capacity < inf.body_bytes || counts_capacity < inf.n_counts) return RDX_E_BUFFER_TOO_SMALL;
+        if ((!body && inf.body_bytes) || (!counts && inf.n_counts)) return RDX_E_INVALID_ARGUMENT;
+        *b = body;
+        *c = counts;
+        return RDX_OK;
+    };
+    return execute_host(ctx, *req, static_cast<const uint8_t *>(d_chunk), chunk_len, bind, info, nullptr, device);
+}
+
+rdx_status rdx_context_configure(rdx_context *ctx, const rdx_context_config *cfg) {
+    if (!ctx || !cfg || cfg->coalesce > 1) return RDX_E_INVALID_ARGUMENT;
+    ctx->cfg = effective_config(*cfg);
+    return RDX_OK;
+}
+
+rdx_status rdx_context_stats(rdx_context *ctx, uint32_t index, rdx_device_stats *out) {
+    if (!ctx || !out || index >= ctx->entries.size()) return RDX_E_INVALID_ARGUMENT;
+    PoolEntry &e = *ctx->entries[index];
+    std::lock_guard<std::mutex> g(e.mu);
+    *out = rdx_device_stats{};
+    out->device = e.device;
+    out->workspaces = (uint32_t)e.all_ws.size();
+    out->workspaces_busy = e.busy;
+    out->max_workspaces = ctx->cfg.max_workspaces;
+    out->requests = e.requests;
+    out->coalesced_requests = e.coalesced;
+    out->coalesced_launches = e.launches;
+    out->outstanding_bytes = e.outstanding.load(std::memory_order_relaxed);
+    out->waits = e.waits;
+    return RDX_OK;
 }
 
 }  // extern "C"

@@ -1,12 +1,17 @@
 // Concurrent single-chunk requests from native threads (no Python, no GIL): the way the Rust server
-// issues them — every Tokio / Rayon worker runs one request at a time to completion (src/app.rs:147-152,
-// thread_limit = num_cpus - 1, src/app_state.rs:22).  T threads, each with its own rdx_workspace and HIP
-// stream, each request = rdx_execute_device on an HBM-resident chunk + a stream synchronize (the result
-// is needed before the HTTP response); chunks rotate over buffers larger than the Infinity Cache.
-// Also the host path: rdx_execute from page-locked chunks (PCIe-bound).
+// issues them — one process (app_state.rs:21-37), every Tokio / Rayon worker running one request at a time
+// to completion (src/app.rs:147-152, thread_limit = num_cpus - 1, src/app_state.rs:22).
 //
-//   rdx_conc_bench <config c1|c3|c2> <threads> <requests per thread> [device|host]
-// prints one JSON line: requests/s, GB/s of selected bytes, us per request per thread.
+//   rdx_conc_bench <config c1|c2|c3|c4> <threads> <requests per thread> [path] [devices] [lanes]
+//     path    device:   each thread its own rdx_workspace + stream, rdx_execute_device on an HBM-resident
+//                       chunk + a stream synchronize (independent launches; round-2 form)
+//             resident: rdx_execute_resident on an HBM-resident chunk, response into host memory; small
+//                       all-axes requests coalesce into shared k_multi launches (the context's pool)
+//             host:     rdx_execute from page-locked host chunks (PCIe-bound)
+//     devices comma-separated HIP ordinals of ONE context (default 0): the in-process multi-GPU server;
+//             host / resident requests are placed by the pool (least outstanding bytes)
+//     lanes   coalescer launches in flight per device (default: the engine's)
+// Chunks rotate over buffers larger than the Infinity Cache (per device).  Prints one JSON line.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,8 +19,10 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -58,6 +65,12 @@ static Config make_config(const std::string &n) {
         c.filters = {{RDX_FILTER_SHUFFLE, 0, 4}};
         c.bytes = 64u << 20;
         c.alg_bytes = c.bytes;
+    } else if (n == "c4") {  // configs[3]'s chunk: f32 4 MiB, shuffle es=4, native order, sum
+        c.op = RDX_OP_SUM;
+        c.dtype = RDX_DTYPE_FLOAT32;
+        c.filters = {{RDX_FILTER_SHUFFLE, 0, 4}};
+        c.bytes = 4u << 20;
+        c.alg_bytes = c.bytes;
     } else {                 // configs[2]: f64 [128,128,128] hyperslab, missing_value -9999, min
         c.op = RDX_OP_MIN;
         c.dtype = RDX_DTYPE_FLOAT64;
@@ -73,17 +86,32 @@ static Config make_config(const std::string &n) {
 
 int main(int argc, char **argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s c1|c2|c3 threads requests_per_thread [device|host]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s c1|c2|c3|c4 threads requests_per_thread [device|resident|host] [devs] [lanes]\n",
+                     argv[0]);
         return 1;
     }
     const Config cfg = make_config(argv[1]);
     const int T = std::max(1, std::atoi(argv[2]));
     const int R = std::max(1, std::atoi(argv[3]));
-    const bool host = argc > 4 && std::string(argv[4]) == "host";
+    const std::string path = argc > 4 ? argv[4] : "device";
+    const bool host = path == "host", resident = path == "resident";
+    std::vector<int> devs;
+    {
+        std::stringstream ss(argc > 5 ? argv[5] : "0");
+        std::string tok;
+        while (std::getline(ss, tok, ',')) devs.push_back(std::atoi(tok.c_str()));
+    }
+    const int D = (int)devs.size();
     rdx_context *ctx = nullptr;
-    if (rdx_context_create(nullptr, 0, &ctx) != RDX_OK) {
+    if (rdx_context_create(devs.data(), D, &ctx) != RDX_OK) {
         std::fprintf(stderr, "no device\n");
         return 2;
+    }
+    if (argc > 6) {
+        rdx_context_config cc{};
+        cc.coalesce = 1;
+        cc.coalesce_lanes = (uint32_t)std::atoi(argv[6]);
+        if (rdx_context_configure(ctx, &cc) != RDX_OK) return 2;
     }
     // request
     double mv = cfg.miss_value;
@@ -121,43 +149,52 @@ int main(int argc, char **argv) {
             std::memcpy(hostdata.data() + 4 * i, &x, 4);
         }
     }
-    // rotating chunk buffers: > 256 MiB in total
+    // rotating chunk buffers: > 256 MiB in total per device (host: one shared set of page-locked chunks)
     const int nbuf = (int)std::max<uint64_t>(4, (512ull << 20) / cfg.bytes);
-    std::vector<void *> bufs(nbuf);
-    for (auto &b : bufs) {
-        if (host) {
-            if (rdx_host_alloc(ctx, cfg.bytes, &b) != RDX_OK) return 2;
-            std::memcpy(b, hostdata.data(), cfg.bytes);
-        } else {
-            CHECK_HIP(hipMalloc(&b, cfg.bytes));
-            CHECK_HIP(hipMemcpy(b, hostdata.data(), cfg.bytes, hipMemcpyHostToDevice));
+    std::vector<std::vector<void *>> bufs(host ? 1 : D, std::vector<void *>(nbuf));
+    for (size_t d = 0; d < bufs.size(); ++d) {
+        for (auto &b : bufs[d]) {
+            if (host) {
+                if (rdx_host_alloc(ctx, cfg.bytes, &b) != RDX_OK) return 2;
+                std::memcpy(b, hostdata.data(), cfg.bytes);
+            } else {
+                CHECK_HIP(hipSetDevice(devs[d]));
+                CHECK_HIP(hipMalloc(&b, cfg.bytes));
+                CHECK_HIP(hipMemcpy(b, hostdata.data(), cfg.bytes, hipMemcpyHostToDevice));
+            }
         }
     }
     std::atomic<int> errors{0}, ready{0};
     std::atomic<bool> go{false};
     std::vector<double> per_thread_us(T);
-    // each thread: its workspace, stream and output buffers (set up before the clock starts), a warm-up
-    // request, then R timed requests once every thread is ready
+    // each thread: (device path) its workspace, stream and output buffers, set up before the clock starts;
+    // a warm-up request, then R timed requests once every thread is ready
     auto worker = [&](int t) {
         rdx_workspace *ws = nullptr;
         hipStream_t s = nullptr;
         void *d_body = nullptr, *d_counts = nullptr, *d_status = nullptr;
         std::vector<uint8_t> body(std::max<uint64_t>(info.body_bytes, 16));
         std::vector<int64_t> counts(std::max<uint64_t>(info.n_counts, 1));
+        const int my_dev = t % D;
         bool ok = true;
-        if (!host)
-            ok = rdx_workspace_create(ctx, 0, &ws) == RDX_OK && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
-                 hipMalloc(&d_body, 64) == hipSuccess && hipMalloc(&d_counts, 64) == hipSuccess &&
-                 hipMalloc(&d_status, 64) == hipSuccess;
+        if (path == "device")
+            ok = hipSetDevice(devs[my_dev]) == hipSuccess && rdx_workspace_create(ctx, devs[my_dev], &ws) == RDX_OK &&
+                 hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess && hipMalloc(&d_body, 64) == hipSuccess &&
+                 hipMalloc(&d_counts, 64) == hipSuccess && hipMalloc(&d_status, 64) == hipSuccess;
         auto one = [&](int i) {
-            void *chunk = bufs[(i * T + t) % nbuf];
+            const int k = (i * T + t) % nbuf;
             rdx_response_info out{};
             rdx_status st;
             if (host) {
-                st = rdx_execute(ctx, &req, chunk, cfg.bytes, body.data(), body.size(), counts.data(), counts.size(), &out);
+                st = rdx_execute(ctx, &req, bufs[0][k], cfg.bytes, body.data(), body.size(), counts.data(), counts.size(),
+                                 &out);
+            } else if (resident) {
+                const int d = (i * T + t) % D;   // requests spread over the devices holding their chunks
+                st = rdx_execute_resident(ctx, devs[d], &req, bufs[d][k], cfg.bytes, body.data(), body.size(),
+                                          counts.data(), counts.size(), &out);
             } else {
-                st = rdx_execute_device(ws, &req, chunk, cfg.bytes, d_body, (int64_t *)d_counts, (uint32_t *)d_status,
-                                        s, &out);
+                st = rdx_execute_device(ws, &req, bufs[my_dev][k], cfg.bytes, d_body, (int64_t *)d_counts,
+                                        (uint32_t *)d_status, s, &out);
                 if (st == RDX_OK && hipStreamSynchronize(s) != hipSuccess) st = RDX_E_DEVICE;
             }
             if (st != RDX_OK) ++errors;
@@ -170,7 +207,7 @@ int main(int argc, char **argv) {
         if (ok)
             for (int i = 0; i < R; ++i) one(i);
         per_thread_us[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
-        if (!host) {
+        if (path == "device") {
             (void)hipFree(d_body);
             (void)hipFree(d_counts);
             (void)hipFree(d_status);
@@ -181,9 +218,7 @@ int main(int argc, char **argv) {
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) th.emplace_back(worker, t);
     while (ready.load() < T) std::this_thread::yield();
-    const auto t0 = std::chrono::steady_clock::now();
     go.store(true, std::memory_order_release);
-    (void)t0;
     for (auto &x : th) x.join();
     // the timed region: from the start signal to the last thread's last completed request (teardown excluded)
     double el = 0;
@@ -191,16 +226,34 @@ int main(int argc, char **argv) {
     const double reqs = (double)T * R;
     double lat = 0;
     for (double v : per_thread_us) lat += v / T;
-    std::printf("{\"config\": \"%s\", \"path\": \"%s\", \"threads\": %d, \"requests\": %.0f, \"requests_per_s\": %.1f, "
-                "\"us_per_request_aggregate\": %.3f, \"us_per_request_per_thread\": %.3f, \"GBs_alg\": %.1f, "
-                "\"GiBs_chunk\": %.1f, \"roofline_frac\": %.4f, \"errors\": %d}\n",
-                cfg.name.c_str(), host ? "rdx_execute (page-locked host chunk)" : "rdx_execute_device + synchronize",
-                T, reqs, reqs / el, el / reqs * 1e6, lat, reqs * cfg.alg_bytes / el / 1e9,
-                reqs * cfg.bytes / el / (1024.0 * 1024 * 1024), reqs * cfg.alg_bytes / el / 1e9 / 8000.0, errors.load());
-    for (auto &b : bufs) {
-        if (host) rdx_host_free(ctx, b);
-        else (void)hipFree(b);
+    uint64_t creq = 0, claunch = 0, waits = 0, wsn = 0;
+    std::string per_dev;
+    for (int d = 0; d < D; ++d) {
+        rdx_device_stats st{};
+        if (rdx_context_stats(ctx, (uint32_t)d, &st) == RDX_OK) {
+            creq += st.coalesced_requests;
+            claunch += st.coalesced_launches;
+            waits += st.waits;
+            wsn += st.workspaces;
+            per_dev += (d ? "," : "") + std::to_string(st.requests);
+        }
     }
+    const char *pname = host ? "rdx_execute (page-locked host chunk)"
+                        : resident ? "rdx_execute_resident (coalesced)" : "rdx_execute_device + synchronize";
+    std::printf("{\"config\": \"%s\", \"path\": \"%s\", \"devices\": %d, \"threads\": %d, \"requests\": %.0f, "
+                "\"requests_per_s\": %.1f, \"us_per_request_aggregate\": %.3f, \"us_per_request_per_thread\": %.3f, "
+                "\"GBs_alg\": %.1f, \"GiBs_chunk\": %.1f, \"roofline_frac\": %.4f, \"coalesced_requests\": %llu, "
+                "\"coalesced_launches\": %llu, \"workspaces\": %llu, \"waits\": %llu, \"requests_per_device\": [%s], "
+                "\"errors\": %d}\n",
+                cfg.name.c_str(), pname, D, T, reqs, reqs / el, el / reqs * 1e6, lat, reqs * cfg.alg_bytes / el / 1e9,
+                reqs * cfg.bytes / el / (1024.0 * 1024 * 1024), reqs * cfg.alg_bytes / el / 1e9 / (8000.0 * D),
+                (unsigned long long)creq, (unsigned long long)claunch, (unsigned long long)wsn,
+                (unsigned long long)waits, per_dev.c_str(), errors.load());
+    for (size_t d = 0; d < bufs.size(); ++d)
+        for (auto &b : bufs[d]) {
+            if (host) rdx_host_free(ctx, b);
+            else (void)hipFree(b);
+        }
     rdx_context_destroy(ctx);
     return errors ? 4 : 0;
 }

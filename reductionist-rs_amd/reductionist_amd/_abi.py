@@ -91,6 +91,21 @@ class rdx_result(C.Structure):
                 ("cbor_bytes", C.c_uint64), ("reserved", C.c_uint64)]
 
 
+class rdx_context_config(C.Structure):
+    _fields_ = [("max_workspaces", C.c_uint32), ("coalesce", C.c_uint32), ("coalesce_lanes", C.c_uint32),
+                ("reserved", C.c_uint32), ("coalesce_max_bytes", C.c_uint64),
+                ("coalesce_host_max_bytes", C.c_uint64)]
+
+
+class rdx_device_stats(C.Structure):
+    _fields_ = [("device", C.c_int32), ("workspaces", C.c_uint32), ("workspaces_busy", C.c_uint32),
+                ("max_workspaces", C.c_uint32), ("requests", C.c_uint64), ("coalesced_requests", C.c_uint64),
+                ("coalesced_launches", C.c_uint64), ("outstanding_bytes", C.c_uint64), ("waits", C.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 class CRequest:
     """Owns the ctypes arrays an rdx_request points into (keep it alive during the call)."""
 
@@ -178,6 +193,9 @@ def _declare(lib):
         "rdx_cbor_bound": (U64, [P(rdx_response_info), C.c_uint32]),
         "rdx_cbor_encode": (C.c_int, [P(rdx_response_info), VP, VP, C.c_uint32, VP, U64, P(U64)]),
         "rdx_cbor_encode_device": (C.c_int, [VP, P(rdx_response_info), VP, VP, C.c_uint32, VP, U64, VP, VP, VP]),
+        "rdx_context_configure": (C.c_int, [VP, P(rdx_context_config)]),
+        "rdx_context_stats": (C.c_int, [VP, C.c_uint32, P(rdx_device_stats)]),
+        "rdx_execute_resident": (C.c_int, [VP, C.c_int, req_p, VP, U64, VP, U64, P(C.c_int64), U64, info_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -194,7 +212,8 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_workspace_destroy", "rdx_execute_device", "rdx_execute_batch_device", "rdx_inflate_error_string",
             "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
             "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device",
-            "rdx_execute_cbor", "rdx_blosc2_cbuffer_sizes", "rdx_last_unsupported_reason"]
+            "rdx_execute_cbor", "rdx_blosc2_cbuffer_sizes", "rdx_last_unsupported_reason",
+            "rdx_context_configure", "rdx_context_stats", "rdx_execute_resident"]
 
 
 def lib():

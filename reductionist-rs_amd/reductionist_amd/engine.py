@@ -92,6 +92,33 @@ class Engine:
         self.lib.rdx_result_free(self.ctx, res)
         return st, info, body
 
+    def execute_resident(self, creq: _abi.CRequest, device: int, d_chunk: int, chunk_len: int):
+        """rdx_execute_resident: a chunk already in HBM of `device`, the response into host buffers (small
+        all-axes requests coalesce with concurrent callers').  Returns (status, info, body, counts); the
+        ctypes call releases the GIL, so Python threads issue concurrent requests."""
+        info = _abi.rdx_response_info()
+        st = self.lib.rdx_plan(creq.ref, chunk_len, C.byref(info))
+        if st != _abi.OK:
+            return st, info, b"", []
+        body = (C.c_uint8 * max(1, info.body_bytes))()
+        counts = (C.c_int64 * max(1, info.n_counts))()
+        st = self.lib.rdx_execute_resident(self.ctx, device, creq.ref, C.c_void_p(d_chunk), chunk_len, body,
+                                           info.body_bytes, counts, info.n_counts, C.byref(info))
+        return st, info, bytes(body)[: info.body_bytes], [int(c) for c in counts[: info.n_counts]]
+
+    def configure(self, max_workspaces=0, coalesce=True, coalesce_lanes=0, coalesce_max_bytes=0,
+                  coalesce_host_max_bytes=0):
+        """rdx_context_configure (0 = the engine's default for that field)."""
+        cfg = _abi.rdx_context_config(max_workspaces, 1 if coalesce else 0, coalesce_lanes, 0, coalesce_max_bytes,
+                                      coalesce_host_max_bytes)
+        check(self.lib.rdx_context_configure(self.ctx, C.byref(cfg)))
+
+    def stats(self, index: int = 0) -> dict:
+        """rdx_context_stats of pool entry `index`."""
+        st = _abi.rdx_device_stats()
+        check(self.lib.rdx_context_stats(self.ctx, index, C.byref(st)))
+        return st.as_dict()
+
     def host_alloc(self, nbytes: int):
         """Page-locked host buffer (rdx_host_alloc) as (pointer, numpy uint8 view); free with host_free."""
         import numpy as np

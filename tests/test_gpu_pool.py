@@ -1,0 +1,222 @@
+"""The context's device pool (include/rdx.h rdx_context): concurrent callers, the way the server issues
+requests — every request its own synchronous operation<T>() call on a worker thread (app.rs:147-152,
+app_state.rs:21-37).  Through the C ABI from Python threads (ctypes releases the GIL):
+
+* rdx_execute_resident (chunks already in HBM) and rdx_execute (host chunks) from many threads: small
+  all-axes requests coalesce into shared k_multi launches; every response bit-exact vs the oracle;
+* placement over a pool listing one GPU twice (rdx_context_create([0, 0])): both entries serve, each with
+  its own workspaces; least outstanding bytes;
+* back-pressure: max_workspaces = 1 with many threads — all requests served by one workspace;
+* a NaN min inside a coalesced launch fails only its own request."""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import encode_filters, make_request, random_case
+from oracle import py_oracle as oracle
+from reductionist_amd import Engine, _abi
+from test_gpu_parity import same_result
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+def _cases(seed, n, allaxes_only=False, max_dim=24):
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        op, req, raw = random_case(rng, allow_nan=True, max_dim=max_dim, max_ndim=4)
+        if allaxes_only:
+            req.pop("axis", None)
+            req.pop("filters", None)
+            if op == "select":
+                op = "sum"
+        data = encode_filters(raw, req.get("filters"), oracle.shuffle)
+        try:
+            creq = make_request(op, req, oracle.convert)
+        except ValueError:
+            continue
+        out.append((op, req, data, creq, oracle.execute(creq, data)))
+    return out
+
+
+def _plannable(cases):
+    """Requests that reach the pool: the Python wrappers plan first (rdx_plan, host only)."""
+    import ctypes as C
+    info = _abi.rdx_response_info()
+    return sum(_abi.lib().rdx_plan(c[3].ref, len(c[2]), C.byref(info)) == 0 for c in cases)
+
+
+def _check_one(case, st, info, body, counts):
+    op, req, _, _, (ost, oinfo, obody, ocounts) = case
+    assert st == ost, (op, req, st, ost)
+    if ost:
+        return
+    assert info.shape_list() == oinfo.shape_list() and counts == ocounts, (op, req)
+    assert same_result(_abi.DTYPE_NAMES[info.dtype], body, obody), (op, req, body.hex(), obody.hex())
+
+
+def _threaded(n_threads, cases, fn):
+    """Run fn(case) for every case from n_threads threads (case i on thread i % n_threads, started together);
+    returns the results in case order."""
+    results = [None] * len(cases)
+    errors = []
+    go = threading.Barrier(n_threads)
+
+    def worker(t):
+        try:
+            go.wait()
+            for i in range(t, len(cases), n_threads):
+                results[i] = fn(cases[i])
+        except BaseException as e:   # noqa: BLE001 - re-raised in the main thread
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    if errors:
+        raise errors[0]
+    return results
+
+
+def _to_device(torch, cases):
+    bufs = []
+    for case in cases:
+        data = case[2]
+        buf = torch.zeros(max(16, len(data)), dtype=torch.uint8)
+        if data:
+            buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        bufs.append(buf.cuda())
+    torch.cuda.synchronize()
+    return bufs
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_resident_threads_coalesce_bit_exact(torch, lanes):
+    eng = Engine([0])
+    eng.configure(coalesce_lanes=lanes)
+    cases = _cases(7100 + lanes, 400)
+    bufs = _to_device(torch, cases)
+    idx = {id(c): i for i, c in enumerate(cases)}
+    res = _threaded(8, cases, lambda c: eng.execute_resident(c[3], 0, bufs[idx[id(c)]].data_ptr(), len(c[2])))
+    for case, r in zip(cases, res):
+        _check_one(case, *r)
+    s = eng.stats(0)
+    assert s["requests"] == _plannable(cases) and s["outstanding_bytes"] == 0 and s["workspaces_busy"] == 0
+    assert 0 < s["coalesced_requests"] < s["requests"]        # all-axes ones only (axis / select run alone)
+    assert 0 < s["coalesced_launches"] <= s["coalesced_requests"]
+    eng.close()
+
+
+def test_resident_large_allaxes_and_c_shapes(torch):
+    """Multi-workgroup requests per coalesced launch: C1-shaped f32 sums (D-int) and C3-shaped f64 min / max
+    (missing_value -9999) from 6 threads, each bit-exact; and with coalescing off, the same answers."""
+    cases = []
+    for i in range(12):
+        v1 = np.random.default_rng(0x5EED0001 + 16 * i).integers(-8, 9, 1 << 20).astype(np.float32)
+        creq = _abi.CRequest("sum", "float32")
+        cases.append(("sum", {}, v1.tobytes(), creq, oracle.execute(creq, v1.tobytes())))
+        rng = np.random.default_rng(0x5EED0005 + 16 * i)
+        v3 = rng.standard_normal(128 ** 3) * 100
+        v3[rng.random(v3.size) < 0.05] = -9999.0
+        req = {"dtype": "float64", "shape": [128, 128, 128], "selection": [[8, 120, 1], [0, 128, 2], [16, 112, 1]],
+               "missing": {"missing_value": -9999.0}}
+        op = "min" if i % 2 == 0 else "max"
+        creq = make_request(op, req, oracle.convert)
+        cases.append((op, req, v3.tobytes(), creq, oracle.execute(creq, v3.tobytes())))
+    bufs = _to_device(torch, cases)
+    for coalesce in (True, False):
+        eng = Engine([0])
+        eng.configure(coalesce=coalesce)
+        res = _threaded(6, list(range(len(cases))),
+                        lambda i: eng.execute_resident(cases[i][3], 0, bufs[i].data_ptr(), len(cases[i][2])))
+        for case, r in zip(cases, res):
+            _check_one(case, *r)
+        s = eng.stats(0)
+        assert s["coalesced_requests"] == (len(cases) if coalesce else 0)
+        eng.close()
+
+
+def test_host_chunks_coalesce(torch):
+    """rdx_execute from threads with host chunks below coalesce_host_max_bytes: the chunk crosses PCIe on
+    the caller's workspace stream, then joins a coalesced launch."""
+    eng = Engine([0])
+    cases = _cases(7300, 300)
+    res = _threaded(8, cases, lambda c: eng.execute_raw(c[3], c[2]))
+    for case, r in zip(cases, res):
+        _check_one(case, *r)
+    s = eng.stats(0)
+    assert s["coalesced_requests"] > 0 and s["workspaces"] <= s["max_workspaces"]
+    eng.close()
+
+
+def test_pool_twice_one_gpu_places_and_isolates(torch):
+    """rdx_context_create([0, 0]): two pool entries on one GPU.  Concurrent host requests spread over both
+    (least outstanding bytes), each entry keeps its own workspaces, results bit-exact; resident requests
+    name device 0 and may go to either entry."""
+    eng = Engine([0, 0])
+    cases = _cases(7400, 300)
+    res = _threaded(8, cases, lambda c: eng.execute_raw(c[3], c[2]))
+    for case, r in zip(cases, res):
+        _check_one(case, *r)
+    s0, s1 = eng.stats(0), eng.stats(1)
+    assert s0["device"] == s1["device"] == 0
+    assert s0["requests"] + s1["requests"] == _plannable(cases)
+    assert s0["requests"] > 0 and s1["requests"] > 0
+    assert s0["workspaces"] >= 1 and s1["workspaces"] >= 1
+    assert s0["outstanding_bytes"] == s1["outstanding_bytes"] == 0
+    bufs = _to_device(torch, cases)
+    res = _threaded(8, list(range(len(cases))),
+                    lambda i: eng.execute_resident(cases[i][3], 0, bufs[i].data_ptr(), len(cases[i][2])))
+    for case, r in zip(cases, res):
+        _check_one(case, *r)
+    # a resident chunk on a device outside the pool is an invalid argument, not a crash
+    ok = _abi.CRequest("sum", "int32")
+    st, *_ = eng.execute_resident(ok, 7, bufs[0].data_ptr(), 16)
+    assert st == _abi.E_INVALID_ARGUMENT
+    with pytest.raises(Exception):
+        eng.stats(2)
+    eng.close()
+
+
+def test_back_pressure_one_workspace(torch):
+    """max_workspaces = 1, coalescing off, 8 threads: one workspace serves everything, the others wait."""
+    eng = Engine([0])
+    eng.configure(max_workspaces=1, coalesce=False)
+    cases = _cases(7500, 160)
+    res = _threaded(8, cases, lambda c: eng.execute_raw(c[3], c[2]))
+    for case, r in zip(cases, res):
+        _check_one(case, *r)
+    s = eng.stats(0)
+    assert s["workspaces"] == 1 and s["max_workspaces"] == 1 and s["waits"] > 0 and s["coalesced_requests"] == 0
+    eng.close()
+
+
+def test_nan_fails_only_its_own_request(torch):
+    """min over a chunk holding a NaN panics in the reference (operations.rs:355-357 -> RDX_E_NAN_UNORDERED);
+    inside a coalesced launch the neighbours still get their results."""
+    eng = Engine([0])
+    eng.configure(coalesce_lanes=1)
+    good = np.arange(1000, dtype=np.float32)
+    bad = good.copy()
+    bad[500] = np.nan
+    creq = _abi.CRequest("min", "float32")
+    chunks = [bad if i % 3 == 0 else good for i in range(48)]
+    bufs = [torch.from_numpy(c.view(np.uint8).copy()).cuda() for c in chunks]
+    res = _threaded(12, list(range(48)), lambda i: eng.execute_resident(creq, 0, bufs[i].data_ptr(), 4000))
+    for i, (st, info, body, counts) in enumerate(res):
+        if i % 3 == 0:
+            assert st == _abi.E_NAN_UNORDERED
+        else:
+            assert st == 0 and np.frombuffer(body, np.float32)[0] == 0.0 and counts == [1000]
+    eng.close()

@@ -18,7 +18,8 @@ HDR = (ROOT / "include" / "rdx.h").read_text()
 
 RUST_TO_C = {"RdxSlice": "rdx_slice", "RdxFilter": "rdx_filter", "RdxMissing": "rdx_missing",
              "RdxRequest": "rdx_request", "RdxResponseInfo": "rdx_response_info", "RdxMultiItem": "rdx_multi_item",
-             "RdxResult": "rdx_result"}
+             "RdxResult": "rdx_result", "RdxContextConfig": "rdx_context_config",
+             "RdxDeviceStats": "rdx_device_stats"}
 PRIM = {"u32": (4, 4), "i32": (4, 4), "c_int": (4, 4), "u64": (8, 8), "i64": (8, 8), "f64": (8, 8)}
 
 
