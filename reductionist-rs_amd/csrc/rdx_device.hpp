@@ -692,16 +692,37 @@ __device__ __forceinline__ bool arrive_last(uint32_t *tk, uint32_t n, uint32_t b
     return __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
 }
 
-// The hand-off's second half: this workgroup's records are published; count its arrival (8-way
-// sharded, `members` workgroups per chunk) and, if it is the last, fold records P[0 .. nrec) in index
-// order (deterministic) and write the chunk's response.
+// A chunk's response as 3 tagged granules in a page-locked host slot (KOut::host_slots): the host polls
+// them for this launch's tag, as the in-launch hand-off does (no fence, no end-of-kernel flush in the way:
+// the caller sees its result as soon as the fold's stores cross the link).  {value lo32}, {value hi32},
+// {count (< 2^40) | status << 40}, each with the epoch in bits 48-63; system-scope vector stores.
+__device__ __forceinline__ void put_host_slot(uint64_t *slot, uint64_t value, int64_t count, uint32_t status,
+                                              uint32_t tag) {
+    const uint64_t t = (uint64_t)tag << 48;
+    __hip_atomic_store(slot + 0, (value & 0xffffffffull) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot + 1, (value >> 32) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot + 2, ((uint64_t)count & ((1ull << 40) - 1)) | ((uint64_t)(status & 0xffu) << 40) | t,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The hand-off's second half: this workgroup's records are published; elect the folder and let it fold
+// records P[0 .. nrec) in index order (deterministic) and write the chunk's response.
+//   fold_last == 0: count the arrival (8-way sharded counters, `members` workgroups per chunk); the last
+//     to arrive folds.  Costs two dependent atomic round trips per workgroup (~1.1 us each under load).
+//   fold_last == 1: the chunk's last block (b == members - 1) folds, polling each record until it carries
+//     this launch's tag; every other block publishes and exits.  Workgroups are dispatched in index order
+//     (per XCD), so every block the folder waits on was dispatched before it and runs to completion
+//     without waiting on anything; the host uses this form only for launches of <= kFoldLastChunks
+//     folders, far fewer than one XCD's workgroup slots, so folders can never fill an XCD and keep a
+//     lower-index block of their own chunk from being dispatched.  A record that never
+//     arrives (a device fault) still ends in RDX_E_DEVICE after kSpinLimit polls, never in a hang.
 template <typename T, int OP>
 __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chunk, uint32_t members, uint32_t nrec,
                                 uint32_t b) {
     __shared__ uint32_t s_last, s_fault;
     constexpr int kR = granules<T, OP>();   // u64 granules per record
     if (threadIdx.x == 0) {
-        s_last = arrive_last(out.tickets + (uint64_t)chunk * kTicketWords, members, b);
+        s_last = out.fold_last ? (b == members - 1) : arrive_last(out.tickets + (uint64_t)chunk * kTicketWords, members, b);
         s_fault = 0;
     }
     RDX_STAMP(2);
@@ -728,20 +749,26 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
     if (fault) s_fault = 1;   // benign race: every writer stores 1
     block_reduce(acc);
     if (threadIdx.x == 0) {
-        if constexpr (OP == OP_COUNT) {
-            reinterpret_cast<int64_t *>(out.body + chunk * out.body_stride)[0] = acc.cnt;
+        uint32_t e = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
+        if (s_fault) e = RDX_E_DEVICE;
+        if (out.host_slots) {
+            const uint64_t v = OP == OP_COUNT ? (uint64_t)acc.cnt : (uint64_t)to_u<T>(acc.value());
+            put_host_slot(reinterpret_cast<uint64_t *>(out.body) + 3 * (uint64_t)chunk, v, acc.cnt, e, out.epoch);
         } else {
-            reinterpret_cast<T *>(out.body + chunk * out.body_stride)[0] = acc.value();
+            if constexpr (OP == OP_COUNT) {
+                reinterpret_cast<int64_t *>(out.body + chunk * out.body_stride)[0] = acc.cnt;
+            } else {
+                reinterpret_cast<T *>(out.body + chunk * out.body_stride)[0] = acc.value();
+            }
+            out.counts[chunk * out.counts_stride] = acc.cnt;
+            if (out.status) {
+                if (!out.status_any) out.status[chunk] = e;
+                else if (e) __hip_atomic_fetch_or(out.status, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (!Red<T, OP>::kRank && chunk == 0) out.status[0] = 0;   // nothing can fail
+            }
         }
-        out.counts[chunk * out.counts_stride] = acc.cnt;
-        if (out.status) {
-            uint32_t e = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
-            if (s_fault) e = RDX_E_DEVICE;
-            if (!out.status_any) out.status[chunk] = e;
-            else if (e) __hip_atomic_fetch_or(out.status, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else if (!Red<T, OP>::kRank && chunk == 0) out.status[0] = 0;   // nothing can fail
-        }
-        __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!out.fold_last)
+            __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     RDX_STAMP(3);
 }
@@ -753,7 +780,15 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
     constexpr int kR = granules<T, OP>();
     block_reduce(r);
     const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kR;
-    if (threadIdx.x == 0) publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
+#if RDX_PROBES
+    // fault injection (probe builds): grid block drop_block - 1 never publishes its record (it still
+    // arrives / folds as usual), the way a faulted producer would look to the folder
+    const bool drop = out.drop_block == 1 + blockIdx.x;
+#else
+    constexpr bool drop = false;
+#endif
+    if (threadIdx.x == 0 && !drop) publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
+    if (out.fold_last && b != bpc - 1) return;   // only the folder goes on (no arrival to count)
     arrive_and_fold<T, OP>(out, P, chunk, bpc, bpc, b);
 }
 

@@ -57,6 +57,14 @@ struct KOut {
     uint32_t status_any;      // 1: one status word for all chunks (chunks = outputs of an axis
                               // reduction), NaN ORed in; the caller clears it when a NaN can set it
     uint32_t epoch;           // this launch's hand-off tag (never 0): records carry it per granule
+    uint32_t fold_last;       // 1: the chunk's LAST block (the last one dispatched) folds the records,
+                              // polling them; no arrival counters (rdx_device.hpp arrive_and_fold)
+    uint32_t host_slots;      // 1: `body` is a page-locked host slot of 3 tagged granules per chunk
+                              // (value lo, value hi, count | status), written with system-scope stores
+#if RDX_PROBES
+    uint32_t drop_block;      // probe builds: 1 + the grid block that skips publishing (0: none)
+    uint32_t pad_probe;
+#endif
 };
 
 // Reduction over ALL axes of a view whose elements form one ascending contiguous run
@@ -152,10 +160,12 @@ struct KMultiReq {
 };
 static_assert(sizeof(KMultiReq) == 152, "KMultiReq layout");
 
+enum : uint32_t { kMultiFoldLast = 1, kMultiHostSlots = 2 };   // KMultiArgs::flags -> KOut
 struct KMultiArgs {
     uint64_t *partials;              // hand-off records: request k's block b at (block0 + b) * kRecordU64
     uint32_t *tickets;               // request k's arrival counters at k * kTicketWords
     uint32_t n_items, epoch;
+    uint32_t flags, pad;
     KMultiReq req[kMultiMaxItems];
 };
 static_assert(sizeof(KMultiArgs) <= 4096, "k_multi arguments exceed 4 KiB");

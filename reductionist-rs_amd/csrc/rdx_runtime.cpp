@@ -7,6 +7,8 @@
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
+#include <chrono>
+#include <cstdio>
 #include <deque>
 #include <memory>
 #include <thread>
@@ -60,12 +62,14 @@ struct Tuning {
     int axis_fold_sep = env_int("RDX_AXIS_FOLD_SEP", -1);              // cols fold launch: -1 auto, 0 off, 1 on
 #if RDX_PROBES
     int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
+    int drop_block = env_int("RDX_DROP_BLOCK", 0);                     // fault injection: 1 + grid block
 #else
     int axis_probe = 0;   // product builds: the phase probe is compiled out (make EXTRA=-DRDX_PROBES=1)
 #endif
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
+    int fold_last = env_int("RDX_FOLD_LAST", 1);                       // A/B: 0 = arrival counters everywhere
 };
 
 const Tuning &tuning() {
@@ -127,40 +131,54 @@ struct rdx_workspace {
 
 namespace {
 
-// One in-flight k_multi launch of the coalescer: its own workspace (stream, hand-off records) and a
-// result slot per request (device, then page-locked host) filled by one copy per launch.
-constexpr uint64_t kSlotBytes = 32;   // [0, 8) body (value / i64 count), [8, 16) count, [16, 20) status
+// One k_multi launch lane of the coalescer: its own workspace (stream, hand-off records), an event, and a
+// page-locked result slot per request that the kernel writes directly (no copy-engine round trip).
+// Launches with up to this many chunks (folders) use the fold-by-last-block hand-off (KOut::fold_last).
+constexpr uint64_t kFoldLastChunks = 64;
+constexpr uint64_t kSlotWords = 3;   // rdx_device.hpp put_host_slot: value lo, value hi, count | status
+struct Job;
 struct Lane {
     rdx_workspace *ws = nullptr;
-    uint8_t *d_res = nullptr;
-    uint8_t *h_res = nullptr;
-    hipEvent_t done = nullptr;
+    uint64_t *h_res = nullptr;               // kMultiMaxItems slots, fine-grained page-locked memory
+    hipEvent_t done = nullptr;               // recorded after the launch: the fault fallback
+    Job *batch[kMultiMaxItems] = {};
+    uint32_t n = 0;                          // requests of the launch (0: the lane is free)
+    uint32_t remaining = 0;                  // of which not yet seen
+    uint32_t tag = 0;                        // the launch's epoch (its slots' tag)
+    uint32_t polls = 0;
+    std::chrono::steady_clock::time_point t0;   // when the launch was issued (dispatch statistics)
 };
 
 rdx_context_config effective_config(const rdx_context_config &c);
 void destroy_lane(Lane *L);
 
-// A request waiting for (or in) a coalesced launch.
+// A request waiting for (or in) a coalesced launch.  The caller owns it and spins on `done`.
 struct Job {
     KMultiReq q{};                 // chunk / view / op; outputs are bound to the lane's slots at launch
     uint64_t body_bytes = 0, n_counts = 0;
     void *h_body = nullptr;        // host destinations
     int64_t *h_counts = nullptr;
     rdx_status st = RDX_OK;
-    bool done = false;
+    std::atomic<bool> done{false};
 };
 
 // One entry of the context's device pool.
 struct PoolEntry {
     int device = 0;
-    std::mutex mu;                               // everything below but `outstanding`
+    std::mutex mu;                               // everything below but `outstanding` / the dispatcher's lanes
     std::condition_variable ws_cv;               // a workspace was released
     std::vector<rdx_workspace *> free_ws;
     std::vector<rdx_workspace *> all_ws;
     uint32_t busy = 0, creating = 0;
-    std::condition_variable job_cv;              // a coalesced launch finished
-    std::deque<Job *> jobs;                      // FIFO of queued requests
-    std::vector<Lane *> idle_lanes, all_lanes;
+    // the coalescer: callers append to `jobs`; one dispatcher thread per entry launches and completes them
+    std::condition_variable job_cv;              // the idle dispatcher waits here for work
+    std::deque<Job *> jobs;
+    std::thread dispatcher;
+    bool dispatcher_idle = false, stop = false;
+    std::vector<Lane *> lanes;                   // dispatcher-owned
+    // dispatcher timing (RDX_DISPATCH_STATS=1: printed to stderr when the context is destroyed)
+    double t_launch = 0, t_flight = 0, t_complete = 0;
+    uint64_t n_launch = 0, n_done = 0;
     std::atomic<uint64_t> outstanding{0};        // chunk bytes in flight (placement key)
     uint64_t requests = 0, coalesced = 0, launches = 0, waits = 0;
 };
@@ -327,6 +345,11 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
     out.status = d_status;
     out.body_stride = body_bytes;
     out.counts_stride = n_counts;
+    // all-axes launches of few chunks: the last block of each chunk folds (no arrival counters)
+    out.fold_last = n_chunks <= kFoldLastChunks && tuning().fold_last ? 1u : 0u;
+#if RDX_PROBES
+    out.drop_block = (uint32_t)tuning().drop_block;
+#endif
 
     switch (p.mode) {
         case Mode::AllContig: {
@@ -410,6 +433,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 c.out.body_stride = p.op == RDX_OP_COUNT ? 8 : p.esz;
                 c.out.counts_stride = 1;
                 c.out.status_any = 1;
+                c.out.fold_last = a.n_out <= kFoldLastChunks && tuning().fold_last ? 1u : 0u;
                 c.out.partials = ws->partials.p;
                 c.out.tickets = ws->tickets.p;
                 RDX_HIP(launch_all_contig(p.dtype, p.op, c, (uint32_t)a.n_out, s));
@@ -1018,8 +1042,21 @@ rdx_status rdx_context_create(const int *devices, int n_devices, rdx_context **o
 void rdx_context_destroy(rdx_context *ctx) {
     if (!ctx) return;
     for (auto &e : ctx->entries) {
+        {
+            std::lock_guard<std::mutex> g(e->mu);
+            e->stop = true;
+        }
+        e->job_cv.notify_all();
+        if (e->dispatcher.joinable()) e->dispatcher.join();   // returns once its queue and lanes are empty
+        if (env_int("RDX_DISPATCH_STATS", 0) && e->n_launch)
+            std::fprintf(stderr,
+                         "{\"rdx_dispatch\": {\"device\": %d, \"launches\": %llu, \"requests\": %llu, "
+                         "\"launch_host_us\": %.2f, \"issue_to_seen_done_us\": %.2f, \"complete_us\": %.2f}}\n",
+                         e->device, (unsigned long long)e->n_launch, (unsigned long long)e->coalesced,
+                         e->t_launch / e->n_launch, e->t_flight / std::max<uint64_t>(1, e->n_done),
+                         e->t_complete / std::max<uint64_t>(1, e->n_done));
         for (rdx_workspace *ws : e->all_ws) destroy_workspace(ws);
-        for (Lane *l : e->all_lanes) destroy_lane(l);
+        for (Lane *l : e->lanes) destroy_lane(l);
     }
     for (auto &kv : ctx->pinned_free)
         for (void *p : kv.second) (void)hipHostFree(p);
@@ -1239,9 +1276,12 @@ bool multi_req(const ExecPlan &p, const rdx_multi_item &it, KMultiReq &q) {
 // One k_multi launch over reqs[0..n): one residency round of the chip (5 workgroups per CU) serves the
 // whole launch; a launch that wants more gets proportionally fewer, longer-running workgroups per request
 // (each lane keeps 4-8 loads in flight per step), so no request pays several dispatch + hand-off rounds.
-rdx_status launch_multi_group(rdx_workspace *ws, const KMultiReq *reqs, uint32_t n, hipStream_t s) {
+rdx_status launch_multi_group(rdx_workspace *ws, const KMultiReq *reqs, uint32_t n, hipStream_t s,
+                              uint32_t flags = 0) {
     KMultiArgs args;
     args.n_items = n;
+    args.flags = flags | (tuning().fold_last ? kMultiFoldLast : 0u);   // <= 24 folders: always fold-last
+    args.pad = 0;
     const uint64_t target = (uint64_t)ws->cus * tuning().multi_blocks_per_cu;
     uint64_t want = 0;
     for (uint32_t k = 0; k < n; ++k) want += std::min<uint64_t>(reqs[k].bpc, (uint64_t)ws->cus * 8);
@@ -1374,7 +1414,6 @@ rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease) {
 void destroy_lane(Lane *L) {
     if (!L) return;
     if (L->ws) destroy_workspace(L->ws);   // synchronises its stream first
-    if (L->d_res) (void)hipFree(L->d_res);
     if (L->h_res) (void)hipHostFree(L->h_res);
     if (L->done) (void)hipEventDestroy(L->done);
     delete L;
@@ -1385,9 +1424,13 @@ rdx_status create_lane(int device, Lane **out) {
     if (!L) return RDX_E_OUT_OF_MEMORY;
     rdx_status st = create_workspace(device, &L->ws);
     if (!st) {
-        hipError_t e = hipMalloc((void **)&L->d_res, kMultiMaxItems * kSlotBytes);
-        if (e == hipSuccess) e = hipHostMalloc((void **)&L->h_res, kMultiMaxItems * kSlotBytes, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&L->done, hipEventDisableTiming);
+        // fine-grained (coherent): the kernel's system-scope stores land in host memory directly
+        hipError_t e = hipHostMalloc((void **)&L->h_res, kMultiMaxItems * kSlotWords * sizeof(uint64_t),
+                                     hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            std::memset(L->h_res, 0, kMultiMaxItems * kSlotWords * sizeof(uint64_t));
+            e = hipEventCreateWithFlags(&L->done, hipEventDisableTiming);
+        }
         st = map_err(e);
     }
     if (st) {
@@ -1398,103 +1441,169 @@ rdx_status create_lane(int device, Lane **out) {
     return RDX_OK;
 }
 
-// Completion of a launch the caller needs before it can answer: poll the event (a blocking
-// synchronisation sleeps on an interrupt and wakes tens of microseconds late; only lane holders poll).
-rdx_status wait_done(hipEvent_t ev) {
-    for (;;) {
-        const hipError_t e = hipEventQuery(ev);
-        if (e == hipSuccess) return RDX_OK;
-        if (e != hipErrorNotReady) return map_err(e);
-        std::this_thread::yield();
-    }
-}
-
-// One coalesced launch: the queued requests' descriptors with their outputs bound to the lane's result
-// slots, one k_multi launch, one copy of the slots to page-locked memory, then each request's result into
-// its caller's buffers.
-rdx_status run_lane(Lane &L, Job *const *batch, uint32_t n) {
+// Launch a lane's batch: the queued requests' descriptors with their outputs bound to the lane's host
+// slots (the folds write them over the link as tagged granules; KOut::host_slots).
+rdx_status launch_lane(Lane &L) {
     rdx_workspace *ws = L.ws;
-    RDX_HIP(hipSetDevice(ws->device));
-    const hipStream_t s = ws->own_stream;
+    // the epoch wraps at 2^16 launches: clear the slots so that no stale slot can carry a current tag (the
+    // lane is idle here; its stream orders the next launch after everything before)
+    if (ws->epoch + 1 > 0xffffu) std::memset(L.h_res, 0, kMultiMaxItems * kSlotWords * sizeof(uint64_t));
     KMultiReq g[kMultiMaxItems];
-    for (uint32_t i = 0; i < n; ++i) {
-        g[i] = batch[i]->q;
-        uint8_t *slot = L.d_res + (uint64_t)i * kSlotBytes;
-        g[i].body = slot;
-        g[i].counts = reinterpret_cast<int64_t *>(slot + 8);
-        g[i].status = reinterpret_cast<uint32_t *>(slot + 16);
+    for (uint32_t i = 0; i < L.n; ++i) {
+        g[i] = L.batch[i]->q;
+        g[i].body = reinterpret_cast<uint8_t *>(L.h_res + (uint64_t)i * kSlotWords);
+        g[i].counts = nullptr;
+        g[i].status = nullptr;
     }
     rdx_status st;
-    if ((st = launch_multi_group(ws, g, n, s))) return st;
-    RDX_HIP(hipMemcpyAsync(L.h_res, L.d_res, (uint64_t)n * kSlotBytes, hipMemcpyDeviceToHost, s));
-    RDX_HIP(hipEventRecord(L.done, s));
-    if ((st = wait_done(L.done))) return st;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t *slot = L.h_res + (uint64_t)i * kSlotBytes;
-        Job &j = *batch[i];
-        uint32_t status = 0;
-        std::memcpy(&status, slot + 16, sizeof status);
-        j.st = (rdx_status)status;
-        if (j.body_bytes) std::memcpy(j.h_body, slot, j.body_bytes);
-        if (j.n_counts) std::memcpy(j.h_counts, slot + 8, sizeof(int64_t));
-    }
+    if ((st = launch_multi_group(ws, g, L.n, ws->own_stream, kMultiHostSlots))) return st;
+    L.tag = ws->epoch;
+    RDX_HIP(hipEventRecord(L.done, ws->own_stream));
+    L.remaining = L.n;
+    L.polls = 0;
     return RDX_OK;
 }
 
-// Queue the request on its entry and wait for its result.  Whoever finds a lane free (an idle one, or a
-// new one below coalesce_lanes) takes everything queued (up to kMultiMaxItems, oldest first) into one
-// launch — its own request among them or not — and loops until its own request is done.  Under load the
-// queue grows while the lanes are busy, so launches fill up by themselves; alone, a request launches at
-// once.
-rdx_status coalesce(rdx_context *ctx, PoolEntry &e, Job &job) {
-    std::unique_lock<std::mutex> lk(e.mu);
-    e.jobs.push_back(&job);
-    ++e.coalesced;
-    while (!job.done) {
-        Lane *lane = nullptr;
-        if (!e.jobs.empty()) {
-            if (!e.idle_lanes.empty()) {
-                lane = e.idle_lanes.back();
-                e.idle_lanes.pop_back();
-            } else if (e.all_lanes.size() < ctx->cfg.coalesce_lanes) {
-                const rdx_status st = create_lane(e.device, &lane);   // under the lock: once per lane
-                if (st) {
-                    lane = nullptr;
-                    if (e.all_lanes.empty()) {   // nothing can serve the queue: fail it
-                        for (Job *j : e.jobs) {
-                            j->st = st;
-                            j->done = true;
-                        }
-                        e.jobs.clear();
-                        e.job_cv.notify_all();
-                        break;
-                    }
-                } else {
-                    e.all_lanes.push_back(lane);
-                }
+void finish_job(Job &j, rdx_status st) {
+    j.st = st;
+    j.done.store(true, std::memory_order_release);
+}
+
+// Poll a launched lane's slots: every request whose three granules carry the launch's tag is decoded into
+// its caller's buffers and released.  `kernel_done`: the launch has ended (its event), so a slot still
+// without the tag will never get it (a device fault): its request fails with RDX_E_DEVICE.  Returns true
+// when the lane became free.
+bool poll_lane(Lane &L, bool kernel_done) {
+    for (uint32_t i = 0; i < L.n; ++i) {
+        Job *j = L.batch[i];
+        if (!j) continue;
+        const uint64_t *slot = L.h_res + (uint64_t)i * kSlotWords;
+        const uint64_t g0 = __atomic_load_n(slot + 0, __ATOMIC_ACQUIRE);
+        const uint64_t g1 = __atomic_load_n(slot + 1, __ATOMIC_ACQUIRE);
+        const uint64_t g2 = __atomic_load_n(slot + 2, __ATOMIC_ACQUIRE);
+        const bool fresh = (g0 >> 48) == L.tag && (g1 >> 48) == L.tag && (g2 >> 48) == L.tag;
+        if (!fresh && !kernel_done) continue;
+        if (!fresh) {
+            finish_job(*j, RDX_E_DEVICE);
+        } else {
+            const uint64_t value = (g0 & 0xffffffffull) | (g1 & 0xffffffffull) << 32;
+            const int64_t count = (int64_t)(g2 & ((1ull << 40) - 1));
+            if (j->body_bytes) std::memcpy(j->h_body, &value, j->body_bytes);   // little-endian: low bytes first
+            if (j->n_counts) std::memcpy(j->h_counts, &count, sizeof count);
+            finish_job(*j, (rdx_status)((g2 >> 40) & 0xffu));
+        }
+        L.batch[i] = nullptr;
+        --L.remaining;
+    }
+    if (L.remaining) return false;
+    L.n = 0;
+    return true;
+}
+
+// The entry's dispatcher thread: the only thread that launches coalesced work on this entry.  It takes
+// everything queued (up to kMultiMaxItems per launch, oldest first) onto any free lane at once, polls the
+// lanes' events, and completes their requests.  While the lanes are busy the queue grows, so launches
+// fill up by themselves under load; a lone request launches at once.  With nothing queued or in flight
+// it sleeps on job_cv.
+void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
+    (void)hipSetDevice(e->device);
+    std::deque<Job *> pending;
+    uint32_t in_flight = 0;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(e->mu);
+            if (pending.empty() && in_flight == 0) {
+                e->dispatcher_idle = true;
+                e->job_cv.wait(lk, [&] { return !e->jobs.empty() || e->stop; });
+                e->dispatcher_idle = false;
+                if (e->jobs.empty() && e->stop) return;
+            }
+            while (!e->jobs.empty()) {
+                pending.push_back(e->jobs.front());
+                e->jobs.pop_front();
             }
         }
-        if (!lane) {
-            e.job_cv.wait(lk);
-            continue;
+        bool progressed = false;
+        // launch on free lanes (created up to coalesce_lanes)
+        while (!pending.empty()) {
+            Lane *lane = nullptr;
+            for (Lane *l : e->lanes)
+                if (l->n == 0) { lane = l; break; }
+            if (!lane && e->lanes.size() < ctx->cfg.coalesce_lanes) {
+                if (create_lane(e->device, &lane) == RDX_OK) e->lanes.push_back(lane);
+                else lane = nullptr;
+            }
+            if (!lane) {
+                if (e->lanes.empty()) {   // nothing can serve the queue: fail it
+                    for (Job *j : pending) {
+                        j->st = RDX_E_DEVICE;
+                        j->done.store(true, std::memory_order_release);
+                    }
+                    pending.clear();
+                }
+                break;
+            }
+            while (lane->n < (uint32_t)kMultiMaxItems && !pending.empty()) {
+                lane->batch[lane->n++] = pending.front();
+                pending.pop_front();
+            }
+            const uint32_t n = lane->n;
+            const auto t0 = std::chrono::steady_clock::now();
+            const rdx_status st = launch_lane(*lane);
+            lane->t0 = std::chrono::steady_clock::now();
+            e->t_launch += std::chrono::duration<double, std::micro>(lane->t0 - t0).count();
+            ++e->n_launch;
+            if (st) {
+                for (uint32_t i = 0; i < lane->n; ++i) finish_job(*lane->batch[i], st);
+                lane->n = 0;
+            } else {
+                ++in_flight;
+            }
+            {
+                std::lock_guard<std::mutex> g(e->mu);
+                ++e->launches;
+                e->coalesced += n;
+            }
+            progressed = true;
         }
-        Job *batch[kMultiMaxItems];
-        uint32_t n = 0;
-        while (n < (uint32_t)kMultiMaxItems && !e.jobs.empty()) {
-            batch[n++] = e.jobs.front();
-            e.jobs.pop_front();
+        // results of launched lanes: their slots, and (every 64th poll) the launch's event as the fault
+        // fallback
+        for (Lane *l : e->lanes) {
+            if (l->n == 0) continue;
+            bool kernel_done = false;
+            if (++l->polls % 64 == 0) {
+                const hipError_t q = hipEventQuery(l->done);
+                kernel_done = q != hipErrorNotReady;
+            }
+            const uint32_t before = l->remaining;
+            const auto t1 = std::chrono::steady_clock::now();
+            if (poll_lane(*l, kernel_done)) {
+                e->t_flight += std::chrono::duration<double, std::micro>(t1 - l->t0).count();
+                ++e->n_done;
+                --in_flight;
+            }
+            if (l->remaining != before) progressed = true;
         }
-        ++e.launches;
-        lk.unlock();
-        const rdx_status st = run_lane(*lane, batch, n);
-        lk.lock();
-        for (uint32_t i = 0; i < n; ++i) {
-            if (st) batch[i]->st = st;
-            batch[i]->done = true;
-        }
-        e.idle_lanes.push_back(lane);
-        e.job_cv.notify_all();
+        if (!progressed) std::this_thread::yield();
     }
+}
+
+// Queue the request on its entry's coalescer and wait for its result (spinning: the result comes back
+// within microseconds of the launch, far below a sleep/wake-up round trip).
+rdx_status coalesce(rdx_context *ctx, PoolEntry &e, Job &job) {
+    {
+        std::lock_guard<std::mutex> g(e.mu);
+        if (!e.dispatcher.joinable()) {
+            try {
+                e.dispatcher = std::thread(dispatcher_loop, ctx, &e);
+            } catch (...) {
+                return RDX_E_OUT_OF_MEMORY;
+            }
+        }
+        e.jobs.push_back(&job);
+        if (e.dispatcher_idle) e.job_cv.notify_one();
+    }
+    while (!job.done.load(std::memory_order_acquire)) std::this_thread::yield();
     return job.st;
 }
 
