@@ -25,8 +25,10 @@ extra (every number DESIGN.md quotes comes from here):
   c4b_blosc2             the batch as blosc2 chunks (LZ4 / BloscLZ + shuffle), decoded on the device
   configs                (N=1) device-resident C1, C3 (min / max / valid_range) and C5 select launches
   mixed_requests         (N=1) 20 mixed C1/C3 requests in ONE heterogeneous launch (rdx_execute_multi_device)
-  concurrent_native      (N=1) C1 / C2 / C3 requests from native C++ threads (rdx_conc_bench: own workspace
-                         and stream per thread, execute + synchronize per request, no Python on the path)
+  concurrent_native      (N=1) C1 / C2 / C3 requests from native C++ threads (rdx_conc_bench): independent
+                         launches per thread, and the context pool's coalesced path (rdx_execute_resident)
+  pool                   (rank 0, all --gpus devices) ONE process, one context over every GPU, native threads
+                         issuing C4 requests from pinned host memory and HBM-resident (the server's shape)
   cbor_response          (N=1) the CBOR response body of an axis = [] count over the C5 shape (32 Mi counts)
                          packed on the device (rdx_cbor_encode_device) vs the host encoder
   host_inclusive         (N=1) C2 / C3 / C5 through rdx_execute from pageable and pinned host memory,
@@ -759,23 +761,57 @@ def leg_mixed(cx, n_pairs=10, sets=2, k=30, serial=True):
     return res
 
 
+def conc_bench(cfg, threads, reqs, path="device", devices="0"):
+    """One run of reductionist-rs_amd/rdx_conc_bench (native C++ threads over the C ABI, no Python on the
+    path): its JSON line."""
+    exe = ROOT / "reductionist-rs_amd" / "rdx_conc_bench"
+    r = subprocess.run([str(exe), cfg, str(threads), str(reqs), path, devices], capture_output=True, text=True,
+                       timeout=180)
+    if r.returncode != 0:
+        raise RuntimeError(f"rdx_conc_bench {cfg} {threads} {path} {devices}: {r.stderr[-500:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def leg_native_concurrent(cx):
-    """Concurrent single-chunk requests from native C++ threads (reductionist-rs_amd/rdx_conc_bench: each
-    thread its own workspace + stream, rdx_execute_device + synchronize per request, the way Tokio/Rayon
-    workers run requests, app.rs:147-152), 1 thread and the worker-pool size (num_cpus - 1, capped at the
-    box's CPU share)."""
+    """Concurrent single-chunk requests from native C++ threads, the way Tokio/Rayon workers run them
+    (app.rs:147-152): 1 thread and the worker-pool size (num_cpus - 1, capped at the box's CPU share).
+      device:   each thread its own workspace + stream, rdx_execute_device + synchronize per request
+                (independent launches);
+      resident: rdx_execute_resident on the context's pool — concurrent small all-axes requests are
+                coalesced by the pool's dispatcher into shared launches (same-plan groups / k_multi), each
+                caller's result written to page-locked host memory by the fold."""
     exe = ROOT / "reductionist-rs_amd" / "rdx_conc_bench"
     if not exe.exists():
         return {"skipped": f"{exe} not built"}
     out = []
     pool = pool_threads()
-    for cfg, threads, reqs in (("c3", 1, 2000), ("c3", pool, 2000), ("c1", 1, 2000), ("c1", pool, 2000),
-                               ("c2", 1, 300), ("c2", 4, 300)):
-        r = subprocess.run([str(exe), cfg, str(threads), str(reqs)], capture_output=True, text=True, timeout=120)
-        if r.returncode != 0:
-            raise RuntimeError(f"rdx_conc_bench {cfg} {threads}: {r.stderr[-500:]}")
-        out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    for cfg, threads, reqs, path in (("c3", 1, 2000, "device"), ("c3", pool, 2000, "device"),
+                                     ("c3", 1, 2000, "resident"), ("c3", pool, 2000, "resident"),
+                                     ("c1", 1, 2000, "device"), ("c1", pool, 2000, "device"),
+                                     ("c1", 1, 2000, "resident"), ("c1", pool, 2000, "resident"),
+                                     ("c1", 4 * pool, 1000, "resident"),
+                                     ("c2", 1, 300, "device"), ("c2", 4, 300, "device")):
+        out.append(conc_bench(cfg, threads, reqs, path))
     return out
+
+
+def leg_pool(cx):
+    """The server's real shape (app_state.rs:21-37: ONE process, every request on a worker thread): one
+    rdx_context pooling all --gpus devices, T native threads issuing C4 requests (4 MiB shuffled f32 chunks,
+    sum) — from page-locked host memory through rdx_execute (PCIe H2D per request), and HBM-resident
+    through rdx_execute_resident — placed by least outstanding bytes.  Run by rank 0 alone while the other
+    ranks wait at a barrier (their GPUs idle)."""
+    exe = ROOT / "reductionist-rs_amd" / "rdx_conc_bench"
+    res = None
+    if cx.rank == 0 and exe.exists():
+        n = cx.torch.cuda.device_count()
+        devs = ",".join(str(d) for d in range(min(n, cx.world)))
+        pool = pool_threads()
+        res = {"devices": devs,
+               "host": conc_bench("c4", max(pool, 2 * cx.world), 300, "host", devs),
+               "resident": conc_bench("c4", max(pool, 4 * cx.world), 1000, "resident", devs)}
+    cx.barrier()
+    return res
 
 
 def leg_cbor(cx, with_cpu):
@@ -1075,6 +1111,8 @@ def main():
         extra["cbor_response"] = leg_cbor(cx, solo and not args.no_cpu_baseline)
     if world == 1 and not args.no_host:
         extra["host_inclusive"] = leg_host(cx)
+    if not args.no_configs:
+        extra["pool"] = leg_pool(cx)
     cpu_line = None
     if solo and not args.no_cpu_baseline:
         cpu_line, extra["cpu_baselines"] = leg_cpu(cx, args.cpu_seconds)

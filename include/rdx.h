@@ -202,7 +202,7 @@ void rdx_context_destroy(rdx_context *ctx);
 typedef struct rdx_context_config {
     uint32_t max_workspaces;        /* per pool entry (0: 16); requests beyond it wait for a free one           */
     uint32_t coalesce;              /* 1 (default): coalesce small all-axes requests into k_multi launches; 0: off */
-    uint32_t coalesce_lanes;        /* k_multi launches in flight per pool entry (0: 2)                        */
+    uint32_t coalesce_lanes;        /* coalesced launches in flight per pool entry (0: 3)                      */
     uint32_t reserved;
     uint64_t coalesce_max_bytes;    /* rdx_execute_resident chunks up to this many bytes coalesce (0: 64 MiB)  */
     uint64_t coalesce_host_max_bytes; /* rdx_execute / _owned host chunks up to this many (0: 1 MiB)           */

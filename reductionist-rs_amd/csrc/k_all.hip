@@ -38,6 +38,15 @@ __device__ __forceinline__ uint32_t comp(const uint4 &v, int j) {
     return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
+// Chunk `chunk`'s base: the argument's own table (read in place from the kernel-argument segment — the
+// kernels' only parameter, at offset 0 — so a runtime index does not copy the argument to scratch), the
+// device pointer array, or the single chunk.
+template <class A>
+__device__ __forceinline__ const uint8_t *chunk_ptr(const A &a, uint32_t chunk) {
+    if (a.src.table) return (*(const A *)__builtin_amdgcn_kernarg_segment_ptr()).tbl.p[chunk];
+    return chunk_base(a.src, chunk);
+}
+
 template <typename T, int OP, int MK>
 __device__ __forceinline__ void consume(Red<T, OP> &r, T x, const KAllContig &a, uint64_t e) {
     auto rank = [&]() -> int64_t { return a.r0 + (int64_t)(e - a.off) * a.rs; };
@@ -198,12 +207,19 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
     }
 }
 
+// Which loops are software pipelined (next tiles' loads issued before the current ones are folded).
+#ifndef RDX_PIPE_SUM
+#define RDX_PIPE_SUM 0   // variant builds: 1 = every sum, 2 = byte-shuffled 8-byte sums
+#endif
+template <typename T, int OP, bool FUSED>
+constexpr bool kPipelined = Red<T, OP>::kRank || (OP == OP_SUM && (RDX_PIPE_SUM == 1 || (RDX_PIPE_SUM == 2 && FUSED && sizeof(T) == 8)));
+
 template <typename T, int OP, bool FUSED, int MK, int UNR>
 __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     RDX_STAMP(0);
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
-    const uint8_t *base = chunk_base(a.src, chunk);
+    const uint8_t *base = chunk_ptr(a, chunk);
     const bool bswap = a.src.bswap;
     const uint32_t selA = bswap ? 0x00010405u : 0x05040100u;
     const uint32_t selB = bswap ? 0x02030607u : 0x07060302u;
@@ -233,53 +249,63 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     // round trips cost more than the imbalance, profiles/r02_pool_ab.jsonl.)
     const uint64_t te = tile_elems<T, FUSED>();
     const uint64_t nfull = (vb - va) / te;
+#if RDX_TILE_STRIDE
+    // tiles b, b + bpc, b + 2 bpc, ...: the chunk's workgroups sweep it together, a window of bpc tiles
+    // wide (few DRAM pages / translations live at once) instead of bpc separate streams
+    const uint64_t kstride = bpc, k0 = b;
+    const uint64_t nk = b < nfull ? (nfull - b + bpc - 1) / bpc : 0;
+#else
     const uint64_t per = (nfull + bpc - 1) / bpc;
     const uint64_t t_begin = (uint64_t)b * per;
     const uint64_t t_end = t_begin + per < nfull ? t_begin + per : nfull;
-    uint64_t t = t_begin;
+    const uint64_t kstride = 1, k0 = t_begin;
+    const uint64_t nk = t_end > t_begin ? t_end - t_begin : 0;
+#endif
+    auto tile = [&](uint64_t k) { return va + (k0 + k * kstride) * te; };   // first element of the k-th tile
+    uint64_t k = 0;
     // Float min/max (the heaviest per-element fold) are software pipelined: the next UNR tiles'
     // loads are issued before the current UNR tiles are consumed (two register sets, alternating),
     // so a lane's fold work overlaps its next round trip (f32 min over 8 x 64 MiB 86 -> 80 us).  Sums
     // keep the plain loop: pipelined they measured 1-3 % slower (78.6 -> 80.7 us, tools/gpu_pipe.sh).
-    if constexpr (Red<T, OP>::kRank) {
-    if (t + UNR <= t_end) {
+    if constexpr (kPipelined<T, OP, FUSED>) {
+    if (k + UNR <= nk) {
         Tile<T, FUSED> x[UNR], y[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, va + (t + u) * te, vb);
+        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + u), vb);
         while (true) {
-            const bool m1 = t + 2 * UNR <= t_end;
+            const bool m1 = k + 2 * UNR <= nk;
             if (m1) {
 #pragma unroll
-                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(y[u], base, a.src.plane, va + (t + UNR + u) * te, vb);
+                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(y[u], base, a.src.plane, tile(k + UNR + u), vb);
             }
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, va + (t + u) * te, vb, selA, selB);
-            t += UNR;
+            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
+            k += UNR;
             if (!m1) break;
-            const bool m2 = t + 2 * UNR <= t_end;
+            const bool m2 = k + 2 * UNR <= nk;
             if (m2) {
 #pragma unroll
-                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, va + (t + UNR + u) * te, vb);
+                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + UNR + u), vb);
             }
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, y[u], a, va + (t + u) * te, vb, selA, selB);
-            t += UNR;
+            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, y[u], a, tile(k + u), vb, selA, selB);
+            k += UNR;
             if (!m2) break;
         }
     }
     } else {
-    for (; t + UNR <= t_end; t += UNR) {
+    for (; k + UNR <= nk; k += UNR) {
         Tile<T, FUSED> x[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, va + (t + u) * te, vb);
+        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + u), vb);
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, va + (t + u) * te, vb, selA, selB);
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
     }
     }
-    for (; t < t_end; ++t) {
+    for (; k < nk; ++k) {
         Tile<T, FUSED> x0;
-        load_tile<T, FUSED, true>(x0, base, a.src.plane, va + t * te, vb);
-        consume_tile<T, OP, FUSED, MK, true>(r, x0, a, va + t * te, vb, selA, selB);
+        load_tile<T, FUSED, true>(x0, base, a.src.plane, tile(k), vb);
+        consume_tile<T, OP, FUSED, MK, true>(r, x0, a, tile(k), vb, selA, selB);
     }
     if (b == 0 && va + nfull * te < vb) {
         Tile<T, FUSED> x0;
@@ -350,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
     constexpr int kU = VW > 1 ? 4 : 8;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
-    const uint8_t *base = chunk_base(a.src, chunk);
+    const uint8_t *base = chunk_ptr(a, chunk);
     const bool bswap = a.src.bswap;
     const KView &v = a.view;
     DimRegs<ND> d;
@@ -410,12 +436,17 @@ void launch_contig_u(const KAllContig &a, dim3 grid, hipStream_t s) {
 #undef RDX_CONTIG
 }
 
+#ifndef RDX_UNR_F8
+#define RDX_UNR_F8 2   // tiles in flight per lane for byte-shuffled 8-byte elements (8 plane loads per tile)
+#endif
+
 template <typename T, int OP>
 hipError_t launch_contig_t(const KAllContig &a, uint32_t n_chunks, hipStream_t s) {
     const dim3 grid(a.blocks_per_chunk * n_chunks);
     // 2 tiles in flight per lane at one workgroup per CU: 4 tiles, or 2/4/6/8 workgroups per CU,
     // measured slower with non-temporal loads (tools/gpu_bpcu.sh, gpurun_out/bpcu*).
-    launch_contig_u<T, OP, 2>(a, grid, s);
+    if (sizeof(T) == 8 && a.src.fused) launch_contig_u<T, OP, RDX_UNR_F8>(a, grid, s);
+    else launch_contig_u<T, OP, 2>(a, grid, s);
     return hipGetLastError();
 }
 

@@ -34,6 +34,15 @@ struct KSrc {
     uint64_t plane;                     // bytes per byte-plane (= chunk elements) when fused
     uint32_t fused;
     uint32_t bswap;
+    uint32_t table;                     // 1: chunk i's base is tbl.p[i] of the kernel's own arguments
+    uint32_t pad;
+};
+
+// Chunk pointers carried in the kernel arguments (a coalesced group of same-plan requests: no table
+// upload between the host call and the kernel).
+constexpr int kTableChunks = 64;
+struct KChunkTable {
+    const uint8_t *p[kTableChunks];
 };
 
 // Missing-data predicate (src/types/missing.rs:114-122).  Values are raw T bits.
@@ -78,6 +87,7 @@ struct KAllContig {
     int64_t r0, rs;
     uint32_t filter_semantics;  // Count(All) uses missing_filter (operations.rs:25-33)
     uint32_t blocks_per_chunk;
+    KChunkTable tbl;            // src.table: chunk pointers (last: only this much is read)
 };
 
 // A strided view: dims innermost-first.  offset(e) = base_off + sum idx_k * vstride_k,
@@ -103,6 +113,7 @@ struct KAllStrided {
     uint32_t blocks_per_chunk;
     uint32_t vec;       // elements per 16-byte lane load along the contiguous inner dim (1 = scalar)
     uint32_t pad;
+    KChunkTable tbl;    // src.table: chunk pointers
 };
 
 // Reduction over a subset of axes.  Output o (C order over kept dims) reduces the elements

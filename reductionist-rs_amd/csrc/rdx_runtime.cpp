@@ -2,6 +2,10 @@
 // device-resident execution.  No CPU fallback exists: without a gfx950 device every execute entry
 // point fails with RDX_E_NO_DEVICE / RDX_E_DEVICE.
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+#include <ctime>
 
 #include <algorithm>
 #include <atomic>
@@ -70,6 +74,7 @@ struct Tuning {
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
     int fold_last = env_int("RDX_FOLD_LAST", 1);                       // A/B: 0 = arrival counters everywhere
+    int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
 };
 
 const Tuning &tuning() {
@@ -139,9 +144,9 @@ constexpr uint64_t kSlotWords = 3;   // rdx_device.hpp put_host_slot: value lo, 
 struct Job;
 struct Lane {
     rdx_workspace *ws = nullptr;
-    uint64_t *h_res = nullptr;               // kMultiMaxItems slots, fine-grained page-locked memory
-    hipEvent_t done = nullptr;               // recorded after the launch: the fault fallback
-    Job *batch[kMultiMaxItems] = {};
+    uint64_t *h_res = nullptr;               // kTableChunks slots, fine-grained page-locked memory
+    Job *batch[kTableChunks] = {};
+    bool group = false;                      // the launch: one plan over the batch's chunks (else k_multi)
     uint32_t n = 0;                          // requests of the launch (0: the lane is free)
     uint32_t remaining = 0;                  // of which not yet seen
     uint32_t tag = 0;                        // the launch's epoch (its slots' tag)
@@ -154,12 +159,22 @@ void destroy_lane(Lane *L);
 
 // A request waiting for (or in) a coalesced launch.  The caller owns it and spins on `done`.
 struct Job {
+    // one plan over many chunks (a batched k_all_contig / k_all_strided launch): requests with the same
+    // plan and launch descriptor (all but the chunk) share one; the descriptor's src.base is null here
+    Mode mode = Mode::AllContig;
+    uint32_t dtype = 0, op = 0, esz = 0;
+    KAllContig contig{};
+    KAllStrided strided{};
+    const uint8_t *chunk = nullptr;        // device
+    // the heterogeneous form (k_multi), when the request fits it
+    bool multi_ok = false;
     KMultiReq q{};                 // chunk / view / op; outputs are bound to the lane's slots at launch
     uint64_t body_bytes = 0, n_counts = 0;
     void *h_body = nullptr;        // host destinations
     int64_t *h_counts = nullptr;
     rdx_status st = RDX_OK;
-    std::atomic<bool> done{false};
+    std::atomic<uint32_t> done{0};       // futex word: 0 pending, 1 done
+    std::atomic<uint32_t> sleeping{0};   // the caller gave up spinning and waits on the futex
 };
 
 // One entry of the context's device pool.
@@ -1315,7 +1330,7 @@ namespace {
 rdx_context_config effective_config(const rdx_context_config &c) {
     rdx_context_config e = c;
     if (!e.max_workspaces) e.max_workspaces = 16;
-    if (!e.coalesce_lanes) e.coalesce_lanes = 2;
+    if (!e.coalesce_lanes) e.coalesce_lanes = 3;
     if (e.coalesce_lanes > 16) e.coalesce_lanes = 16;
     if (!e.coalesce_max_bytes) e.coalesce_max_bytes = 64ull << 20;
     if (!e.coalesce_host_max_bytes) e.coalesce_host_max_bytes = 1ull << 20;
@@ -1415,7 +1430,6 @@ void destroy_lane(Lane *L) {
     if (!L) return;
     if (L->ws) destroy_workspace(L->ws);   // synchronises its stream first
     if (L->h_res) (void)hipHostFree(L->h_res);
-    if (L->done) (void)hipEventDestroy(L->done);
     delete L;
 }
 
@@ -1425,12 +1439,9 @@ rdx_status create_lane(int device, Lane **out) {
     rdx_status st = create_workspace(device, &L->ws);
     if (!st) {
         // fine-grained (coherent): the kernel's system-scope stores land in host memory directly
-        hipError_t e = hipHostMalloc((void **)&L->h_res, kMultiMaxItems * kSlotWords * sizeof(uint64_t),
+        hipError_t e = hipHostMalloc((void **)&L->h_res, kTableChunks * kSlotWords * sizeof(uint64_t),
                                      hipHostMallocCoherent);
-        if (e == hipSuccess) {
-            std::memset(L->h_res, 0, kMultiMaxItems * kSlotWords * sizeof(uint64_t));
-            e = hipEventCreateWithFlags(&L->done, hipEventDisableTiming);
-        }
+        if (e == hipSuccess) std::memset(L->h_res, 0, kTableChunks * kSlotWords * sizeof(uint64_t));
         st = map_err(e);
     }
     if (st) {
@@ -1447,26 +1458,81 @@ rdx_status launch_lane(Lane &L) {
     rdx_workspace *ws = L.ws;
     // the epoch wraps at 2^16 launches: clear the slots so that no stale slot can carry a current tag (the
     // lane is idle here; its stream orders the next launch after everything before)
-    if (ws->epoch + 1 > 0xffffu) std::memset(L.h_res, 0, kMultiMaxItems * kSlotWords * sizeof(uint64_t));
-    KMultiReq g[kMultiMaxItems];
-    for (uint32_t i = 0; i < L.n; ++i) {
-        g[i] = L.batch[i]->q;
-        g[i].body = reinterpret_cast<uint8_t *>(L.h_res + (uint64_t)i * kSlotWords);
-        g[i].counts = nullptr;
-        g[i].status = nullptr;
-    }
+    if (ws->epoch + 1 > 0xffffu) std::memset(L.h_res, 0, kTableChunks * kSlotWords * sizeof(uint64_t));
     rdx_status st;
-    if ((st = launch_multi_group(ws, g, L.n, ws->own_stream, kMultiHostSlots))) return st;
+    const hipStream_t s = ws->own_stream;
+    if (L.group) {   // one plan, the chunks in the kernel arguments, chunk i's result into slot i
+        const Job &j0 = *L.batch[0];
+        KOut out{};
+        if ((st = next_epoch(ws, s, out.epoch))) return st;
+        out.body = reinterpret_cast<uint8_t *>(L.h_res);
+        out.host_slots = 1;
+        out.fold_last = L.n <= kFoldLastChunks && tuning().fold_last ? 1u : 0u;
+        if (j0.mode == Mode::AllContig) {
+            KAllContig a = j0.contig;
+            a.src.table = 1;
+            for (uint32_t i = 0; i < L.n; ++i) a.tbl.p[i] = L.batch[i]->chunk;
+            const uint64_t te = a.src.fused ? 4096 : 16384 / j0.esz;
+            a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, L.n, ws->cus);
+            if ((st = ensure(ws, ws->partials, (uint64_t)L.n * a.blocks_per_chunk * kRecordU64, s, true))) return st;
+            if ((st = ensure(ws, ws->tickets, (uint64_t)L.n * kTicketWords, s, true))) return st;
+            out.partials = ws->partials.p;
+            out.tickets = ws->tickets.p;
+            a.out = out;
+            RDX_HIP(launch_all_contig(j0.dtype, j0.op, a, L.n, s));
+        } else {
+            KAllStrided a = j0.strided;
+            a.src.table = 1;
+            for (uint32_t i = 0; i < L.n; ++i) a.tbl.p[i] = L.batch[i]->chunk;
+            const uint64_t per_block = (uint64_t)kBlock * (a.vec > 1 ? 4 : 8);
+            const uint64_t want = (a.view.n / a.vec + per_block - 1) / per_block;
+            const uint64_t cap = ((uint64_t)ws->cus * 8 + L.n - 1) / L.n;
+            a.blocks_per_chunk = (uint32_t)std::max<uint64_t>(1, std::min(want, std::max<uint64_t>(cap, 1)));
+            if ((st = ensure(ws, ws->partials, (uint64_t)L.n * a.blocks_per_chunk * kRecordU64, s, true))) return st;
+            if ((st = ensure(ws, ws->tickets, (uint64_t)L.n * kTicketWords, s, true))) return st;
+            out.partials = ws->partials.p;
+            out.tickets = ws->tickets.p;
+            a.out = out;
+            RDX_HIP(launch_all_strided(j0.dtype, j0.op, a, L.n, s));
+        }
+    } else {
+        KMultiReq g[kMultiMaxItems];
+        for (uint32_t i = 0; i < L.n; ++i) {
+            g[i] = L.batch[i]->q;
+            g[i].body = reinterpret_cast<uint8_t *>(L.h_res + (uint64_t)i * kSlotWords);
+            g[i].counts = nullptr;
+            g[i].status = nullptr;
+        }
+        if ((st = launch_multi_group(ws, g, L.n, s, kMultiHostSlots))) return st;
+    }
     L.tag = ws->epoch;
-    RDX_HIP(hipEventRecord(L.done, ws->own_stream));
     L.remaining = L.n;
     L.polls = 0;
     return RDX_OK;
 }
 
+// Completion: the result is in the caller's buffers; release it, and wake it only if it is asleep
+// (seq_cst on both sides: either the caller sees `done` before it sleeps, or this sees `sleeping`).
 void finish_job(Job &j, rdx_status st) {
     j.st = st;
-    j.done.store(true, std::memory_order_release);
+    j.done.store(1, std::memory_order_seq_cst);
+    if (j.sleeping.load(std::memory_order_seq_cst))
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&j.done), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+
+// The caller's wait: spin (no system call: a result arrives within tens of microseconds of its launch),
+// then sleep on the futex (RDX_WAIT_SPIN iterations of the spin; 0 = sleep at once).
+void wait_job(Job &j) {
+    const int spin = tuning().wait_spin;
+    for (int i = 0; i < spin; ++i) {
+        if (j.done.load(std::memory_order_acquire)) return;
+        __builtin_ia32_pause();
+    }
+    j.sleeping.store(1, std::memory_order_seq_cst);
+    while (!j.done.load(std::memory_order_seq_cst)) {
+        const timespec ts{0, 1000000};   // re-check every millisecond whatever happens
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&j.done), FUTEX_WAIT_PRIVATE, 0, &ts, nullptr, 0);
+    }
 }
 
 // Poll a launched lane's slots: every request whose three granules carry the launch's tag is decoded into
@@ -1498,6 +1564,45 @@ bool poll_lane(Lane &L, bool kernel_done) {
     if (L.remaining) return false;
     L.n = 0;
     return true;
+}
+
+// Same plan and launch descriptor but the chunk: one batched launch serves both.
+bool same_group(const Job &a, const Job &b) {
+    if (a.mode != b.mode || a.dtype != b.dtype || a.op != b.op) return false;
+    return a.mode == Mode::AllContig ? std::memcmp(&a.contig, &b.contig, sizeof a.contig) == 0
+                                     : std::memcmp(&a.strided, &b.strided, sizeof a.strided) == 0;
+}
+
+// The next launch of a free lane: the oldest request's group (every queued request with its plan, up to
+// kTableChunks) as one batched launch; a lone request with no partner among heterogeneous ones goes with
+// them into one k_multi launch (up to kMultiMaxItems, in queue order, every one k_multi can take).
+void form_batch(std::deque<Job *> &pending, Lane &L) {
+    L.n = 0;
+    Job *first = pending.front();
+    uint32_t mates = 0;
+    for (size_t i = 1; i < pending.size() && mates + 1 < (uint32_t)kTableChunks; ++i)
+        if (same_group(*first, *pending[i])) ++mates;
+    if (mates > 0 || !first->multi_ok) {
+        L.group = true;
+        for (auto it = pending.begin(); it != pending.end() && L.n < (uint32_t)kTableChunks;) {
+            if (*it == first || same_group(*first, **it)) {
+                L.batch[L.n++] = *it;
+                it = pending.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        return;
+    }
+    L.group = false;
+    for (auto it = pending.begin(); it != pending.end() && L.n < (uint32_t)kMultiMaxItems;) {
+        if ((*it)->multi_ok) {
+            L.batch[L.n++] = *it;
+            it = pending.erase(it);
+        } else {
+            ++it;
+        }
+    }
 }
 
 // The entry's dispatcher thread: the only thread that launches coalesced work on this entry.  It takes
@@ -1535,18 +1640,12 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
             }
             if (!lane) {
                 if (e->lanes.empty()) {   // nothing can serve the queue: fail it
-                    for (Job *j : pending) {
-                        j->st = RDX_E_DEVICE;
-                        j->done.store(true, std::memory_order_release);
-                    }
+                    for (Job *j : pending) finish_job(*j, RDX_E_DEVICE);
                     pending.clear();
                 }
                 break;
             }
-            while (lane->n < (uint32_t)kMultiMaxItems && !pending.empty()) {
-                lane->batch[lane->n++] = pending.front();
-                pending.pop_front();
-            }
+            form_batch(pending, *lane);
             const uint32_t n = lane->n;
             const auto t0 = std::chrono::steady_clock::now();
             const rdx_status st = launch_lane(*lane);
@@ -1567,12 +1666,12 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
             progressed = true;
         }
         // results of launched lanes: their slots, and (every 64th poll) the launch's event as the fault
-        // fallback
+        // fallback (the lane's stream idle)
         for (Lane *l : e->lanes) {
             if (l->n == 0) continue;
             bool kernel_done = false;
-            if (++l->polls % 64 == 0) {
-                const hipError_t q = hipEventQuery(l->done);
+            if (++l->polls % 64 == 0) {   // the lane's stream holds nothing but this launch
+                const hipError_t q = hipStreamQuery(l->ws->own_stream);
                 kernel_done = q != hipErrorNotReady;
             }
             const uint32_t before = l->remaining;
@@ -1603,7 +1702,7 @@ rdx_status coalesce(rdx_context *ctx, PoolEntry &e, Job &job) {
         e.jobs.push_back(&job);
         if (e.dispatcher_idle) e.job_cv.notify_one();
     }
-    while (!job.done.load(std::memory_order_acquire)) std::this_thread::yield();
+    wait_job(job);
     return job.st;
 }
 
@@ -1644,11 +1743,32 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
     auto coalescible = [&](const uint8_t *d_base, Job &job) -> bool {
         if (compressed || cb || !ctx->cfg.coalesce) return false;
         if (chunk_len > (resident ? ctx->cfg.coalesce_max_bytes : ctx->cfg.coalesce_host_max_bytes)) return false;
+        if ((p.mode != Mode::AllContig && p.mode != Mode::AllStrided) || !p.unfused_es.empty() || !p.miss_list.empty())
+            return false;
+        job.mode = p.mode;
+        job.dtype = p.dtype;
+        job.op = p.op;
+        job.esz = p.esz;
+        job.chunk = d_base;
+        KSrc src{};
+        src.plane = chunk_len / p.esz;
+        src.fused = p.fused;
+        src.bswap = p.bswap;
+        if (p.mode == Mode::AllContig) {
+            job.contig = p.all_contig;
+            job.contig.src = src;
+            job.contig.miss = p.miss;
+        } else {
+            job.strided = p.all_strided;
+            job.strided.src = src;
+            job.strided.miss = p.miss;
+            job.strided.vec = vec_width(job.strided.view, p.esz, d_base, nullptr, 1, p.fused);
+        }
         rdx_multi_item it{};
         it.req = &req;
         it.d_chunk = d_base;
         it.chunk_len = chunk_len;
-        if (!multi_req(p, it, job.q)) return false;
+        job.multi_ok = multi_req(p, it, job.q);
         job.body_bytes = p.info.body_bytes;
         job.n_counts = p.info.n_counts;
         job.h_body = body;

@@ -220,3 +220,31 @@ def test_nan_fails_only_its_own_request(torch):
         else:
             assert st == 0 and np.frombuffer(body, np.float32)[0] == 0.0 and counts == [1000]
     eng.close()
+
+
+def test_resident_same_plan_groups(torch):
+    """Concurrent requests with one plan (the same variable's chunks: shuffled big-endian f32 sums, and
+    strided f64 hyperslab max with a valid_range) are served by batched launches of that plan, chunk
+    pointers in the kernel arguments; D-int values, so every sum is exact.  Bit-exact vs the oracle."""
+    rng = np.random.default_rng(7700)
+    cases = []
+    for i in range(40):
+        v = rng.integers(-8, 9, 1 << 18).astype(np.float32)
+        req = {"dtype": "float32", "byte_order": "big", "filters": [{"id": "shuffle", "element_size": 4}]}
+        data = oracle.shuffle(v.astype(">f4").tobytes(), 4)
+        creq = make_request("sum", req, oracle.convert)
+        cases.append(("sum", req, data, creq, oracle.execute(creq, data)))
+        w = rng.integers(-1000, 1000, 40 * 50 * 30).astype(np.float64)
+        req = {"dtype": "float64", "shape": [40, 50, 30], "selection": [[1, 39, 2], [0, 50, 1], [3, 27, 1]],
+               "missing": {"valid_range": [-900.0, 900.0]}}
+        creq = make_request("max", req, oracle.convert)
+        cases.append(("max", req, w.tobytes(), creq, oracle.execute(creq, w.tobytes())))
+    bufs = _to_device(torch, cases)
+    eng = Engine([0])
+    res = _threaded(12, list(range(len(cases))),
+                    lambda i: eng.execute_resident(cases[i][3], 0, bufs[i].data_ptr(), len(cases[i][2])))
+    for case, r in zip(cases, res):
+        _check_one(case, *r)
+    s = eng.stats(0)
+    assert s["coalesced_requests"] == len(cases) and s["coalesced_launches"] < len(cases)
+    eng.close()
