@@ -587,7 +587,9 @@ def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
             list(ex.map(one, range(n_total)))
             tz = time.perf_counter() - c0
         out["cpu_baseline"] = {"value": round(n_total * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
-                               "kind": "port", "sample": f"oracle_blosc2_decompress (scalar C++, g++ -O2) of all "
+                               "kind": "port", "sample": f"this repo's scalar port of the blosc2 decoder "
+                                                         f"(oracle_blosc2_decompress, g++ -O2; NOT c-blosc2 / blusc, "
+                                                         f"whose SIMD decoders are absent from the image) over all "
                                                          f"{n_total} lz4 chunks on a {threads}-thread pool, {tz:.2f} s"}
     return out
 
@@ -1001,10 +1003,12 @@ def leg_cpu(cx, seconds):
     return headline, res
 
 
-def cpu_baseline_c4(threads, distinct=64):
+def cpu_baseline_c4(threads, distinct=256):
     """C4 on the host the way the reference serves it: independent requests on a worker pool
     (thread_limit = num_cpus - 1, src/app_state.rs:22; capped at the CPUs this job may use).  1024 chunks
-    of 4 MiB (64 distinct, cycled), unshuffle + f32 sum each, by the oracle; ctypes releases the GIL."""
+    of 4 MiB (256 distinct = 1 GiB, cycled: four times the host's 256 MB L3, so the chunks stream from
+    DRAM as a server's downloaded chunks would), unshuffle + f32 sum each, by the oracle; ctypes releases
+    the GIL."""
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     from oracle import py_oracle as oracle
@@ -1031,8 +1035,8 @@ def cpu_baseline_c4(threads, distinct=64):
         list(ex.map(one, range(C4_CHUNKS)))
         el = time.perf_counter() - t0
     return {"value": round(C4_CHUNKS * 4 * C4_ELEMS / el / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "port", "sample": f"all {C4_CHUNKS} chunks ({distinct} distinct, cycled), {threads} worker "
-                                      f"threads, oracle g++ -O2, {el:.2f} s"}
+            "kind": "port", "sample": f"all {C4_CHUNKS} chunks ({distinct} distinct = {distinct * 4} MiB, cycled: "
+                                      f"not cache-resident), {threads} worker threads, oracle g++ -O2, {el:.2f} s"}
 
 
 def devices_used(cx):

@@ -34,7 +34,7 @@ pub fn gpu_routes() -> axum::Router<crate::app_state::SharedAppState> {
 
 /// Replaces `operation::<T>` (app.rs:163-183) for the GPU plugins; `operation_handler` (app.rs:123-153)
 /// calls it in place of `operation` (under the same task permit / rayon spawn).
-pub fn operation_gpu<T: operation::Operation>(
+pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
     request_data: models::RequestData,
     data: Bytes,
 ) -> Result<models::Response, ActiveStorageError> {
@@ -42,12 +42,13 @@ pub fn operation_gpu<T: operation::Operation>(
     // chunk in ~100-220 ms, a CPU core in ~4-7 ms.  A lone gzip/zlib request therefore
     // keeps the reference's host decompression (compression.rs:18-27); those chunks are inflated on the
     // device only in batches (rdx_decompress_batch_device).
-    // blosc2: a chunk is hundreds of independent block streams, decoded in parallel on the device
-    // (k_blosc2), so the compressed chunk goes to the engine as it is; a codec the device
-    // does not decode comes back as UnsupportedOperation and is decompressed here instead.
-    if request_data.compression == Some(models::Compression::Blosc2) {
-        let vec: Vec<u8> = data.clone().into();
-        match debug_span!("operation_gpu").in_scope(|| T::execute(&request_data, vec)) {
+    // blosc2: a chunk is hundreds of independent block streams that the device decodes in parallel
+    // (k_blosc2), but a lone 4 MiB chunk still takes 1.6-1.7 ms there, and no record here
+    // shows that beating the reference's host decoder for ONE request; so a lone blosc2 request is
+    // decompressed on the host too unless the operator opts in (REDUCTIONIST_GPU_BLOSC2=1).  A codec the
+    // device does not decode comes back as UnsupportedOperation and is decompressed here instead.
+    if request_data.compression == Some(models::Compression::Blosc2) && gpu_blosc2() {
+        match debug_span!("operation_gpu").in_scope(|| operations_gpu::execute_slice(&request_data, &data, T::OP)) {
             Err(ActiveStorageError::UnsupportedOperation { .. }) => {}
             other => return other,
         }
@@ -56,9 +57,15 @@ pub fn operation_gpu<T: operation::Operation>(
         Some(c) => (host_decompressed(request_data), compression::decompress(c, &data)?),
         None => (request_data, data),
     };
-    // Bytes -> Vec<u8> without a copy, as the reference asserts (app.rs:173-181)
-    let vec: Vec<u8> = data.into();
-    debug_span!("operation_gpu").in_scope(|| T::execute(&request_data, vec))
+    // the chunk as downloaded — page-locked when the downloader filled a pinned_gpu::PinnedBuf — straight
+    // to the engine: no Bytes -> Vec conversion (zero copies, app.rs:173-181's intent)
+    debug_span!("operation_gpu").in_scope(|| operations_gpu::execute_slice(&request_data, &data, T::OP))
+}
+
+/// Lone blosc2 requests decoded on the device (opt-in: REDUCTIONIST_GPU_BLOSC2=1; see operation_gpu).
+fn gpu_blosc2() -> bool {
+    static ON: std::sync::OnceLock<bool> = std::sync::OnceLock::new();
+    *ON.get_or_init(|| std::env::var("REDUCTIONIST_GPU_BLOSC2").map(|v| v == "1").unwrap_or(false))
 }
 
 /// The request that goes to the engine with a chunk this host has already decompressed.  `compression`
@@ -86,9 +93,10 @@ pub async fn operation_handler_cbor<const OP: u32>(
     let mem_permits = state.resource_manager.memory(memory).await?;
     let data = state.chunk_store.get(&auth, &request_data, &state.resource_manager, mem_permits).await?;
     let run = move || -> Result<Bytes, ActiveStorageError> {
-        // a lone gzip / zlib chunk is inflated on the host, as in operation_gpu; blosc2 goes to the device
+        // a lone compressed chunk is decompressed on the host, as in operation_gpu (blosc2 goes to the
+        // device only with REDUCTIONIST_GPU_BLOSC2=1)
         let (request_data, data) = match request_data.compression {
-            Some(c) if c != models::Compression::Blosc2 => {
+            Some(c) if c != models::Compression::Blosc2 || !gpu_blosc2() => {
                 let d = compression::decompress(c, &data)?;
                 (host_decompressed(request_data), d)
             }

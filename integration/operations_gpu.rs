@@ -38,6 +38,11 @@ fn ctx() -> *mut RdxContext {
     CTX.get().expect("operations_gpu::init not called").0
 }
 
+/// The engine context (pinned_gpu allocates download buffers from it).
+pub fn context() -> *mut RdxContext {
+    ctx()
+}
+
 /// `Gpu<OP>` — OP: 0 count, 1 max, 2 min, 3 select, 4 sum (rdx_op).
 pub struct Gpu<const OP: u32>;
 pub type GpuCount = Gpu<0>;
@@ -46,32 +51,48 @@ pub type GpuMin = Gpu<2>;
 pub type GpuSelect = Gpu<3>;
 pub type GpuSum = Gpu<4>;
 
+/// The rdx_op code of a GPU plugin (app_gpu::operation_gpu calls execute_slice with it).
+pub trait GpuOp {
+    const OP: u32;
+}
+impl<const OP: u32> GpuOp for Gpu<OP> {
+    const OP: u32 = OP;
+}
+
 impl<const OP: u32> Operation for Gpu<OP> {
     fn execute(rd: &models::RequestData, data: Vec<u8>) -> Result<models::Response, ActiveStorageError> {
-        let req = Marshalled::new(rd, OP)?;
-        let mut res: *mut RdxResult = std::ptr::null_mut();
-        // One call, any request (compressed chunks included): the engine sizes and allocates the
-        // response in page-locked memory (include/rdx.h rdx_execute_owned).
-        let st = unsafe { rdx_execute_owned(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, &mut res) };
-        if planned_on_cpu(st) {
-            return cpu_operation::<OP>(rd, data);
-        }
-        check(st, rd.compression, rd.dtype)?;
-        let owner = Owned(res);
-        let info = unsafe { (*res).info };
-        let shape: Vec<usize> = info.shape[..info.ndim as usize].iter().map(|&s| s as usize).collect();
-        let counts: Vec<i64> = owner.counts().to_vec();
-        // the body stays in the engine's page-locked block until the HTTP response is dropped
-        let body = Bytes::from_owner(owner);
-        Ok(models::Response::new(
-            body,
-            dtype_of(info.dtype),
-            shape,
-            counts,
-            rd.option_shape_as_bytes.unwrap_or(false),
-            rd.option_count_as_bytes.unwrap_or(false),
-        ))
+        execute_slice(rd, &data, OP)
     }
+}
+
+/// The plugin's body over any byte slice: a `Vec` (the `Operation` trait), or the downloader's `Bytes`
+/// as it is — page-locked when it came from `pinned_gpu::PinnedBuf` (the engine then DMAs it without a
+/// staging copy), so `operation_gpu` never converts it to a `Vec` (that conversion would copy a
+/// non-`Vec` owner and break the reference's zero-copy assertion, app.rs:173-181).
+pub fn execute_slice(rd: &models::RequestData, data: &[u8], op: u32) -> Result<models::Response, ActiveStorageError> {
+    let req = Marshalled::new(rd, op)?;
+    let mut res: *mut RdxResult = std::ptr::null_mut();
+    // One call, any request (compressed chunks included): the engine sizes and allocates the
+    // response in page-locked memory (include/rdx.h rdx_execute_owned).
+    let st = unsafe { rdx_execute_owned(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, &mut res) };
+    if planned_on_cpu(st) {
+        return cpu_operation(rd, data, op);
+    }
+    check(st, rd.compression, rd.dtype)?;
+    let owner = Owned(res);
+    let info = unsafe { (*res).info };
+    let shape: Vec<usize> = info.shape[..info.ndim as usize].iter().map(|&s| s as usize).collect();
+    let counts: Vec<i64> = owner.counts().to_vec();
+    // the body stays in the engine's page-locked block until the HTTP response is dropped
+    let body = Bytes::from_owner(owner);
+    Ok(models::Response::new(
+        body,
+        dtype_of(info.dtype),
+        shape,
+        counts,
+        rd.option_shape_as_bytes.unwrap_or(false),
+        rd.option_count_as_bytes.unwrap_or(false),
+    ))
 }
 
 /// RDX_E_UNSUPPORTED for a reason other than the chunk's blosc2 codec: a request the reference serves
@@ -83,11 +104,12 @@ fn planned_on_cpu(st: i32) -> bool {
 
 /// The reference's synchronous path for this route, unchanged: `operation::<T>` (app.rs:163-183: the
 /// filter pipeline, validate_raw_size, then the CPU plugin of operations.rs).  `app::operation` becomes
-/// `pub(crate)` for this.
-fn cpu_operation<const OP: u32>(rd: &models::RequestData, data: Vec<u8>) -> Result<models::Response, ActiveStorageError> {
+/// `pub(crate)` for this.  Rare (see planned_on_cpu), so the one copy of the chunk
+/// into a fresh `Bytes` is of no consequence.
+fn cpu_operation(rd: &models::RequestData, data: &[u8], op: u32) -> Result<models::Response, ActiveStorageError> {
     use crate::operations;
-    let (rd, data) = (rd.clone(), Bytes::from(data));
-    match OP {
+    let (rd, data) = (rd.clone(), Bytes::copy_from_slice(data));
+    match op {
         0 => crate::app::operation::<operations::Count>(rd, data),
         1 => crate::app::operation::<operations::Max>(rd, data),
         2 => crate::app::operation::<operations::Min>(rd, data),
@@ -109,7 +131,7 @@ pub fn execute_cbor<const OP: u32>(rd: &models::RequestData, data: &[u8]) -> Res
     let st = unsafe { rdx_execute_cbor(ctx(), &req.c, data.as_ptr() as *const c_void, data.len() as u64, flags, &mut res) };
     if planned_on_cpu(st) {
         // the reference's path and its own serialisation (app.rs:31-43)
-        let response = cpu_operation::<OP>(rd, data.to_vec())?;
+        let response = cpu_operation(rd, data, OP)?;
         return Ok(Bytes::from(serde_cbor::to_vec(&models::CBORResponse::new(&response)).unwrap()));
     }
     check(st, rd.compression, rd.dtype)?;

@@ -209,7 +209,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 
 // Which loops are software pipelined (next tiles' loads issued before the current ones are folded).
 #ifndef RDX_PIPE_SUM
-#define RDX_PIPE_SUM 0   // variant builds: 1 = every sum, 2 = byte-shuffled 8-byte sums
+#define RDX_PIPE_SUM 2   // byte-shuffled 8-byte sums (f64 8 x 64 MiB: 85.0 -> 83.4 us; every sum (1): f32 slower)
 #endif
 template <typename T, int OP, bool FUSED>
 constexpr bool kPipelined = Red<T, OP>::kRank || (OP == OP_SUM && (RDX_PIPE_SUM == 1 || (RDX_PIPE_SUM == 2 && FUSED && sizeof(T) == 8)));
@@ -261,7 +261,18 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     const uint64_t kstride = 1, k0 = t_begin;
     const uint64_t nk = t_end > t_begin ? t_end - t_begin : 0;
 #endif
+#if RDX_TILE_ROT
+    // each workgroup starts its range at a different point and wraps (decorrelates the DRAM channels the
+    // workgroups of a chunk stream from at one time)
+    const uint64_t rot = nk ? ((uint64_t)b * 0x9E3779B1u) % nk : 0;
+    auto tile = [&](uint64_t k) {
+        uint64_t kk = k + rot;
+        kk -= kk >= nk ? nk : 0;
+        return va + (k0 + kk * kstride) * te;
+    };
+#else
     auto tile = [&](uint64_t k) { return va + (k0 + k * kstride) * te; };   // first element of the k-th tile
+#endif
     uint64_t k = 0;
     // Float min/max (the heaviest per-element fold) are software pipelined: the next UNR tiles'
     // loads are issued before the current UNR tiles are consumed (two register sets, alternating),

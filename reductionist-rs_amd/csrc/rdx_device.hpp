@@ -705,6 +705,10 @@ __device__ __forceinline__ void put_host_slot(uint64_t *slot, uint64_t value, in
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+template <typename T, int OP>
+__device__ __forceinline__ void write_folded(const KOut &out, uint32_t chunk, const Red<T, OP> &acc, bool fault);
+constexpr int kWaveFold = 6;   // records per lane of a wave-0 fold (nrec <= 384)
+
 // The hand-off's second half: this workgroup's records are published; elect the folder and let it fold
 // records P[0 .. nrec) in index order (deterministic) and write the chunk's response.
 //   fold_last == 0: count the arrival (8-way sharded counters, `members` workgroups per chunk); the last
@@ -731,8 +735,33 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
     Red<T, OP> acc;
     acc.init();
     uint32_t fault = 0;
+    if (nrec <= 64 * kWaveFold) {
+        // Up to 384 records (C1: 128, C3: 336): wave 0 alone folds them — lane l merges records l, l + 64,
+        // ... (all of its loads in flight at once: one round trip), then the wave butterfly; no LDS, no
+        // workgroup barrier on the folder's critical path
+        if (threadIdx.x >= 64) return;
+        uint64_t g[kWaveFold][kMaxGranules];
+#pragma unroll
+        for (int u = 0; u < kWaveFold; ++u) {
+            const uint32_t j = threadIdx.x + 64u * u;
+            if (j < nrec) load_record<T, OP>(P + (uint64_t)j * kR, g[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kWaveFold; ++u) {
+            const uint32_t j = threadIdx.x + 64u * u;
+            if (j >= nrec) continue;
+            Red<T, OP> o;
+            accept_record<T, OP>(P + (uint64_t)j * kR, g[u], o, out.epoch, fault);
+            acc.merge(o);
+        }
+        wave_reduce(acc);
+        const bool any_fault = __builtin_amdgcn_ballot_w64(fault != 0) != 0;
+        if (threadIdx.x == 0) write_folded<T, OP>(out, chunk, acc, any_fault);
+        RDX_STAMP(3);
+        return;
+    }
     // records j = tid, tid + 256, ... merged in that order; two in flight per thread, so up to 512
-    // records (C3: 336) cost one load round trip instead of one per 256
+    // records cost one load round trip instead of one per 256
     for (uint32_t j0 = threadIdx.x; j0 < nrec; j0 += 2 * kBlock) {
         const uint32_t j1 = j0 + kBlock;
         uint64_t g0[kMaxGranules] = {}, g1[kMaxGranules] = {};
@@ -748,9 +777,16 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
     }
     if (fault) s_fault = 1;   // benign race: every writer stores 1
     block_reduce(acc);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) write_folded<T, OP>(out, chunk, acc, s_fault != 0);
+    RDX_STAMP(3);
+}
+
+// The folded response of a chunk (thread 0 of the folder): its body / count / status, or its host slot.
+template <typename T, int OP>
+__device__ __forceinline__ void write_folded(const KOut &out, uint32_t chunk, const Red<T, OP> &acc, bool fault) {
+    {
         uint32_t e = (Red<T, OP>::kRank && acc.nan) ? (uint32_t)RDX_E_NAN_UNORDERED : 0u;
-        if (s_fault) e = RDX_E_DEVICE;
+        if (fault) e = RDX_E_DEVICE;
         if (out.host_slots) {
             const uint64_t v = OP == OP_COUNT ? (uint64_t)acc.cnt : (uint64_t)to_u<T>(acc.value());
             put_host_slot(reinterpret_cast<uint64_t *>(out.body) + 3 * (uint64_t)chunk, v, acc.cnt, e, out.epoch);
@@ -770,7 +806,6 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
         if (!out.fold_last)
             __hip_atomic_store(out.tickets + (uint64_t)chunk * kTicketWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    RDX_STAMP(3);
 }
 
 // Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
@@ -788,7 +823,10 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
     constexpr bool drop = false;
 #endif
     if (threadIdx.x == 0 && !drop) publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
-    if (out.fold_last && b != bpc - 1) return;   // only the folder goes on (no arrival to count)
+    if (out.fold_last && b != bpc - 1) {   // only the folder goes on (no arrival to count)
+        RDX_STAMP(2);
+        return;
+    }
     arrive_and_fold<T, OP>(out, P, chunk, bpc, bpc, b);
 }
 

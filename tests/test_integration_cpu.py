@@ -167,3 +167,19 @@ def test_shim_error_details_match_the_reference():
     assert ops.count("if planned_on_cpu(st)") == 2
     for op in ("Count", "Max", "Min", "Select", "Sum"):
         assert f"crate::app::operation::<operations::{op}>(rd, data)" in ops
+
+
+def test_pinned_download_path():
+    """§8f row 3 (s3_client.rs:215-233, chunk_downloader_http.rs:137-146): the downloader fills a page-locked
+    PinnedBuf (rdx_host_alloc / rdx_host_free) with the same one copy per body part, and operation_gpu hands
+    the Bytes to the engine as a slice — no Bytes -> Vec conversion anywhere on the GPU path."""
+    pin = (ROOT / "integration" / "pinned_gpu.rs").read_text()
+    assert "rdx_host_alloc(" in pin and "rdx_host_free(" in pin and "Bytes::from_owner(self)" in pin
+    assert "impl Drop for PinnedBuf" in pin and "impl AsRef<[u8]> for PinnedBuf" in pin
+    app = (ROOT / "integration" / "app_gpu.rs").read_text()
+    code = "\n".join(line for line in app.splitlines() if not line.strip().startswith("//"))
+    assert ".into();" not in code and "T::execute(" not in code
+    assert code.count("operations_gpu::execute_slice(&request_data, &data, T::OP)") == 2
+    ops = (ROOT / "integration" / "operations_gpu.rs").read_text()
+    assert "pub fn execute_slice(rd: &models::RequestData, data: &[u8], op: u32)" in ops
+    assert "execute_slice(rd, &data, OP)" in ops            # the Operation trait goes through it too

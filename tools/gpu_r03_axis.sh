@@ -13,3 +13,8 @@ done
 for fk in 32 128; do
   RDX_AXIS_COLS_VW=4 RDX_AXIS_COLS_WGS_PER_CU=1 RDX_AXIS_FOLD_KIB=$fk timeout -k 10 120 python -u tools/probe_axis.py > $OUT/axis_vw4_w1_fk$fk.jsonl 2>>$OUT/axis.err || exit 1
 done
+for rep in 1 2; do
+  for v in "" _p2 _rot; do
+    RDX_LIB_PATH=reductionist-rs_amd/librdx$v.so timeout -k 10 200 python -u tools/probe_f64.py > $OUT/f64${v}_$rep.jsonl 2>>$OUT/f64.err || exit 1
+  done
+done

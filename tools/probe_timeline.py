@@ -87,6 +87,13 @@ def main():
         ws.execute_device(c3, v.data_ptr(), v.numel() * 8, o8.data_ptr(), cnt.data_ptr(), None, stream.cuda_stream)
     torch.cuda.synchronize()
     res["c3_min"] = timeline(lib, (bench.C3_NSEL // 2 + 1023) // 1024, "f64")
+    # C1: f32 4 MiB contiguous sum (k_all_contig, 128 workgroups of 2 tiles)
+    v1 = torch.rand(1 << 20, device="cuda", generator=g)
+    c1 = _abi.CRequest("sum", "float32")
+    for k in range(12):
+        ws.execute_device(c1, v1.data_ptr(), 4 << 20, o8.data_ptr(), cnt.data_ptr(), None, stream.cuda_stream)
+    torch.cuda.synchronize()
+    res["c1_sum"] = timeline(lib, 128)
     print(json.dumps(res), flush=True)
 
 
