@@ -5,7 +5,7 @@ pure-Rust port of c-blosc2); its one test compresses b"hello world" with blusc i
 (compression.rs:90-110).  With no blosc2 library in this image, chunks are assembled here from the
 published c-blosc2 chunk format (README_CHUNK_FORMAT): header (16 bytes, or 32 with the extended
 blosc2 fields when flags carry both shuffle bits), bstarts, per block `typesize` split streams (or one),
-each a signed 32-bit csize followed by a BloscLZ / LZ4 / zlib stream, a raw copy (csize == stream
+each a signed 32-bit csize followed by a BloscLZ / LZ4 / Snappy / zlib stream, a raw copy (csize == stream
 size), a zero run (csize 0) or a byte run (csize = -byte, token byte 1); memcpy'ed and special-value
 chunks.  Filters run forward per block (filters[0] first): byte shuffle, bitshuffle.  The LZ encoders
 are datagen/blosc2_writer.cpp's (greedy, this repo's own), so a decoder matching these chunks is checked
@@ -41,7 +41,7 @@ def lib():
 
 
 def lz(codec: int, data: bytes, max_dist: int = 8191 + 65535) -> bytes:
-    """One BloscLZ (codec 0) / LZ4 (codec 1) stream by this repo's greedy encoder."""
+    """One BloscLZ (codec 0) / LZ4 (codec 1) / Snappy (codec 2) stream by this repo's greedy encoder."""
     cap = 2 * len(data) + 64
     out = (C.c_uint8 * cap)()
     src = C.create_string_buffer(bytes(data), max(1, len(data)))
@@ -49,7 +49,7 @@ def lz(codec: int, data: bytes, max_dist: int = 8191 + 65535) -> bytes:
     assert n >= 0
     return bytes(out)[:n]
 
-BLOSCLZ, LZ4, ZLIB, ZSTD = 0, 1, 3, 4
+BLOSCLZ, LZ4, SNAPPY, ZLIB, ZSTD = 0, 1, 2, 3, 4
 NOFILTER, SHUFFLE, BITSHUFFLE, DELTA, TRUNC = 0, 1, 2, 3, 4
 
 
@@ -80,7 +80,7 @@ def _stream(codec: int, s: bytes, mode: str) -> bytes:
         return struct.pack("<i", 0) if s[0] == 0 else struct.pack("<iB", -s[0], 1)
     if mode == "raw":
         return struct.pack("<i", n) + s
-    if codec in (BLOSCLZ, LZ4):
+    if codec in (BLOSCLZ, LZ4, SNAPPY):
         c = lz(codec, s)
     elif codec == ZLIB:
         c = zlib.compress(s, 6)

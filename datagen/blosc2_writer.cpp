@@ -127,15 +127,82 @@ std::vector<uint8_t> lz4_enc(const uint8_t *in, uint64_t n) {
     return e.v;
 }
 
+// Snappy raw block (google/snappy format_description.txt): varint length, then literals / copies.  Uses
+// every element form so a decoder sees them all: copy-1 for len 4..11 with offset < 2048, copy-2 for
+// offsets < 65536, copy-4 beyond (when `far` allows); literal lengths with 0-4 extension bytes.
+std::vector<uint8_t> snappy_enc(const uint8_t *in, uint64_t n, uint64_t max_dist) {
+    Emit e;
+    for (uint64_t v = n;;) {   // preamble
+        if (v < 128) { e.b((uint8_t)v); break; }
+        e.b((uint8_t)(v | 128));
+        v >>= 7;
+    }
+    auto lits = [&](uint64_t from, uint64_t L) {
+        while (L) {
+            const uint64_t k = L;   // one element (the format allows up to 2^32)
+            const uint64_t m = k - 1;
+            if (m < 60) e.b((uint8_t)(m << 2));
+            else {
+                const uint32_t nb = m < (1u << 8) ? 1 : m < (1u << 16) ? 2 : m < (1u << 24) ? 3 : 4;
+                e.b((uint8_t)((59 + nb) << 2));
+                for (uint32_t q = 0; q < nb; ++q) e.b((uint8_t)(m >> (8 * q)));
+            }
+            for (uint64_t q = 0; q < k; ++q) e.b(in[from + q]);
+            L -= k;
+        }
+    };
+    std::vector<int64_t> tab(1u << 14, -1);
+    uint64_t i = 0, lit0 = 0;
+    while (i + 4 <= n) {
+        const uint32_t hsh = hash4(in + i, 14);
+        const int64_t c = tab[hsh];
+        tab[hsh] = (int64_t)i;
+        uint64_t len = 0;
+        if (c >= 0 && i - (uint64_t)c <= max_dist)
+            while (i + len < n && in[c + len] == in[i + len]) ++len;
+        if (len < 4) {
+            ++i;
+            continue;
+        }
+        lits(lit0, i - lit0);
+        const uint64_t off = i - (uint64_t)c;
+        uint64_t left = len;
+        while (left) {
+            if (off < 2048 && left >= 4 && left <= 11) {
+                e.b((uint8_t)(1 | (left - 4) << 2 | (off >> 8) << 5));
+                e.b((uint8_t)off);
+                left = 0;
+            } else {
+                uint64_t k = left > 64 ? 64 : left;
+                if (left > 64 && left - 64 < 4) k = left - 4;   // keep the remainder a valid copy-1 length
+                if (off < 65536) {
+                    e.b((uint8_t)(2 | (k - 1) << 2));
+                    e.b((uint8_t)off);
+                    e.b((uint8_t)(off >> 8));
+                } else {
+                    e.b((uint8_t)(3 | (k - 1) << 2));
+                    for (int q = 0; q < 4; ++q) e.b((uint8_t)(off >> (8 * q)));
+                }
+                left -= k;
+            }
+        }
+        i += len;
+        lit0 = i;
+    }
+    lits(lit0, n - lit0);
+    return e.v;
+}
+
 }  // namespace
 
 extern "C" {
 
-// One LZ stream by this repo's encoder (codec 0 BloscLZ, 1 LZ4): returns its length, or -1 when it
-// would not fit dst_cap.  max_dist bounds BloscLZ distances (<= 8191 + 65535).
+// One LZ stream by this repo's encoder (codec 0 BloscLZ, 1 LZ4, 2 Snappy): returns its length, or -1 when
+// it would not fit dst_cap.  max_dist bounds BloscLZ (<= 8191 + 65535) and Snappy match distances.
 int64_t blosc2w_lz_compress(uint32_t codec, const uint8_t *src, uint64_t n, uint64_t max_dist, uint8_t *dst,
                                   uint64_t dst_cap) {
-    std::vector<uint8_t> v = codec == 0 ? blosclz_enc(src, n, max_dist) : lz4_enc(src, n);
+    std::vector<uint8_t> v = codec == 0 ? blosclz_enc(src, n, max_dist) : codec == 2 ? snappy_enc(src, n, max_dist)
+                                                                                     : lz4_enc(src, n);
     if (v.size() > dst_cap) return -1;
     std::memcpy(dst, v.data(), v.size());
     return (int64_t)v.size();

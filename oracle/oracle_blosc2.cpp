@@ -11,14 +11,15 @@
 //  chunk format (c-blosc2 README_CHUNK_FORMAT: 16-byte header, 32-byte extended header, bstarts,
 //  per-block streams with the 4-byte csize prefix, runs and memcpy'ed streams, special-value chunks)
 //  and codecs (BloscLZ = FastLZ level-2 token format; the LZ4 block format; zlib = RFC 1950 through
-//  oracle_inflate.cpp), and the filters' published definitions (byte shuffle per block, bitshuffle
+//  oracle_inflate.cpp; Snappy = the raw format of google/snappy format_description.txt, which blusc
+//  decodes through the `snap` crate, Cargo.lock: blusc -> snap), and the filters' published definitions (byte shuffle per block, bitshuffle
 //  = bshuf_trans_bit_elem over the first size - size % 8 elements).
 //  PARITY UNPINNED beyond the reference's own tests (compression.rs:90-143,164-175: the "hello world"
 //  round trip, which blosc stores memcpy'ed, and the invalid-header message), because no blosc2
 //  library, fixture or encoder exists here: chunks are written by this repo's own writer
 //  (datagen/blosc2_chunk.py + datagen/blosc2_writer.cpp), so decoder and writer are checked against
 //  each other and the format description only.
-//  zstd / snappy / dictionaries / delta / user-defined codecs: RDX_BLOSC2_UNSUPPORTED.
+//  zstd / dictionaries / delta / user-defined codecs: RDX_BLOSC2_UNSUPPORTED.
 // ============================================================================================
 #include "../include/rdx.h"
 
@@ -169,6 +170,60 @@ int64_t lz4_dec(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t maxout) {
     return (int64_t)op;
 }
 
+// Snappy raw block (snap::raw::Decoder::decompress): a varint preamble (<= 5 bytes) holding the decoded
+// length, which must fit the output; then elements by the tag's low 2 bits: 0 literal (length
+// (tag >> 2) + 1, or for 60..63 a 1-4 byte little-endian length - 1 after the tag), 1 copy with an 11-bit
+// offset (length 4 + ((tag >> 2) & 7), offset (tag >> 5) << 8 | next byte), 2 / 3 copies with a 2 / 4
+// byte little-endian offset (length (tag >> 2) + 1).  Offset 0, an offset past the bytes written, an
+// element overrunning the input or the preamble's length, or an end short of that length: error.
+int64_t snappy_dec(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t maxout) {
+    uint64_t ip = 0, want = 0;
+    for (int sh = 0;; sh += 7) {
+        if (ip >= n || sh > 28) return -1;
+        const uint8_t b = in[ip++];
+        if (sh == 28 && b > 15) return -1;   // beyond 32 bits
+        want |= (uint64_t)(b & 127u) << sh;
+        if (!(b & 128)) break;
+    }
+    if (want > maxout) return -1;
+    uint64_t op = 0;
+    while (ip < n) {
+        const uint32_t tag = in[ip++];
+        uint64_t len, off = 0;
+        if ((tag & 3) == 0) {
+            len = tag >> 2;
+            if (len >= 60) {
+                const uint32_t nb = (uint32_t)len - 59;
+                if (ip + nb > n) return -1;
+                len = 0;
+                for (uint32_t k = 0; k < nb; ++k) len |= (uint64_t)in[ip + k] << (8 * k);
+                ip += nb;
+            }
+            len += 1;
+            if (n - ip < len || want - op < len) return -1;
+            std::memcpy(out + op, in + ip, len);
+            op += len;
+            ip += len;
+            continue;
+        }
+        if ((tag & 3) == 1) {
+            if (ip + 1 > n) return -1;
+            len = 4 + ((tag >> 2) & 7u);
+            off = (uint64_t)(tag >> 5) << 8 | in[ip];
+            ip += 1;
+        } else {
+            const uint32_t nb = (tag & 3) == 2 ? 2 : 4;
+            if (ip + nb > n) return -1;
+            len = (tag >> 2) + 1;
+            for (uint32_t k = 0; k < nb; ++k) off |= (uint64_t)in[ip + k] << (8 * k);
+            ip += nb;
+        }
+        if (off == 0 || off > op || want - op < len) return -1;
+        for (uint64_t k = 0; k < len; ++k, ++op) out[op] = out[op - off];
+    }
+    return op == want ? (int64_t)op : -1;
+}
+
 // unshuffle (blosc shuffle.c): the first (bsize / ts) * ts bytes are ts planes; the rest copied
 void unshuffle(uint32_t ts, uint64_t bsize, const uint8_t *src, uint8_t *dst) {
     const uint64_t ne = bsize / ts;
@@ -257,8 +312,8 @@ uint64_t decompress(const uint8_t *s, uint64_t len, uint8_t *out, uint64_t cap) 
         return nbytes;
     }
     const uint32_t codec = h.flags >> 5;
-    if (codec == C_SNAPPY || codec == C_ZSTD || codec == 6) throw Fail{RDX_BLOSC2_UNSUPPORTED};
-    if (codec != C_BLOSCLZ && codec != C_LZ4 && codec != C_ZLIB) throw Fail{RDX_BLOSC2_FAILED};
+    if (codec == C_ZSTD || codec == 6) throw Fail{RDX_BLOSC2_UNSUPPORTED};
+    if (codec != C_BLOSCLZ && codec != C_LZ4 && codec != C_ZLIB && codec != C_SNAPPY) throw Fail{RDX_BLOSC2_FAILED};
     for (uint8_t f : h.filters) {
         if (f == FLT_DELTA || f > FLT_TRUNC) throw Fail{RDX_BLOSC2_UNSUPPORTED};
     }
@@ -296,6 +351,7 @@ uint64_t decompress(const uint8_t *s, uint64_t len, uint8_t *out, uint64_t cap) 
                     int64_t got = -1;
                     if (codec == C_BLOSCLZ) got = blosclz_dec(s + pos, (uint64_t)cb, d, neblock);
                     else if (codec == C_LZ4) got = lz4_dec(s + pos, (uint64_t)cb, d, neblock);
+                    else if (codec == C_SNAPPY) got = snappy_dec(s + pos, (uint64_t)cb, d, neblock);
                     else {
                         uint64_t ol = 0;
                         const uint32_t e = oracle_decompress(RDX_COMPRESSION_ZLIB, s + pos, (uint64_t)cb, d, neblock, &ol);

@@ -10,7 +10,7 @@
 //                    waves).  Every wave parses the header itself (no host round trip for a
 //                    device-resident chunk) and validates it exactly as the oracle does, so all waves
 //                    agree on a header-level error.  A stream is a zero run, a byte run, a raw copy or
-//                    a BloscLZ / LZ4 stream.  LZ decoding is wave-uniform serial control (token fields
+//                    a BloscLZ / LZ4 / Snappy stream.  LZ decoding is wave-uniform serial control (token fields
 //                    made scalar with readfirstlane) over an LDS input ring (1 KiB units, the next unit
 //                    prefetched into registers) and an LDS output ring holding the recent window;
 //                    literal runs and matches move 64 bytes per step, one per lane (a match of
@@ -26,7 +26,7 @@
 // zlib-coded streams are not decoded here: each becomes a row of a stream table (source, length,
 // destination, expected size) that k_inflate decodes in the next launch, k_blosc2_zcheck folds their
 // results into the chunks' errors, then k_blosc2_filter runs.
-// Unsupported here (RDX_BLOSC2_UNSUPPORTED, as the oracle): zstd, snappy, dictionaries, delta,
+// Unsupported here (RDX_BLOSC2_UNSUPPORTED, as the oracle): zstd, dictionaries, delta,
 // user-defined codecs / filters (and more than 512 zlib-coded streams per chunk of a batch).
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
@@ -135,11 +135,11 @@ __device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap, bool zlib) 
     h.mode = M_BLOCKS;
     h.codec = h.flags >> 5;
     // zlib-coded streams go to k_inflate through the stream table (refused when the caller gave none)
-    if (h.codec == 2 || h.codec == 4 || h.codec == 6 || (h.codec == 3 && !zlib)) {
+    if (h.codec == 4 || h.codec == 6 || (h.codec == 3 && !zlib)) {
         h.code = RDX_BLOSC2_UNSUPPORTED;
         return h;
     }
-    if (h.codec > 1 && h.codec != 3) { h.code = RDX_BLOSC2_FAILED; return h; }
+    if (h.codec > 3) { h.code = RDX_BLOSC2_FAILED; return h; }
     for (int k = 0; k < 6; ++k)
         if (f[k] == 3 || f[k] > 4) { h.code = RDX_BLOSC2_UNSUPPORTED; return h; }
     h.filt = 0;
@@ -401,6 +401,67 @@ struct LzStream {
         }
         return true;
     }
+
+    // Snappy raw block (oracle_blosc2.cpp snappy_dec): varint preamble = the decoded length (must be n:
+    // a shorter one is the caller's size error, a longer one does not fit), then tagged elements; every
+    // element's fields sit in the tag's 8-byte window (one LDS trip per element).
+    __device__ bool snappy(uint32_t ip) {
+        uint32_t want = 0;
+        {
+            const uint64_t w = peek8(ip);
+            uint32_t k = 0;
+            for (;; ++k) {
+                if (k == 5 || ip + k >= end) return false;
+                const uint32_t b = (uint32_t)(w >> (8 * k)) & 255u;
+                if (k == 4 && b > 15) return false;
+                want |= (b & 127u) << (7 * k);
+                if (!(b & 128)) break;
+            }
+            ip += k + 1;
+        }
+        if (want > n) return false;
+        while (ip < end) {
+            const uint64_t w = peek8(ip);
+            const uint32_t tag = (uint32_t)(w & 255u);
+            uint32_t len, off;
+            if ((tag & 3) == 0) {
+                len = tag >> 2;
+                uint32_t hb = 1;
+                if (len >= 60) {
+                    const uint32_t nb = len - 59;
+                    if (ip + 1 + nb > end) return false;
+                    len = (uint32_t)(w >> 8) & (nb == 4 ? 0xffffffffu : (1u << (8 * nb)) - 1);
+                    if (len == 0xffffffffu) return false;
+                    hb += nb;
+                }
+                len += 1;
+                ip += hb;
+                if (end - ip < len || want - op < len) return false;
+                literals(ip, len);
+                ip += len;
+                continue;
+            }
+            if ((tag & 3) == 1) {
+                if (ip + 2 > end) return false;
+                len = 4 + ((tag >> 2) & 7u);
+                off = (tag >> 5) << 8 | ((uint32_t)(w >> 8) & 255u);
+                ip += 2;
+            } else if ((tag & 3) == 2) {
+                if (ip + 3 > end) return false;
+                len = (tag >> 2) + 1;
+                off = (uint32_t)(w >> 8) & 0xffffu;
+                ip += 3;
+            } else {
+                if (ip + 5 > end) return false;
+                len = (tag >> 2) + 1;
+                off = (uint32_t)(w >> 8);
+                ip += 5;
+            }
+            if (off == 0 || off > op || want - op < len) return false;
+            match(len, off);
+        }
+        return op == want;
+    }
 };
 
 }  // namespace
@@ -505,7 +566,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args
             z.op = z.flushed = 0;
             z.load_unit(0);
             z.stage();
-            const bool ok = h.codec == 0 ? z.blosclz(skew) : z.lz4(skew);
+            const bool ok = h.codec == 0 ? z.blosclz(skew) : h.codec == 1 ? z.lz4(skew) : z.snappy(skew);
             if (!ok || z.op != neblock) { fail(err, RDX_BLOSC2_FAILED); return; }
             z.finish();
         }

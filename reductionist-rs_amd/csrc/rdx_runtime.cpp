@@ -62,7 +62,7 @@ struct Tuning {
     int axis_rows_waves = env_int("RDX_AXIS_ROWS_WAVES_PER_CU", 16);   // sliced-rows fill target
     int axis_cols_wgs = env_int("RDX_AXIS_COLS_WGS_PER_CU", 4);        // sliced-cols fill target
     int axis_cols_vw = env_int("RDX_AXIS_COLS_VW", 0);                 // tuning only: force the cols lane width
-    int axis_cols_w = env_int("RDX_AXIS_COLS_W", 0);                   // tuning only: cap the lanes per tile row
+    int axis_cols_w = env_int("RDX_AXIS_COLS_W", 32);                  // cap on the lanes per tile row (0: none)
     int axis_fold_kib = env_int("RDX_AXIS_FOLD_KIB", 64);              // cols fold bytes per tile (x2 with >= 8 streams)
     int axis_fold_sep = env_int("RDX_AXIS_FOLD_SEP", -1);              // cols fold launch: -1 auto, 0 off, 1 on
 #if RDX_PROBES
@@ -501,6 +501,10 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                     const uint64_t nkv = a.n_out / vw;
                     uint32_t W = 64;
                     while (W > 1 && W / 2 >= nkv) W /= 2;
+                    // at most 32 lanes per row of a tile: narrower tiles need fewer slices to fill the chip,
+                    // so fewer slice records and a shorter fold ([4096,4096] f32 axis 0: 21.5 -> 18.7 us,
+                    // [64,1024,256] axis 1: 18.9 -> 17.9 us; W 16 / 8 / 4 no better or slower:
+                    // profiles/r03_axis_cols_sweep.jsonl)
                     if (tuning().axis_cols_w) W = std::min<uint32_t>(W, (uint32_t)tuning().axis_cols_w);
                     const uint64_t tiles = (nkv + W - 1) / W, G = kBlock / W, R = 64 / W;
                     const uint64_t fold = (uint64_t)tuning().axis_fold_kib * 1024;

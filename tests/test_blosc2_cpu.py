@@ -51,7 +51,7 @@ def test_reference_hello_world_and_invalid():
 
 
 CASES = list(itertools.product(
-    [B.BLOSCLZ, B.LZ4, B.ZLIB],                                   # codec
+    [B.BLOSCLZ, B.LZ4, B.SNAPPY, B.ZLIB],                         # codec
     [1, 4, 8],                                                    # typesize
     [None, 1000, 16384],                                          # blocksize (None: 64 KiB)
     [True, False],                                                # split streams
@@ -179,3 +179,50 @@ def test_version2_bitshuffle_leftover_rule():
         c3 = bytes([3]) + c[1:]
         e3, d3 = oracle.blosc2_decompress(c3)
         assert e3 == 0 and d3 != d and d3[-4:] == d[-4:]
+
+
+SNAPPY_BAD = [bytes([20, 0x0C]) + b"abcd" + bytes([0x11, 0, 0x11, 4]),    # offset 0
+              bytes([20, 0x0C]) + b"abcd" + bytes([0x11, 5, 0x11, 4]),    # offset past the output
+              bytes([21, 0x0C]) + b"abcd" + bytes([0x11, 4, 0x11, 4]),    # preamble longer than the elements
+              bytes([19, 0x0C]) + b"abcd" + bytes([0x11, 4, 0x11, 4]),    # elements overrun the preamble
+              bytes([20, 0x0C]) + b"abc",                                 # truncated literal
+              bytes([20, 0x0C]) + b"abcd" + bytes([0x11, 4, 0x11]),       # truncated copy
+              bytes([20, 0x0C]) + b"abcd" + bytes([0x3F, 4, 0, 0]),       # truncated copy-4
+              bytes([0x94, 0x80, 0x80, 0x80, 0x80, 0x00]) + b"abcd"]     # 6-byte varint
+
+
+def snappy_chunk(stream: bytes, nbytes: int) -> bytes:
+    """One block, one stream (typesize 1), codec Snappy, no filter: the stream wrapped in a chunk."""
+    base = 32 + 4
+    body = struct.pack("<i", len(stream)) + stream
+    h = struct.pack("<BBBBiii", 5, 1, 0x05 | (B.SNAPPY << 5) | 0x10, 1, nbytes, nbytes, base + len(body))
+    h += bytes(6) + bytes([0, 0]) + bytes(6) + bytes([0, 0])
+    return h + struct.pack("<i", base) + body
+
+
+def test_snappy_element_forms_and_errors():
+    """Snappy (codec 2; blusc -> the snap crate, raw format of google/snappy format_description.txt).
+    A hand-assembled known answer from the format description, each element form, and malformed streams
+    (zero / too-far offsets, preamble mismatches, truncation) -> "failed to decompress blosc2 data"."""
+    F = _abi.BLOSC2_FAILED
+    want = b"abcd" * 5
+    # varint 20; literal "abcd" (tag 3 << 2); two copy-1 of len 8 offset 4 (tag 1 | 4 << 2, offset byte)
+    kat = bytes([20, 0x0C]) + b"abcd" + bytes([0x11, 4, 0x11, 4])
+    assert oracle.blosc2_decompress(snappy_chunk(kat, 20)) == (0, want)
+    # copy-2 (len 16 = (15 << 2) | 2, offset 4 LE16) and copy-4 (LE32) give the same bytes
+    for tail in (bytes([0x3E, 4, 0]), bytes([0x3F, 4, 0, 0, 0])):
+        assert oracle.blosc2_decompress(snappy_chunk(bytes([20, 0x0C]) + b"abcd" + tail, 20)) == (0, want)
+    # a literal with a 1-byte length extension (tag 60 << 2, length - 1 = 99), then a copy
+    lit = bytes(range(100))
+    assert oracle.blosc2_decompress(snappy_chunk(bytes([150, 1, 60 << 2, 99]) + lit + bytes([0xC6, 100, 0]), 150)) == \
+        (0, lit + lit[:50])
+    for stream in SNAPPY_BAD:
+        assert oracle.blosc2_decompress(snappy_chunk(stream, 20))[0] == F, stream.hex()
+    # this repo's encoder: far copies (copy-4 beyond 64 KiB), long literals (2-3 extension bytes)
+    rng = np.random.default_rng(21)
+    motif = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    d = motif + rng.integers(0, 256, 300, dtype=np.uint8).tobytes() + motif
+    st = B.lz(B.SNAPPY, d, max_dist=1 << 30)
+    assert any(st[i] & 3 == 3 for i in range(len(st)))   # (loose: some byte looks like a copy-4 tag)
+    c = B.build(d, 1, len(d), B.SNAPPY, (0,) * 6, memcpyed=False)
+    assert oracle.blosc2_decompress(c) == (0, d)

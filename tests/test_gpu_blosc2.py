@@ -65,7 +65,7 @@ def test_batch_every_layout_matches_oracle(torch, workspace, kind, skew):
     for n in (1, 13, 4096, 65536 + 13, 200000):
         d = payload(rng, n, kind)
         for codec, ts, bs, split, filt, ver in itertools.product(
-                [B.BLOSCLZ, B.LZ4, B.ZLIB], [1, 4, 8], [None, 1000, 16384], [True, False],
+                [B.BLOSCLZ, B.LZ4, B.SNAPPY, B.ZLIB], [1, 4, 8], [None, 1000, 16384], [True, False],
                 [(0,) * 6, (0, 0, 0, 0, 0, B.SHUFFLE), (0, 0, 0, 0, 0, B.BITSHUFFLE),
                  (0, 0, 0, 0, B.SHUFFLE, B.BITSHUFFLE)], [5, 2]):
             if ver == 2 and filt.count(0) < 5:
@@ -91,7 +91,8 @@ def test_lone_4mib_chunks_match(torch, workspace):
     for codec, bs, filt in ((B.BLOSCLZ, 1 << 16, (0, 0, 0, 0, 0, B.SHUFFLE)),
                             (B.LZ4, 1 << 18, (0, 0, 0, 0, 0, B.SHUFFLE)),
                             (B.LZ4, 1 << 17, (0, 0, 0, 0, 0, B.BITSHUFFLE)),
-                            (B.BLOSCLZ, 1 << 15, (0,) * 6)):
+                            (B.BLOSCLZ, 1 << 15, (0,) * 6),
+                            (B.SNAPPY, 1 << 16, (0, 0, 0, 0, 0, B.SHUFFLE))):
         c = B.build(d, 4, bs, codec, filt, memcpyed=False)
         [(e, out)] = device_blosc2(torch, workspace, [c], len(d))
         assert e == 0 and out == d, (codec, bs, filt, e)
@@ -104,7 +105,7 @@ def test_far_matches_and_long_runs(torch, workspace):
     motif = rng.integers(0, 256, 20000, dtype=np.uint8).tobytes()
     noise = rng.integers(0, 256, 30000, dtype=np.uint8).tobytes()
     d = motif + noise + motif + bytes(40000) + motif[:9000] + noise[:5000] + motif
-    for codec in (B.BLOSCLZ, B.LZ4):
+    for codec in (B.BLOSCLZ, B.LZ4, B.SNAPPY):
         c = B.build(d, 1, len(d), codec, (0,) * 6, memcpyed=False)
         e, ref = oracle.blosc2_decompress(c)
         assert e == 0 and ref == d
@@ -135,6 +136,22 @@ def test_errors_and_overflow_match_oracle(torch, workspace):
         assert got[i] == expected(c, cap), i
     # the capacity is short of nbytes: overflow reported, with the size the header states
     assert device_blosc2(torch, workspace, [good], 4096)[0][0] == _abi.INFLATE_OUTPUT_OVERFLOW
+    # Snappy streams: the hand-built element forms and malformed streams of test_blosc2_cpu, and random
+    # corruption of an encoder-written chunk, give the oracle's result
+    from test_blosc2_cpu import SNAPPY_BAD, snappy_chunk
+    kat = bytes([20, 0x0C]) + b"abcd"
+    sc = [snappy_chunk(kat + t, 20) for t in (bytes([0x11, 4, 0x11, 4]), bytes([0x3E, 4, 0]), bytes([0x3F, 4, 0, 0, 0]))]
+    sc += [snappy_chunk(st, 20) for st in SNAPPY_BAD]
+    sc.append(snappy_chunk(bytes([150, 1, 60 << 2, 99]) + bytes(range(100)) + bytes([0xC6, 100, 0]), 150))
+    sgood = B.build(d, 4, 16384, B.SNAPPY, memcpyed=False)
+    sc.append(sgood)
+    for k in range(20):
+        b = bytearray(sgood)
+        b[int(rng.integers(32 + 4 * 5, len(b)))] ^= int(rng.integers(1, 256))
+        sc.append(bytes(b))
+    got = device_blosc2(torch, workspace, sc, cap)
+    for i, c in enumerate(sc):
+        assert got[i] == expected(c, cap), i
 
 
 def test_execute_blosc2_requests_match_oracle(engine):
