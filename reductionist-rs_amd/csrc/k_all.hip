@@ -65,19 +65,12 @@ template <typename T, int OP, int MK, int N>
 __device__ __forceinline__ void consume_group(Red<T, OP> &r, const T (&x)[N], const KAllContig &a, uint64_t e0) {
     if constexpr (Red<T, OP>::kRank && MK == MK_NONE) {
         bool nn = false, z = false;
-        auto f = [](T p, T q) { return OP == OP_MAX ? __builtin_fmax(p, q) : __builtin_fmin(p, q); };
 #pragma unroll
         for (int m = 0; m < N; ++m) {
             nn |= x[m] != x[m];
             z |= x[m] == T(0);
-        }
-        // a tree over the group, then one dependent step on the running value (the fold is order-free):
-        // one wave per SIMD leaves nothing to hide a chain of N dependent min/max behind
-        if constexpr (N == 4) r.v = f(r.v, f(f(x[0], x[1]), f(x[2], x[3])));
-        else if constexpr (N == 2) r.v = f(r.v, f(x[0], x[1]));
-        else {
-#pragma unroll
-            for (int m = 0; m < N; ++m) r.v = f(r.v, x[m]);
+            if constexpr (OP == OP_MAX) r.v = __builtin_fmax(r.v, x[m]);
+            else r.v = __builtin_fmin(r.v, x[m]);
         }
         r.nan |= nn;
         r.cnt += N;
@@ -96,35 +89,6 @@ __device__ __forceinline__ void consume_group(Red<T, OP> &r, const T (&x)[N], co
         for (int m = 0; m < N; ++m) consume<T, OP, MK>(r, x[m], a, e0 + m);
     }
 }
-
-// f64 sums: three more Neumaier accumulators per lane beside the Red's own, element m of a group going
-// to accumulator m % 4, so that four independent compensated chains run side by side instead of one
-// chain of dependent f64 adds (one wave per SIMD: nothing else hides their latency).  Each chain is a
-// Neumaier sum, and settle() folds them into the Red with the same compensated step, so the result has
-// the accuracy of one Neumaier sum (exactly-summable data: the exact sum, as before).
-template <typename T, int OP, int MK>
-struct SumLanes {
-    static constexpr bool kOn = OP == OP_SUM && std::is_same_v<T, double> && MK == MK_NONE;
-    double s[3], c[3];
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) s[k] = c[k] = 0.0;
-    }
-    // element into accumulator `slot` (0: the Red's own)
-    __device__ __forceinline__ void add(Red<T, OP> &r, int slot, double x) {
-        if (slot == 0) Red<T, OP>::neumaier(r.s, r.c, x);
-        else Red<T, OP>::neumaier(s[slot - 1], c[slot - 1], x);
-    }
-    __device__ __forceinline__ void settle(Red<T, OP> &r) {
-        if constexpr (kOn) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                Red<T, OP>::neumaier(r.s, r.c, s[k]);
-                r.c += c[k];
-            }
-        }
-    }
-};
 
 // One tile step for one lane: the 16-byte granules this lane owns in tile `t`.
 //   fused   : element granule [e, e+16) with e = t*4096 + lane*16, one 16 B load per plane
@@ -163,9 +127,8 @@ __device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *bas
 }
 
 template <typename T, int OP, bool FUSED, int MK, bool FULL>
-__device__ __forceinline__ void consume_tile(Red<T, OP> &r, SumLanes<T, OP, MK> &q, const Tile<T, FUSED> &tl,
-                                             const KAllContig &a, uint64_t t0, uint64_t vb, uint32_t selA,
-                                             uint32_t selB) {
+__device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED> &tl, const KAllContig &a, uint64_t t0,
+                                             uint64_t vb, uint32_t selA, uint32_t selB) {
     using U = typename UIntOf<T>::type;
     const bool bswap = a.src.bswap;
     if constexpr (FUSED) {
@@ -204,13 +167,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, SumLanes<T, OP, MK> 
                 T xs[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) xs[m] = from_u<T>((U)(((uint64_t)hi[m] << 32) | lo[m]));
-                if constexpr (SumLanes<T, OP, MK>::kOn) {
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) q.add(r, m, (double)xs[m]);
-                    r.cnt += 4;
-                } else {
-                    consume_group<T, OP, MK, 4>(r, xs, a, e + j * 4);
-                }
+                consume_group<T, OP, MK, 4>(r, xs, a, e + j * 4);
             }
         }
     } else {
@@ -243,14 +200,8 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, SumLanes<T, OP, MK> 
                 uint64_t w[2] = {((uint64_t)tl.p[m].y << 32) | tl.p[m].x, ((uint64_t)tl.p[m].w << 32) | tl.p[m].z};
                 T xs[2];
 #pragma unroll
-                for (int k = 0; k < 2; ++k) xs[k] = from_u<T>((U)(bswap ? bswap_u(w[k]) : w[k]));
-                if constexpr (SumLanes<T, OP, MK>::kOn) {
-                    q.add(r, (2 * m) & 3, (double)xs[0]);
-                    q.add(r, (2 * m + 1) & 3, (double)xs[1]);
-                    r.cnt += 2;
-                } else {
-                    consume_group<T, OP, MK, 2>(r, xs, a, e);
-                }
+                for (int q = 0; q < 2; ++q) xs[q] = from_u<T>((U)(bswap ? bswap_u(w[q]) : w[q]));
+                consume_group<T, OP, MK, 2>(r, xs, a, e);
             }
         }
     }
@@ -275,8 +226,6 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
 
     Red<T, OP> r;
     r.init();
-    SumLanes<T, OP, MK> q;
-    q.init();
     const uint64_t lo = a.off, hi = a.off + a.n;
     // 16-byte granules: G elements per granule
     constexpr uint64_t G = FUSED ? 16 : 16 / sizeof(T);
@@ -341,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
                 for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(y[u], base, a.src.plane, tile(k + UNR + u), vb);
             }
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, q, x[u], a, tile(k + u), vb, selA, selB);
+            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
             k += UNR;
             if (!m1) break;
             const bool m2 = k + 2 * UNR <= nk;
@@ -350,7 +299,7 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
                 for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + UNR + u), vb);
             }
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, q, y[u], a, tile(k + u), vb, selA, selB);
+            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, y[u], a, tile(k + u), vb, selA, selB);
             k += UNR;
             if (!m2) break;
         }
@@ -361,20 +310,19 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + u), vb);
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, q, x[u], a, tile(k + u), vb, selA, selB);
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
     }
     }
     for (; k < nk; ++k) {
         Tile<T, FUSED> x0;
         load_tile<T, FUSED, true>(x0, base, a.src.plane, tile(k), vb);
-        consume_tile<T, OP, FUSED, MK, true>(r, q, x0, a, tile(k), vb, selA, selB);
+        consume_tile<T, OP, FUSED, MK, true>(r, x0, a, tile(k), vb, selA, selB);
     }
     if (b == 0 && va + nfull * te < vb) {
         Tile<T, FUSED> x0;
         load_tile<T, FUSED, false>(x0, base, a.src.plane, va + nfull * te, vb);
-        consume_tile<T, OP, FUSED, MK, false>(r, q, x0, a, va + nfull * te, vb, selA, selB);
+        consume_tile<T, OP, FUSED, MK, false>(r, x0, a, va + nfull * te, vb, selA, selB);
     }
-    q.settle(r);
     RDX_STAMP(1);
     finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
