@@ -5,11 +5,13 @@ pure-Rust port of c-blosc2); its one test compresses b"hello world" with blusc i
 (compression.rs:90-110).  With no blosc2 library in this image, chunks are assembled here from the
 published c-blosc2 chunk format (README_CHUNK_FORMAT): header (16 bytes, or 32 with the extended
 blosc2 fields when flags carry both shuffle bits), bstarts, per block `typesize` split streams (or one),
-each a signed 32-bit csize followed by a BloscLZ / LZ4 / Snappy / zlib stream, a raw copy (csize == stream
+each a signed 32-bit csize followed by a BloscLZ / LZ4 / Snappy / zlib / zstd stream, a raw copy (csize == stream
 size), a zero run (csize 0) or a byte run (csize = -byte, token byte 1); memcpy'ed and special-value
 chunks.  Filters run forward per block (filters[0] first): byte shuffle, bitshuffle.  The LZ encoders
-are datagen/blosc2_writer.cpp's (greedy, this repo's own), so a decoder matching these chunks is checked
-against the format description, not against c-blosc2's bytes ("parity unpinned").
+are datagen/blosc2_writer.cpp's (greedy, this repo's own); with enc="lib" the LZ4 / Snappy streams, and
+always the zstd streams, come from the real liblz4 / libsnappy / libzstd bundled with pyarrow, so the
+stream decoders are checked against the real encoders.  The chunk container itself is checked against the
+format description only, not against c-blosc2's bytes ("parity unpinned").
 """
 from __future__ import annotations
 
@@ -74,13 +76,27 @@ def bitshuffle_block(b: bytes, ts: int, version: int = 5) -> bytes:
     return rows.tobytes() + b[size * ts:]
 
 
-def _stream(codec: int, s: bytes, mode: str) -> bytes:
+def lib_stream(codec: int, data: bytes, level: int = 3) -> bytes:
+    """One stream by the REAL codec library (pyarrow's bundled liblz4 / libsnappy / libzstd): LZ4 raw block
+    (c-blosc2 lz4_wrap_compress: LZ4_compress_fast), Snappy raw (c-blosc's snappy_compress), a zstd frame
+    (c-blosc2 zstd_wrap_compress: ZSTD_compressCCtx).  These pin the stream decoders against the real
+    encoders; the chunk container around them is still this repo's writer."""
+    import pyarrow as pa
+    name = {LZ4: "lz4_raw", SNAPPY: "snappy", ZSTD: "zstd"}[codec]
+    if codec == ZSTD:
+        return pa.Codec(name, compression_level=level).compress(bytes(data), asbytes=True)
+    return pa.Codec(name).compress(bytes(data), asbytes=True)
+
+
+def _stream(codec: int, s: bytes, mode: str, enc: str = "repo") -> bytes:
     n = len(s)
     if mode == "auto" and n and s.count(s[0]) == n:
         return struct.pack("<i", 0) if s[0] == 0 else struct.pack("<iB", -s[0], 1)
     if mode == "raw":
         return struct.pack("<i", n) + s
-    if codec in (BLOSCLZ, LZ4, SNAPPY):
+    if codec == ZSTD or (enc == "lib" and codec in (LZ4, SNAPPY)):
+        c = lib_stream(codec, s) if n else b""
+    elif codec in (BLOSCLZ, LZ4, SNAPPY):
         c = lz(codec, s)
     elif codec == ZLIB:
         c = zlib.compress(s, 6)
@@ -93,9 +109,10 @@ def _stream(codec: int, s: bytes, mode: str) -> bytes:
 
 def build(data: bytes, typesize: int = 4, blocksize: int | None = None, codec: int = BLOSCLZ,
           filters=(0, 0, 0, 0, 0, SHUFFLE), split: bool = True, version: int = 5, memcpyed: bool | None = None,
-          stream_mode: str = "auto", b2flags: int = 0) -> bytes:
+          stream_mode: str = "auto", b2flags: int = 0, enc: str = "repo") -> bytes:
     """One chunk.  version 5: extended 32-byte header with the filter pipeline; version 2: the 16-byte
-    blosc1 header (filters from the flag bits).  memcpyed None: only when compressing does not pay."""
+    blosc1 header (filters from the flag bits).  memcpyed None: only when compressing does not pay.
+    enc "lib": LZ4 / Snappy streams by the real libraries (lib_stream); zstd streams always are."""
     nbytes = len(data)
     if blocksize is None:
         blocksize = min(nbytes, 64 * 1024) or 1
@@ -137,7 +154,7 @@ def build(data: bytes, typesize: int = 4, blocksize: int | None = None, codec: i
         ne = len(blk) // ns
         bstarts.append(base + len(body))
         for k in range(ns):
-            body += _stream(codec, blk[k * ne:(k + 1) * ne], stream_mode)
+            body += _stream(codec, blk[k * ne:(k + 1) * ne], stream_mode, enc)
     cbytes = base + len(body)
     if memcpyed is None:
         memcpyed = cbytes >= nbytes + overhead

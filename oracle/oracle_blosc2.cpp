@@ -12,14 +12,14 @@
 //  per-block streams with the 4-byte csize prefix, runs and memcpy'ed streams, special-value chunks)
 //  and codecs (BloscLZ = FastLZ level-2 token format; the LZ4 block format; zlib = RFC 1950 through
 //  oracle_inflate.cpp; Snappy = the raw format of google/snappy format_description.txt, which blusc
-//  decodes through the `snap` crate, Cargo.lock: blusc -> snap), and the filters' published definitions (byte shuffle per block, bitshuffle
+//  decodes through the `snap` crate, Cargo.lock: blusc -> snap; zstd frames through oracle_zstd.cpp), and the filters' published definitions (byte shuffle per block, bitshuffle
 //  = bshuf_trans_bit_elem over the first size - size % 8 elements).
 //  PARITY UNPINNED beyond the reference's own tests (compression.rs:90-143,164-175: the "hello world"
 //  round trip, which blosc stores memcpy'ed, and the invalid-header message), because no blosc2
 //  library, fixture or encoder exists here: chunks are written by this repo's own writer
 //  (datagen/blosc2_chunk.py + datagen/blosc2_writer.cpp), so decoder and writer are checked against
 //  each other and the format description only.
-//  zstd / dictionaries / delta / user-defined codecs: RDX_BLOSC2_UNSUPPORTED.
+//  dictionaries / delta / user-defined codecs: RDX_BLOSC2_UNSUPPORTED.
 // ============================================================================================
 #include "../include/rdx.h"
 
@@ -27,6 +27,7 @@
 #include <cstring>
 #include <vector>
 
+extern "C" int oracle_zstd_decompress(const uint8_t *src, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
 extern "C" uint32_t oracle_decompress(uint32_t compression, const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap,
                                       uint64_t *out_len);
 
@@ -312,8 +313,8 @@ uint64_t decompress(const uint8_t *s, uint64_t len, uint8_t *out, uint64_t cap) 
         return nbytes;
     }
     const uint32_t codec = h.flags >> 5;
-    if (codec == C_ZSTD || codec == 6) throw Fail{RDX_BLOSC2_UNSUPPORTED};
-    if (codec != C_BLOSCLZ && codec != C_LZ4 && codec != C_ZLIB && codec != C_SNAPPY) throw Fail{RDX_BLOSC2_FAILED};
+    if (codec == 6) throw Fail{RDX_BLOSC2_UNSUPPORTED};   // BLOSC_CODEC_USER_DEFINED
+    if (codec > C_ZSTD) throw Fail{RDX_BLOSC2_FAILED};
     for (uint8_t f : h.filters) {
         if (f == FLT_DELTA || f > FLT_TRUNC) throw Fail{RDX_BLOSC2_UNSUPPORTED};
     }
@@ -352,6 +353,10 @@ uint64_t decompress(const uint8_t *s, uint64_t len, uint8_t *out, uint64_t cap) 
                     if (codec == C_BLOSCLZ) got = blosclz_dec(s + pos, (uint64_t)cb, d, neblock);
                     else if (codec == C_LZ4) got = lz4_dec(s + pos, (uint64_t)cb, d, neblock);
                     else if (codec == C_SNAPPY) got = snappy_dec(s + pos, (uint64_t)cb, d, neblock);
+                    else if (codec == C_ZSTD) {   // zstd_wrap_decompress: ZSTD_decompressDCtx, capacity neblock
+                        uint64_t ol = 0;
+                        got = oracle_zstd_decompress(s + pos, (uint64_t)cb, d, neblock, &ol) == 0 ? (int64_t)ol : -1;
+                    }
                     else {
                         uint64_t ol = 0;
                         const uint32_t e = oracle_decompress(RDX_COMPRESSION_ZLIB, s + pos, (uint64_t)cb, d, neblock, &ol);

@@ -43,6 +43,10 @@ def lib():
         L.oracle_inflate_last_error.argtypes = []
         L.oracle_blosc2_sizes.restype = None
         L.oracle_blosc2_sizes.argtypes = [VP, U64, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]
+        L.oracle_zstd_decompress.restype = C.c_int
+        L.oracle_zstd_decompress.argtypes = [VP, U64, VP, U64, C.POINTER(U64)]
+        L.oracle_xxh64.restype = U64
+        L.oracle_xxh64.argtypes = [VP, U64]
         L.oracle_blosc2_decompress.restype = C.c_uint32
         L.oracle_blosc2_decompress.argtypes = [VP, U64, VP, U64, C.POINTER(U64)]
         L.oracle_missing_convert.restype = C.c_int
@@ -147,3 +151,17 @@ def blosc2_decompress(data: bytes, cap: int | None = None):
     e = lib().oracle_blosc2_decompress(src, len(data), out, cap, C.byref(got))
     return int(e), bytes(out)[: min(got.value, cap)]
 
+
+
+def zstd_decompress(data: bytes, cap: int):
+    """ZSTD_decompressDCtx restated (oracle_zstd.cpp): (0, bytes) or (-1, b"")."""
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    out = C.create_string_buffer(max(1, cap))
+    got = C.c_uint64(0)
+    e = lib().oracle_zstd_decompress(src, len(data), out, cap, C.byref(got))
+    return (e, out.raw[:got.value] if e == 0 else b"")
+
+
+def xxh64(data: bytes) -> int:
+    src = C.create_string_buffer(bytes(data), max(1, len(data)))
+    return lib().oracle_xxh64(src, len(data))

@@ -105,8 +105,11 @@ def test_error_taxonomy():
     assert oracle.blosc2_decompress(bytes(bad))[0] == I
     assert oracle.blosc2_decompress(good[:-1])[0] == F      # cbytes > length
     bad = bytearray(good)
-    bad[2] = (bad[2] & 0x1F) | (B.ZSTD << 5)               # zstd
+    bad[2] = (bad[2] & 0x1F) | (6 << 5)                    # a user-defined codec
     assert oracle.blosc2_decompress(bytes(bad))[0] == U
+    bad = bytearray(good)
+    bad[2] = (bad[2] & 0x1F) | (B.ZSTD << 5)               # BloscLZ streams read as zstd frames
+    assert oracle.blosc2_decompress(bytes(bad))[0] == F
     bad = bytearray(good)
     bad[21] = B.DELTA                                       # delta filter
     assert oracle.blosc2_decompress(bytes(bad))[0] == U

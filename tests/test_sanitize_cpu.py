@@ -11,7 +11,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 SRCS = [ROOT / "tests" / "cpp" / "test_sanitize.cpp", ROOT / "reductionist-rs_amd" / "csrc" / "rdx_plan.cpp",
-        ROOT / "oracle" / "rdx_oracle.cpp", ROOT / "oracle" / "oracle_inflate.cpp", ROOT / "oracle" / "oracle_blosc2.cpp"]
+        ROOT / "oracle" / "rdx_oracle.cpp", ROOT / "oracle" / "oracle_inflate.cpp", ROOT / "oracle" / "oracle_blosc2.cpp",
+        ROOT / "oracle" / "oracle_zstd.cpp"]
 DEPS = SRCS + [ROOT / "include" / "rdx.h", ROOT / "reductionist-rs_amd" / "csrc" / "rdx_plan.hpp",
                ROOT / "reductionist-rs_amd" / "csrc" / "rdx_kdesc.h"]
 
