@@ -357,7 +357,7 @@ pub fn check(st: i32, compression: Option<Compression>, dtype: DType) -> Result<
         E_SHUFFLE_LENGTH => panic!("assertion `left == right` failed"),
         // operations.rs:181-183,355-357: NaN in a min/max comparison panics in the reference; parity
         E_NAN_UNORDERED => panic!("unexpected undefined order error for min"),
-        // a blosc2 codec / filter the device does not decode (zstd, dictionaries, delta):
+        // a blosc2 codec / filter the device does not decode (dictionaries, delta, checksummed zstd frames):
         // app_gpu::operation_gpu catches this variant and decompresses on the host instead.  The other
         // reasons never get here: Gpu<OP> serves them on the reference CPU path (planned_on_cpu).
         E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 codec on the GPU".into() }),

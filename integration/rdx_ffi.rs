@@ -64,7 +64,7 @@ pub mod blosc2 {
     pub const INVALID: u32 = 12;      // "invalid blosc2 compressed data"
     pub const FAILED: u32 = 13;       // "failed to decompress blosc2 data"
     pub const SIZE: u32 = 14;         // "unexpected decompressed size for blosc2 data"
-    pub const UNSUPPORTED: u32 = 15;  // zstd / dictionaries / delta: host fallback
+    pub const UNSUPPORTED: u32 = 15;  // dictionaries / delta / checksummed zstd: host fallback
 }
 
 /// rdx_unsupported_reason (include/rdx.h): why the last RDX_E_UNSUPPORTED of this thread was returned.

@@ -26,8 +26,9 @@
 // zlib-coded streams are not decoded here: each becomes a row of a stream table (source, length,
 // destination, expected size) that k_inflate decodes in the next launch, k_blosc2_zcheck folds their
 // results into the chunks' errors, then k_blosc2_filter runs.
-// Unsupported here (RDX_BLOSC2_UNSUPPORTED, as the oracle): zstd, dictionaries, delta,
-// user-defined codecs / filters (and more than 512 zlib-coded streams per chunk of a batch).
+// zstd-coded streams go through the same table (its second half) to k_blosc2_zstd (below).
+// Unsupported here (RDX_BLOSC2_UNSUPPORTED): dictionaries, delta, user-defined codecs / filters, zstd
+// frames with a content checksum, more than 512 zlib- or zstd-coded streams per chunk of a batch.
 #include "rdx_device.hpp"
 #include "rdx_kernels.hpp"
 
@@ -135,11 +136,11 @@ __device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap, bool zlib) 
     h.mode = M_BLOCKS;
     h.codec = h.flags >> 5;
     // zlib-coded streams go to k_inflate through the stream table (refused when the caller gave none)
-    if (h.codec == 4 || h.codec == 6 || (h.codec == 3 && !zlib)) {
+    if (h.codec == 6 || ((h.codec == 3 || h.codec == 4) && !zlib)) {
         h.code = RDX_BLOSC2_UNSUPPORTED;
         return h;
     }
-    if (h.codec > 3) { h.code = RDX_BLOSC2_FAILED; return h; }
+    if (h.codec > 4) { h.code = RDX_BLOSC2_FAILED; return h; }
     for (int k = 0; k < 6; ++k)
         if (f[k] == 3 || f[k] > 4) { h.code = RDX_BLOSC2_UNSUPPORTED; return h; }
     h.filt = 0;
@@ -301,6 +302,27 @@ struct LzStream {
     }
     __device__ void finish() {
         while (op > flushed) flush(op - flushed < kFlush ? (uint32_t)(op - flushed) : kFlush);
+    }
+    // stage a new source (zstd: raw literals in the input, or decoded literals in HBM): `avail` bytes at p;
+    // returns the aligned-coordinate position of p's first byte (the ip literals() takes)
+    __device__ uint32_t source(const uint8_t *p, uint32_t avail) {
+        const uint32_t skew = (uint32_t)((uintptr_t)p & 3);
+        srcw = reinterpret_cast<const uint32_t *>(p - skew);
+        end = skew + avail;
+        staged = 0;
+        load_unit(0);
+        stage();
+        return skew;
+    }
+    // len copies of byte b (zstd RLE blocks)
+    __device__ void run(uint8_t b, uint32_t len) {
+        for (uint32_t s = 0; s < len; s += 64) {
+            room();
+            const uint32_t k = len - s < 64 ? len - s : 64;
+            if (lane < k) L.win[(op + lane) & kRingMask] = b;
+            op += k;
+            asm volatile("" ::: "memory");
+        }
     }
 
     // blosclz_decompress (oracle_blosc2.cpp blosclz_dec); returns false on a malformed stream
@@ -464,6 +486,638 @@ struct LzStream {
     }
 };
 
+// ---- zstd (codec 4): RFC 8878, restated from oracle/oracle_zstd.cpp -------------------------------------
+// One wavefront per zstd-coded stream (a row of the stream table, rows [z_capacity, z_capacity + count)),
+// in its own launch (k_blosc2_zstd) with its own LDS: the decode tables beside the output ring.  Control
+// is wave-uniform scalar code; the compressed bytes are read through 256-byte windows held one dword per
+// lane (v_readlane extracts the dword a bit read needs; a window reload is one coalesced load), so no bit
+// read waits on memory except at a window boundary.  Literals are Huffman-decoded into the tail of the
+// stream's own output region (bytes the sequences have not reached yet: the write position never passes the
+// read position) and copied from there by the sequences through LzStream's staged input ring; matches use
+// LzStream's LDS window / flushed-output reads.  Frames with a content checksum are not decoded here
+// (RDX_BLOSC2_UNSUPPORTED: the host decodes that chunk); neither are dictionaries (a failure, as libzstd).
+constexpr uint32_t kZHufMax = 11;   // Max_Number_of_Bits
+
+struct __attribute__((aligned(16))) ZLds {
+    WaveLds w;                                   // output ring + staged literal source
+    uint32_t ll[512], of[256], ml[512];          // FSE decode entries: symbol | nb << 8 | base << 16
+    uint32_t wt[64];                             // the FSE table of the Huffman weights (accuracy <= 6)
+    uint16_t huf[1 << kZHufMax];                 // Huffman: symbol | nb << 8
+};
+
+__constant__ int16_t kZLLDef[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1,
+                                    -1, -1, -1, -1};
+__constant__ int16_t kZMLDef[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int16_t kZOFDef[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+__constant__ uint32_t kZLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,  12,   13,   14,   15,   16,    18,
+                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+__constant__ uint8_t kZLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t kZMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12,  13,  14,  15,  16,   17,   18,   19,   20,
+                                      21, 22, 23, 24, 25, 26, 27, 28, 29, 30,  31,  32,  33,  34,   35,   37,   39,   41,
+                                      43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+__constant__ uint8_t kZMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                     0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+
+__device__ __forceinline__ uint32_t zhibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+
+// 64 dwords of a byte range, one per lane; bit reads take their dwords with v_readlane (uniform index)
+struct ZWin {
+    const uint32_t *w;
+    uint32_t nw, lane;
+    int32_t wd0;
+    uint32_t v;
+    __device__ void load(int32_t d0) {
+        wd0 = d0;
+        const int32_t d = d0 + (int32_t)lane;
+        v = (d >= 0 && (uint32_t)d < nw) ? gld<uint32_t>(w + d) : 0u;
+    }
+    __device__ __forceinline__ uint32_t dw(int32_t d, bool back) {
+        if (d < wd0 || d >= wd0 + 64) load(back ? (d > 61 ? d - 61 : 0) : d);
+        return __builtin_amdgcn_readlane(v, (int)rfl((uint32_t)(d - wd0)));
+    }
+};
+
+// Bits of a byte range [p, p + n): forward (FSE descriptions, header bytes) or backward (RFC 8878 §4.1
+// bitstreams: from the end, the last byte's highest set bit is padding; bits below the start read as 0
+// and `off` goes negative, which the callers check).
+struct ZBits {
+    ZWin win;
+    uint32_t sb;       // skew bits
+    uint64_t nbytes;
+    int64_t off;       // backward: bits left; forward: next bit
+    __device__ void setup(const uint8_t *p, uint64_t n, uint32_t lane) {
+        const uint32_t skew = (uint32_t)((uintptr_t)p & 3);
+        win.w = reinterpret_cast<const uint32_t *>(p - skew);
+        win.nw = (uint32_t)((skew + n + 3) / 4);
+        win.lane = lane;
+        win.wd0 = -1000;
+        win.v = 0;
+        sb = 8 * skew;
+        nbytes = n;
+        off = 0;
+    }
+    // k (<= 32) bits at relative bit position r (>= 0)
+    __device__ __forceinline__ uint32_t at(uint64_t r, uint32_t k, bool back) {
+        const uint64_t a = sb + r;
+        const int32_t d = (int32_t)(a >> 5);
+        const uint32_t sh = (uint32_t)(a & 31);
+        uint32_t v = win.dw(d, back) >> sh;
+        if (sh + k > 32) v |= win.dw(d + 1, back) << (32 - sh);
+        return k >= 32 ? v : v & ((1u << k) - 1);
+    }
+    __device__ __forceinline__ uint32_t byte(uint64_t i) { return at(8 * i, 8, false); }
+    __device__ bool init_back(const uint8_t *p, uint64_t n, uint32_t lane) {
+        setup(p, n, lane);
+        if (n == 0) return false;
+        const uint32_t last = at(8 * (n - 1), 8, true);
+        if (last == 0) return false;
+        off = (int64_t)(8 * n) - (int64_t)(8 - zhibit(last));
+        return true;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t k) {   // backward, k <= 32
+        if (k == 0) return 0;
+        off -= k;
+        if (off >= 0) return at((uint64_t)off, k, true);
+        const int64_t avail = (int64_t)k + off;
+        if (avail <= 0) return 0;
+        return at(0, (uint32_t)avail, true) << (uint32_t)(-off);
+    }
+    __device__ __forceinline__ uint32_t fwd(uint32_t k, bool &ok) {   // forward, k <= 25
+        if ((uint64_t)off + k > 8 * nbytes) {
+            ok = false;
+            return 0;
+        }
+        const uint32_t v = at((uint64_t)off, k, false);
+        off += k;
+        return v;
+    }
+};
+
+struct ZDec {
+    ZLds &Z;
+    LzStream &z;
+    const uint32_t lane;
+    bool have_huf = false, have_ll = false, have_of = false, have_ml = false;
+    uint32_t huf_bits = 0, ll_log = 0, of_log = 0, ml_log = 0;
+    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+
+    // FSE decode table from a per-lane distribution (lane s: symbol s's normalised count; nsym <= 64):
+    // the spread by one lane's LDS stores, then the states' bits / baselines in order with the per-symbol
+    // counters in a VGPR (lane s), entries assembled in VGPRs and stored coalesced.
+    __device__ bool fse_build(uint32_t *tab, int freq_v, uint32_t nsym, uint32_t log) {
+        const uint32_t size = 1u << log;
+        uint32_t high = size;
+        for (uint32_t s = 0; s < nsym; ++s) {
+            if ((int)__builtin_amdgcn_readlane(freq_v, (int)s) == -1) {
+                --high;
+                if (lane == 0) tab[high] = s;
+            }
+        }
+        const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+        uint32_t pos = 0;
+        for (uint32_t s = 0; s < nsym; ++s) {
+            const int f = (int)__builtin_amdgcn_readlane(freq_v, (int)s);
+            for (int i = 0; i < f; ++i) {
+                if (lane == 0) tab[pos] = s;
+                do pos = (pos + step) & mask;
+                while (pos >= high);
+            }
+        }
+        if (pos != 0) return false;
+        wave_sync();
+        uint32_t cnt = lane < nsym ? (freq_v == -1 ? 1u : (freq_v > 0 ? (uint32_t)freq_v : 0u)) : 0u;
+        for (uint32_t j = 0; j * 64 < size; ++j) {
+            const uint32_t c = j * 64 + lane;
+            const uint32_t symv = c < size ? (tab[c] & 0xffu) : 0u;
+            uint32_t e = 0;
+            const uint32_t m = size - j * 64 < 64 ? size - j * 64 : 64;
+            for (uint32_t l = 0; l < m; ++l) {
+                const uint32_t sym = __builtin_amdgcn_readlane(symv, (int)l);
+                const uint32_t d = __builtin_amdgcn_readlane(cnt, (int)sym);
+                cnt += lane == sym ? 1u : 0u;
+                const uint32_t nb = log - zhibit(d);
+                const uint32_t base = ((d << nb) - size) & 0xffffu;
+                if (lane == l) e = sym | nb << 8 | base << 16;
+            }
+            wave_sync();
+            if (c < size) tab[c] = e;
+        }
+        wave_sync();
+        return true;
+    }
+
+    // FSE table description (forward bits at b.off); symbols <= max_sym (< 64), accuracy <= max_log.
+    __device__ bool fse_read(ZBits &b, uint32_t *tab, uint32_t max_log, uint32_t max_sym, uint32_t &log_out) {
+        bool ok = true;
+        const uint32_t log = 5 + b.fwd(4, ok);
+        if (!ok || log > max_log) return false;
+        int remaining = 1 << log;
+        int freq_v = 0;
+        uint32_t s = 0;
+        while (remaining > 0 && s <= max_sym) {
+            const uint32_t bits = zhibit((uint32_t)remaining + 1) + 1;
+            uint32_t v = b.fwd(bits, ok);
+            if (!ok) return false;
+            const uint32_t lower = (1u << (bits - 1)) - 1;
+            const uint32_t thr = (1u << bits) - 1 - ((uint32_t)remaining + 1);
+            if ((v & lower) < thr) {
+                b.off -= 1;
+                v &= lower;
+            } else if (v > lower) {
+                v -= thr;
+            }
+            const int pr = (int)v - 1;
+            remaining -= pr < 0 ? -pr : pr;
+            if (lane == s) freq_v = pr;
+            ++s;
+            if (pr == 0) {
+                uint32_t rep = b.fwd(2, ok);
+                for (;;) {
+                    if (!ok) return false;
+                    for (uint32_t i = 0; i < rep; ++i) {
+                        if (s > max_sym) return false;
+                        if (lane == s) freq_v = 0;
+                        ++s;
+                    }
+                    if (rep != 3) break;
+                    rep = b.fwd(2, ok);
+                }
+            }
+        }
+        if (remaining != 0 || s > max_sym + 1) return false;
+        b.off = (b.off + 7) & ~(int64_t)7;   // the description ends on a byte boundary
+        log_out = log;
+        return fse_build(tab, freq_v, s, log);
+    }
+
+    // Huffman tree description at stream bytes [p, p + n) -> Z.huf; returns the bytes used (0: corrupt)
+    __device__ uint32_t huf_read(const uint8_t *p, uint64_t n) {
+        ZBits h;
+        h.setup(p, n, lane);
+        if (n < 1) return 0;
+        const uint32_t hdr = h.byte(0);
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;   // weight of symbol 64k + lane in wk
+        uint32_t nw = 0, used;
+        auto put = [&](uint32_t s, uint32_t wv) {
+            const uint32_t k = s >> 6;
+            if (lane == (s & 63)) {
+                if (k == 0) w0 = wv;
+                else if (k == 1) w1 = wv;
+                else if (k == 2) w2 = wv;
+                else w3 = wv;
+            }
+        };
+        if (hdr >= 128) {
+            nw = hdr - 127;
+            const uint32_t bytes = (nw + 1) / 2;
+            if (1 + bytes > n) return 0;
+            for (uint32_t i = 0; i < nw; ++i) {
+                const uint32_t by = h.byte(1 + i / 2);
+                put(i, (i % 2 == 0) ? by >> 4 : by & 15u);
+            }
+            used = 1 + bytes;
+        } else {
+            if (hdr == 0 || 1 + (uint64_t)hdr > n) return 0;
+            ZBits f;
+            f.setup(p + 1, hdr, lane);
+            uint32_t log = 0;
+            if (!fse_read(f, Z.wt, 6, 63, log)) return 0;
+            const uint64_t th = (uint64_t)f.off / 8;
+            if (th >= hdr) return 0;
+            ZBits b;
+            if (!b.init_back(p + 1 + th, hdr - th, lane)) return 0;
+            uint32_t s1 = b.get(log), s2 = b.get(log);
+            if (b.off < 0) return 0;
+            for (;;) {
+                uint32_t e = rfl(Z.wt[s1]);
+                if (nw >= 255) return 0;
+                put(nw++, e & 0xffu);
+                s1 = (e >> 16) + b.get((e >> 8) & 0xffu);
+                if (b.off < 0) {
+                    if (nw >= 255) return 0;
+                    put(nw++, rfl(Z.wt[s2]) & 0xffu);
+                    break;
+                }
+                e = rfl(Z.wt[s2]);
+                if (nw >= 255) return 0;
+                put(nw++, e & 0xffu);
+                s2 = (e >> 16) + b.get((e >> 8) & 0xffu);
+                if (b.off < 0) {
+                    if (nw >= 255) return 0;
+                    put(nw++, rfl(Z.wt[s1]) & 0xffu);
+                    break;
+                }
+            }
+            used = 1 + hdr;
+        }
+        // the implied last weight, Max_Number_of_Bits
+        const uint32_t ws[4] = {w0, w1, w2, w3};
+        uint32_t total = 0, bad = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t wv = (64u * k + lane) < nw ? ws[k] : 0u;
+            bad |= wv > kZHufMax;
+            uint32_t t = wv ? 1u << (wv - 1) : 0u;
+            for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m, 64);
+            total += t;
+        }
+        if (__builtin_amdgcn_ballot_w64(bad) || total == 0) return 0;
+        total = rfl(total);
+        const uint32_t maxbits = zhibit(total) + 1;
+        if (maxbits > kZHufMax) return 0;
+        const uint32_t rest = (1u << maxbits) - total;
+        if (rest & (rest - 1)) return 0;
+        put(nw++, zhibit(rest) + 1);
+        if (nw > 256) return 0;
+        // ranges by weight ascending, symbols in order: a per-weight start (lane wt) from the counts
+        uint32_t start = 0;   // lane wt: first entry of weight wt
+        {
+            uint32_t acc = 0;
+            for (uint32_t wt = 1; wt <= maxbits; ++wt) {
+                uint32_t c = 0;
+                const uint32_t ws2[4] = {w0, w1, w2, w3};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    c += __builtin_popcountll(__builtin_amdgcn_ballot_w64((64u * k + lane) < nw && ws2[k] == wt));
+                if (lane == wt) start = acc;
+                acc += c << (wt - 1);
+            }
+            if (acc != (1u << maxbits)) return 0;
+        }
+        const uint32_t wsf[4] = {w0, w1, w2, w3};
+        for (uint32_t sidx = 0; sidx < nw; ++sidx) {
+            const uint32_t k = sidx >> 6;
+            const uint32_t wv = __builtin_amdgcn_readlane(k == 0 ? wsf[0] : k == 1 ? wsf[1] : k == 2 ? wsf[2] : wsf[3],
+                                                          (int)(sidx & 63));
+            if (wv == 0) continue;
+            const uint32_t at = __builtin_amdgcn_readlane(start, (int)wv);
+            const uint32_t len = 1u << (wv - 1);
+            if (lane == wv) start += len;
+            const uint16_t ent = (uint16_t)(sidx | (maxbits + 1 - wv) << 8);
+            for (uint32_t q = lane; q < len; q += 64) Z.huf[at + q] = ent;
+        }
+        wave_sync();
+        huf_bits = maxbits;
+        have_huf = true;
+        return used;
+    }
+
+    // One Huffman stream of `count` symbols into dst[0..count) (consumed exactly)
+    __device__ bool huf_stream(const uint8_t *p, uint64_t n, uint8_t *dst, uint64_t count) {
+        ZBits b;
+        if (!b.init_back(p, n, lane)) return false;
+        const uint32_t mb = huf_bits;
+        for (uint64_t i = 0; i < count; ++i) {
+            const int64_t save = b.off;
+            const uint32_t idx = b.get(mb);
+            const uint32_t e = rfl((uint32_t)Z.huf[idx]);
+            b.off = save - (int64_t)(e >> 8);
+            if (b.off < 0) return false;
+            if (lane == 0) dst[i] = (uint8_t)e;
+        }
+        return b.off == 0;
+    }
+
+    // a sequence table: mode 0 predefined, 1 RLE, 2 FSE, 3 repeat; bytes used at p (or -1)
+    __device__ int64_t seq_table(uint32_t mode, const uint8_t *p, uint64_t n, uint32_t *tab, uint32_t &log, bool &have,
+                                 const int16_t *def, uint32_t ndef, uint32_t deflog, uint32_t maxlog, uint32_t maxsym) {
+        if (mode == 0) {
+            const int fv = lane < ndef ? (int)def[lane] : 0;
+            if (!fse_build(tab, fv, ndef, deflog)) return -1;
+            log = deflog;
+            have = true;
+            return 0;
+        }
+        if (mode == 1) {
+            if (n < 1) return -1;
+            ZBits h;
+            h.setup(p, n, lane);
+            const uint32_t sym = h.byte(0);
+            if (sym > maxsym) return -1;
+            if (lane == 0) tab[0] = sym;   // nb 0, base 0
+            wave_sync();
+            log = 0;
+            have = true;
+            return 1;
+        }
+        if (mode == 2) {
+            ZBits f;
+            f.setup(p, n, lane);
+            if (!fse_read(f, tab, maxlog, maxsym, log)) return -1;
+            have = true;
+            return f.off / 8;
+        }
+        return have ? 0 : -1;
+    }
+
+    // A compressed block [p, p + n): output appended at z.op; frame output started at fstart
+    __device__ bool compressed_block(const uint8_t *p, uint64_t n, uint64_t fstart) {
+        ZBits h;
+        h.setup(p, n, lane);
+        if (n < 1) return false;
+        const uint32_t b0 = h.byte(0);
+        const uint32_t ltype = b0 & 3, sf = (b0 >> 2) & 3;
+        uint64_t regen, csize = 0, hl;
+        uint32_t nstreams = 1;
+        if (ltype <= 1) {
+            if (sf == 0 || sf == 2) {
+                regen = b0 >> 3;
+                hl = 1;
+            } else if (sf == 1) {
+                if (n < 2) return false;
+                regen = (b0 >> 4) + ((uint64_t)h.byte(1) << 4);
+                hl = 2;
+            } else {
+                if (n < 3) return false;
+                regen = (b0 >> 4) + ((uint64_t)h.byte(1) << 4) + ((uint64_t)h.byte(2) << 12);
+                hl = 3;
+            }
+        } else {
+            if (sf <= 1) {
+                if (n < 3) return false;
+                const uint32_t v = b0 | h.byte(1) << 8 | h.byte(2) << 16;
+                regen = (v >> 4) & 0x3FF;
+                csize = (v >> 14) & 0x3FF;
+                hl = 3;
+                nstreams = sf == 0 ? 1 : 4;
+            } else if (sf == 2) {
+                if (n < 4) return false;
+                const uint32_t v = b0 | h.byte(1) << 8 | h.byte(2) << 16 | h.byte(3) << 24;
+                regen = (v >> 4) & 0x3FFF;
+                csize = (v >> 18) & 0x3FFF;
+                hl = 4;
+                nstreams = 4;
+            } else {
+                if (n < 5) return false;
+                const uint64_t v = (uint64_t)(b0 | h.byte(1) << 8 | h.byte(2) << 16 | h.byte(3) << 24) |
+                                   (uint64_t)h.byte(4) << 32;
+                regen = (v >> 4) & 0x3FFFF;
+                csize = (v >> 22) & 0x3FFFF;
+                hl = 5;
+                nstreams = 4;
+            }
+        }
+        if (regen > (128u << 10)) return false;
+        // literals: raw ones stay in the input; decoded ones go to the tail of the output region
+        const uint8_t *lit = nullptr;
+        uint64_t q = hl;
+        if (regen > (uint64_t)z.n - z.op) return false;
+        uint8_t *tail = z.dst + z.n - regen;
+        if (ltype == 0) {
+            if (q + regen > n) return false;
+            lit = p + q;
+            q += regen;
+        } else if (ltype == 1) {
+            if (q + 1 > n) return false;
+            wave_fill(tail, regen, (uint8_t)h.byte(q));
+            lit = tail;
+            q += 1;
+        } else {
+            if (q + csize > n) return false;
+            const uint8_t *ls = p + q;
+            uint64_t lp = 0;
+            if (ltype == 2) {
+                lp = huf_read(ls, csize);
+                if (lp == 0) return false;
+            } else if (!have_huf) {
+                return false;
+            }
+            if (lp > csize) return false;
+            if (nstreams == 1) {
+                if (!huf_stream(ls + lp, csize - lp, tail, regen)) return false;
+            } else {
+                if (csize - lp < 10 || regen < 6) return false;
+                ZBits jt;
+                jt.setup(ls + lp, 6, lane);
+                const uint64_t s1 = jt.byte(0) | jt.byte(1) << 8, s2 = jt.byte(2) | jt.byte(3) << 8,
+                               s3 = jt.byte(4) | jt.byte(5) << 8;
+                const uint64_t total = csize - lp - 6;
+                if (s1 + s2 + s3 > total) return false;
+                const uint64_t s4 = total - s1 - s2 - s3, seg = (regen + 3) / 4;
+                const uint8_t *d = ls + lp + 6;
+                if (!huf_stream(d, s1, tail, seg) || !huf_stream(d + s1, s2, tail + seg, seg) ||
+                    !huf_stream(d + s1 + s2, s3, tail + 2 * seg, seg) ||
+                    !huf_stream(d + s1 + s2 + s3, s4, tail + 3 * seg, regen - 3 * seg))
+                    return false;
+            }
+            lit = tail;
+            q += csize;
+        }
+        if (lit == tail) {   // the decoded literals are read back below (through L2, not a stale L1 line)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        const uint32_t lip = regen ? z.source(lit, (uint32_t)regen) : 0;
+        // sequences
+        if (q >= n) return false;
+        uint64_t nseq = h.byte(q++);
+        if (nseq >= 128) {
+            if (nseq < 255) {
+                if (q >= n) return false;
+                nseq = ((nseq - 128) << 8) + h.byte(q++);
+            } else {
+                if (q + 2 > n) return false;
+                nseq = h.byte(q) + ((uint64_t)h.byte(q + 1) << 8) + 0x7F00;
+                q += 2;
+            }
+        }
+        uint64_t lpos = 0;
+        if (nseq > 0) {
+            if (q >= n) return false;
+            const uint32_t modes = h.byte(q++);
+            if (modes & 3) return false;
+            int64_t u = seq_table(modes >> 6, p + q, n - q, Z.ll, ll_log, have_ll, kZLLDef, 36, 6, 9, 35);
+            if (u < 0) return false;
+            q += (uint64_t)u;
+            u = seq_table((modes >> 4) & 3, p + q, n - q, Z.of, of_log, have_of, kZOFDef, 29, 5, 8, 31);
+            if (u < 0) return false;
+            q += (uint64_t)u;
+            u = seq_table((modes >> 2) & 3, p + q, n - q, Z.ml, ml_log, have_ml, kZMLDef, 53, 6, 9, 52);
+            if (u < 0) return false;
+            q += (uint64_t)u;
+            if (q >= n) return false;
+            ZBits b;
+            if (!b.init_back(p + q, n - q, lane)) return false;
+            uint32_t sll = b.get(ll_log), sof = b.get(of_log), sml = b.get(ml_log);
+            for (uint64_t i = 0; i < nseq; ++i) {
+                const uint32_t ell = rfl(Z.ll[sll]), eof = rfl(Z.of[sof]), eml = rfl(Z.ml[sml]);
+                const uint32_t ofc = eof & 0xffu, mlc = eml & 0xffu, llc = ell & 0xffu;
+                if (ofc > 31 || mlc > 52 || llc > 35) return false;
+                uint64_t ofv = (1ull << ofc);
+                if (ofc > 16) {   // (get() takes <= 32 bits; split the widest offsets)
+                    const uint64_t hi = b.get(ofc - 16);
+                    ofv += (hi << 16) | b.get(16);
+                } else {
+                    ofv += b.get(ofc);
+                }
+                const uint64_t ml = kZMLBase[mlc] + b.get(kZMLBits[mlc]);
+                const uint64_t ll = kZLLBase[llc] + b.get(kZLLBits[llc]);
+                uint64_t off;
+                if (ofv > 3) {
+                    off = ofv - 3;
+                    rep2 = rep1;
+                    rep1 = rep0;
+                    rep0 = (uint32_t)off;
+                } else {
+                    const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0 ? 1u : 0u);
+                    if (idx == 0) {
+                        off = rep0;
+                    } else if (idx == 3) {
+                        off = (uint64_t)rep0 - 1;
+                        if (off == 0) return false;
+                        rep2 = rep1;
+                        rep1 = rep0;
+                        rep0 = (uint32_t)off;
+                    } else {
+                        off = idx == 1 ? rep1 : rep2;
+                        if (idx == 2) rep2 = rep1;
+                        rep1 = rep0;
+                        rep0 = (uint32_t)off;
+                    }
+                }
+                if (i + 1 < nseq) {   // state updates: literal lengths, match lengths, offsets
+                    sll = (ell >> 16) + b.get((ell >> 8) & 0xffu);
+                    sml = (eml >> 16) + b.get((eml >> 8) & 0xffu);
+                    sof = (eof >> 16) + b.get((eof >> 8) & 0xffu);
+                }
+                if (b.off < 0) return false;
+                if (ll > regen - lpos || ll > (uint64_t)z.n - z.op) return false;
+                if (ll) z.literals(lip + (uint32_t)lpos, (uint32_t)ll);
+                lpos += ll;
+                if (off > (uint64_t)z.op - fstart || ml > (uint64_t)z.n - z.op) return false;
+                z.match((uint32_t)ml, (uint32_t)off);
+            }
+            if (b.off != 0) return false;
+        } else if (q != n) {
+            return false;
+        }
+        const uint64_t rest = regen - lpos;
+        if (rest > (uint64_t)z.n - z.op) return false;
+        if (rest) z.literals(lip + (uint32_t)lpos, (uint32_t)rest);
+        return true;
+    }
+
+    // ZSTD_decompressDCtx over [p, p + n) into z (capacity z.n): 0, RDX_BLOSC2_FAILED or _UNSUPPORTED
+    __device__ uint32_t stream(const uint8_t *p, uint64_t n) {
+        ZBits h;
+        h.setup(p, n, lane);
+        uint64_t q = 0;
+        if (n == 0) return RDX_BLOSC2_FAILED;
+        while (q < n) {
+            if (q + 4 > n) return RDX_BLOSC2_FAILED;
+            const uint32_t magic = h.byte(q) | h.byte(q + 1) << 8 | h.byte(q + 2) << 16 | h.byte(q + 3) << 24;
+            if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {   // skippable frame
+                if (q + 8 > n) return RDX_BLOSC2_FAILED;
+                const uint64_t sz = h.byte(q + 4) | h.byte(q + 5) << 8 | h.byte(q + 6) << 16 | (uint64_t)h.byte(q + 7) << 24;
+                if (q + 8 + sz > n) return RDX_BLOSC2_FAILED;
+                q += 8 + sz;
+                continue;
+            }
+            if (magic != 0xFD2FB528u) return RDX_BLOSC2_FAILED;
+            q += 4;
+            if (q >= n) return RDX_BLOSC2_FAILED;
+            const uint32_t fhd = h.byte(q++);
+            const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did_flag = fhd & 3;
+            if (fhd & 0x08) return RDX_BLOSC2_FAILED;
+            uint64_t window = 0;
+            if (!single) {
+                if (q >= n) return RDX_BLOSC2_FAILED;
+                const uint32_t wd = h.byte(q++);
+                const uint64_t wlog = 10 + (wd >> 3);
+                if (wlog > 27) return RDX_BLOSC2_FAILED;
+                const uint64_t wbase = 1ull << wlog;
+                window = wbase + (wbase / 8) * (wd & 7);
+            }
+            const uint32_t did_bytes = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
+            if (q + did_bytes > n) return RDX_BLOSC2_FAILED;
+            uint64_t did = 0;
+            for (uint32_t k = 0; k < did_bytes; ++k) did |= (uint64_t)h.byte(q + k) << (8 * k);
+            q += did_bytes;
+            if (did != 0) return RDX_BLOSC2_FAILED;
+            const uint32_t fcs_bytes = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+            if (q + fcs_bytes > n) return RDX_BLOSC2_FAILED;
+            uint64_t fcs = 0;
+            for (uint32_t k = 0; k < fcs_bytes; ++k) fcs |= (uint64_t)h.byte(q + k) << (8 * k);
+            if (fcs_bytes == 2) fcs += 256;
+            q += fcs_bytes;
+            if (single) window = fcs;
+            if (checksum) return RDX_BLOSC2_UNSUPPORTED;   // XXH64 of the output: decoded on the host
+            const uint64_t bmax = window < (128u << 10) ? window : (128u << 10);
+            const uint64_t fstart = z.op;
+            have_huf = have_ll = have_of = have_ml = false;
+            rep0 = 1;
+            rep1 = 4;
+            rep2 = 8;
+            for (;;) {
+                if (q + 3 > n) return RDX_BLOSC2_FAILED;
+                const uint32_t bh = h.byte(q) | h.byte(q + 1) << 8 | h.byte(q + 2) << 16;
+                q += 3;
+                const uint32_t last = bh & 1, type = (bh >> 1) & 3, bsize = bh >> 3;
+                if (type == 3 || bsize > bmax) return RDX_BLOSC2_FAILED;
+                if (type == 0) {
+                    if (q + bsize > n || bsize > (uint64_t)z.n - z.op) return RDX_BLOSC2_FAILED;
+                    if (bsize) z.literals(z.source(p + q, bsize), bsize);
+                    q += bsize;
+                } else if (type == 1) {
+                    if (q + 1 > n || bsize > (uint64_t)z.n - z.op) return RDX_BLOSC2_FAILED;
+                    z.run((uint8_t)h.byte(q), bsize);
+                    q += 1;
+                } else {
+                    if (q + bsize > n) return RDX_BLOSC2_FAILED;
+                    const uint64_t before = z.op;
+                    if (!compressed_block(p + q, bsize, fstart)) return RDX_BLOSC2_FAILED;
+                    if (z.op - before > bmax) return RDX_BLOSC2_FAILED;
+                    q += bsize;
+                }
+                if (last) break;
+            }
+            if (fcs_bytes && z.op - fstart != fcs) return RDX_BLOSC2_FAILED;
+        }
+        return 0;
+    }
+};
+
 }  // namespace
 
 __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args a) {
@@ -542,11 +1196,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args
             wave_fill(dst, neblock, (uint8_t)(-cb));
         } else if ((uint64_t)cb == neblock) {
             wave_copy(dst, src + pos, neblock);
-        } else if (h.codec == 3) {   // zlib: a row of the stream table, inflated by k_inflate next
+        } else if (h.codec == 3 || h.codec == 4) {   // a row of the stream table: k_inflate (zlib, rows
+            // [0, z_capacity)) or k_blosc2_zstd (zstd, rows [z_capacity, 2 z_capacity)) decodes it next
+            const uint32_t which = h.codec == 4 ? 1u : 0u;
             uint32_t slot = 0;
-            if (lane == 0) slot = atomicAdd(a.z_count, 1u);
+            if (lane == 0) slot = atomicAdd(a.z_count + which, 1u);
             slot = rfl((uint32_t)__shfl((int)slot, 0, 64));
             if (slot >= a.z_capacity) { fail(err, RDX_BLOSC2_UNSUPPORTED); return; }
+            slot += which * (uint32_t)a.z_capacity;
             if (lane == 0) {
                 a.z_in[slot] = src + pos;
                 a.z_len[slot] = (uint64_t)cb;
@@ -660,10 +1317,49 @@ __global__ __launch_bounds__(256) void k_blosc2_filter(const KBlosc2Args a) {
 // Results of the zlib-coded streams (k_inflate over the table): a stream that failed or did not produce
 // exactly its block share fails its chunk, as blosc_d's size check.
 __global__ __launch_bounds__(256) void k_blosc2_zcheck(const KBlosc2Args a) {
-    const uint32_t n = __hip_atomic_load(a.z_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n && i < a.z_capacity;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        if (a.z_err[i] != 0 || a.z_out_len[i] != a.z_cap[i]) atomicCAS(a.err + a.z_chunk[i], 0u, (uint32_t)RDX_BLOSC2_FAILED);
+    for (uint32_t which = 0; which < 2; ++which) {
+        const uint32_t n = __hip_atomic_load(a.z_count + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n && j < a.z_capacity;
+             j += (uint64_t)gridDim.x * blockDim.x) {
+            const uint64_t i = j + which * a.z_capacity;
+            const uint32_t code = a.z_err[i] == RDX_BLOSC2_UNSUPPORTED ? (uint32_t)RDX_BLOSC2_UNSUPPORTED
+                                                                      : (uint32_t)RDX_BLOSC2_FAILED;
+            if (a.z_err[i] != 0 || a.z_out_len[i] != a.z_cap[i]) atomicCAS(a.err + a.z_chunk[i], 0u, code);
+        }
+    }
+}
+
+// zstd rows of the stream table: one wavefront per row, looping over the rows registered by k_blosc2_decode
+__global__ __launch_bounds__(64 * kWaves) void k_blosc2_zstd(const KBlosc2Args a) {
+    __shared__ ZLds LZ[kWaves];
+    const uint32_t wave = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t cnt = rfl(__hip_atomic_load(a.z_count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint64_t n = cnt < a.z_capacity ? cnt : a.z_capacity;
+    for (uint64_t r = (uint64_t)blockIdx.x * kWaves + wave; r < n; r += (uint64_t)gridDim.x * kWaves) {
+        const uint64_t row = a.z_capacity + r;
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(rfl64((uint64_t)gld<const uint8_t *>(a.z_in + row)));
+        const uint64_t len = rfl64(gld<uint64_t>(a.z_len + row));
+        uint8_t *dst = reinterpret_cast<uint8_t *>(rfl64((uint64_t)gld<uint8_t *>(a.z_out + row)));
+        const uint64_t cap = rfl64(gld<uint64_t>(a.z_cap + row));
+        LzStream z{LZ[wave].w, lane};
+        z.dst = dst;
+        z.n = (uint32_t)cap;
+        z.op = z.flushed = 0;
+        ZDec zd{LZ[wave], z, lane};
+        const uint32_t e = zd.stream(src, len);
+        if (e == 0) z.finish();
+        if (lane == 0) {
+            a.z_out_len[row] = e == 0 ? z.op : 0;
+            a.z_err[row] = e;
+        }
+    }
+}
+
+hipError_t launch_blosc2_zstd(const KBlosc2Args &a, hipStream_t s) {
+    if (!a.z_capacity) return hipSuccess;
+    const uint64_t wgs = std::min<uint64_t>((a.z_capacity + kWaves - 1) / kWaves, 1024);   // workgroups loop over rows
+    hipLaunchKernelGGL(k_blosc2_zstd, dim3((uint32_t)wgs), dim3(64 * kWaves), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_blosc2_zcheck(const KBlosc2Args &a, hipStream_t s) {

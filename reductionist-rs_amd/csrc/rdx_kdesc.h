@@ -214,8 +214,10 @@ struct KBlosc2Args {
     uint32_t *err;              // rdx_inflate_error; zeroed by the caller before the launch
     uint32_t n;
     uint32_t wg_per_chunk;      // workgroups (4 decoding waves each) per chunk
-    // zlib-coded block streams are not decoded here but appended to this table (slot = atomic counter)
-    // and inflated by k_inflate afterwards; null: such chunks fail with RDX_BLOSC2_UNSUPPORTED
+    // zlib- and zstd-coded block streams are not decoded here but appended to this table (slot = atomic
+    // counter: zlib rows [0, z_capacity) counted by z_count[0], inflated by k_inflate afterwards; zstd rows
+    // [z_capacity, 2 z_capacity) counted by z_count[1], decoded by k_blosc2_zstd); null: such chunks fail
+    // with RDX_BLOSC2_UNSUPPORTED
     const uint8_t **z_in;       // stream start
     uint64_t *z_len;            // csize
     uint8_t **z_out;            // destination (decode scratch or output)
@@ -223,8 +225,8 @@ struct KBlosc2Args {
     uint32_t *z_chunk;          // chunk index
     uint64_t *z_out_len;        // k_inflate: bytes produced
     uint32_t *z_err;            // k_inflate: rdx_inflate_error
-    uint32_t *z_count;          // entries used (zeroed by the caller)
-    uint64_t z_capacity;
+    uint32_t *z_count;          // [2]: zlib / zstd entries used (zeroed by the caller)
+    uint64_t z_capacity;        // rows per codec (the arrays hold 2 z_capacity)
 };
 
 // Element-wise map in output order: Select (operations.rs:487-526) and axis=[]

@@ -31,6 +31,8 @@ hipError_t launch_blosc2(const KBlosc2Args &a, bool filters, hipStream_t s);
 // after launch_blosc2(a, false) and the zlib-coded streams' inflate (launch_inflate_table): fold their
 // results into the chunks' errors, then the filter launch
 hipError_t launch_blosc2_zcheck(const KBlosc2Args &a, hipStream_t s);
+// after launch_blosc2(a, false): the zstd-coded streams of the table (rows [z_capacity, 2 z_capacity))
+hipError_t launch_blosc2_zstd(const KBlosc2Args &a, hipStream_t s);
 
 #define RDX_DECLARE_DTYPE(tn)                                                                                  \
     hipError_t launch_all_contig_##tn(uint32_t op, const KAllContig &a, uint32_t n_chunks, hipStream_t s);    \

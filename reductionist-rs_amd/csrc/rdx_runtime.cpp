@@ -582,7 +582,7 @@ thread_local uint32_t g_inflate_error = RDX_INFLATE_OK;
 // compression::decompress (compression.rs:18-27) of n device-resident streams into d_out (stream i at
 // d_out + i*cap), asynchronous on s.
 // blosc2: `may_zlib` false when the caller has read every chunk's header on the host and none is
-// zlib-coded: no stream table, no k_inflate / zcheck launches.
+// zlib- or zstd-coded: no stream table, no k_inflate / k_blosc2_zstd / zcheck launches.
 constexpr uint64_t kZTableMaxRows = 1ull << 20;   // 48 B per row: <= 48 MiB of HBM
 
 rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n, const uint8_t *const *h_ptrs,
@@ -618,13 +618,16 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
         // batch, at least 8192 and at most kZTableMaxRows in all, handed out in arrival order across the
         // batch; a stream that finds the table full fails its chunk with RDX_BLOSC2_UNSUPPORTED (the host
         // decompresses that chunk)
+        // (zstd-coded streams: the second half of the table, the same bound per codec, decoded by
+        // k_blosc2_zstd)
         const uint64_t zcap = std::min<uint64_t>(kZTableMaxRows, std::max<uint64_t>(8192, n * 512));
-        if ((st = ensure(ws, ws->zt_in, zcap, s)) || (st = ensure(ws, ws->zt_len, zcap, s)) ||
-            (st = ensure(ws, ws->zt_cap, zcap, s)) || (st = ensure(ws, ws->zt_out_len, zcap, s)) ||
-            (st = ensure(ws, ws->zt_out, zcap, s)) || (st = ensure(ws, ws->zt_chunk, zcap, s)) ||
-            (st = ensure(ws, ws->zt_err, zcap, s)) || (st = ensure(ws, ws->zt_count, 1, s)))
+        const uint64_t rows = 2 * zcap;
+        if ((st = ensure(ws, ws->zt_in, rows, s)) || (st = ensure(ws, ws->zt_len, rows, s)) ||
+            (st = ensure(ws, ws->zt_cap, rows, s)) || (st = ensure(ws, ws->zt_out_len, rows, s)) ||
+            (st = ensure(ws, ws->zt_out, rows, s)) || (st = ensure(ws, ws->zt_chunk, rows, s)) ||
+            (st = ensure(ws, ws->zt_err, rows, s)) || (st = ensure(ws, ws->zt_count, 2, s)))
             return st;
-        RDX_HIP(hipMemsetAsync(ws->zt_count.p, 0, sizeof(uint32_t), s));
+        RDX_HIP(hipMemsetAsync(ws->zt_count.p, 0, 2 * sizeof(uint32_t), s));
         a.z_in = ws->zt_in.p;
         a.z_len = ws->zt_len.p;
         a.z_out = ws->zt_out.p;
@@ -637,6 +640,7 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
         RDX_HIP(launch_blosc2(a, false, s));
         RDX_HIP(launch_inflate_table(ws->zt_in.p, ws->zt_len.p, ws->zt_out.p, ws->zt_cap.p, ws->zt_count.p, zcap,
                                      ws->zt_out_len.p, ws->zt_err.p, s));
+        RDX_HIP(launch_blosc2_zstd(a, s));
         RDX_HIP(launch_blosc2_zcheck(a, s));
         return RDX_OK;
     }
@@ -673,8 +677,9 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
         if ((st = ensure(ws, ws->raw, cap, s))) return st;
         const uint8_t *ptrs[1] = {d_src};
         const uint64_t lens[1] = {len};
-        // a blosc2 chunk in host memory: its header says whether any stream can be zlib-coded (codec 3)
-        const bool may_zlib = !(blosc2 && h_src && len >= 16 && (h_src[2] >> 5) != 3);
+        // a blosc2 chunk in host memory: its header says whether any stream can be zlib- or zstd-coded
+        // (codec 3 / 4: the stream table)
+        const bool may_zlib = !(blosc2 && h_src && len >= 16 && (h_src[2] >> 5) != 3 && (h_src[2] >> 5) != 4);
         if ((st = decompress_launch(ws, req.compression, 1, ptrs, lens, ws->raw.p, cap, ws->zout_len.p, ws->zerr.p, s,
                                     may_zlib)))
             return st;

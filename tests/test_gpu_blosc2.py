@@ -65,7 +65,7 @@ def test_batch_every_layout_matches_oracle(torch, workspace, kind, skew):
     for n in (1, 13, 4096, 65536 + 13, 200000):
         d = payload(rng, n, kind)
         for codec, ts, bs, split, filt, ver in itertools.product(
-                [B.BLOSCLZ, B.LZ4, B.SNAPPY, B.ZLIB], [1, 4, 8], [None, 1000, 16384], [True, False],
+                [B.BLOSCLZ, B.LZ4, B.SNAPPY, B.ZLIB, B.ZSTD], [1, 4, 8], [None, 1000, 16384], [True, False],
                 [(0,) * 6, (0, 0, 0, 0, 0, B.SHUFFLE), (0, 0, 0, 0, 0, B.BITSHUFFLE),
                  (0, 0, 0, 0, B.SHUFFLE, B.BITSHUFFLE)], [5, 2]):
             if ver == 2 and filt.count(0) < 5:
@@ -92,7 +92,9 @@ def test_lone_4mib_chunks_match(torch, workspace):
                             (B.LZ4, 1 << 18, (0, 0, 0, 0, 0, B.SHUFFLE)),
                             (B.LZ4, 1 << 17, (0, 0, 0, 0, 0, B.BITSHUFFLE)),
                             (B.BLOSCLZ, 1 << 15, (0,) * 6),
-                            (B.SNAPPY, 1 << 16, (0, 0, 0, 0, 0, B.SHUFFLE))):
+                            (B.SNAPPY, 1 << 16, (0, 0, 0, 0, 0, B.SHUFFLE)),
+                            (B.ZSTD, 1 << 16, (0, 0, 0, 0, 0, B.SHUFFLE)),
+                            (B.ZSTD, 1 << 18, (0,) * 6)):
         c = B.build(d, 4, bs, codec, filt, memcpyed=False)
         [(e, out)] = device_blosc2(torch, workspace, [c], len(d))
         assert e == 0 and out == d, (codec, bs, filt, e)
@@ -196,8 +198,17 @@ def test_execute_blosc2_requests_match_oracle(engine):
     assert engine.execute_raw(creq, b"invalid format")[0] == _abi.E_DECOMPRESSION
     assert lib.rdx_inflate_last_error() == _abi.BLOSC2_INVALID
     z = bytearray(B.build(np.arange(5000, dtype=np.int32).tobytes(), 4, 4096, B.BLOSCLZ, memcpyed=False))
-    z[2] = (z[2] & 0x1F) | (B.ZSTD << 5)
+    z[2] = (z[2] & 0x1F) | (6 << 5)                        # a user-defined codec
     assert engine.execute_raw(creq, bytes(z))[0] == _abi.E_UNSUPPORTED
+    # zstd-coded chunks through rdx_execute (decoded by k_blosc2_zstd), every op vs the oracle
+    v = np.arange(20000, dtype=np.int32) % 97
+    zc = B.build(v.tobytes(), 4, 8192, B.ZSTD, memcpyed=False)
+    for op in ("sum", "min", "max", "count"):
+        creq = make_request(op, {"dtype": "int32", "compression": "blosc2"}, product_convert)
+        ocreq = make_request(op, {"dtype": "int32", "compression": "blosc2"}, oracle.convert)
+        ost, oinfo, obody, ocounts = oracle.execute(ocreq, zc)
+        pst, pinfo, pbody, pcounts = engine.execute_raw(creq, zc)
+        assert ost == 0 and pst == 0 and pbody == obody and pcounts == ocounts, op
 
 
 def test_execute_device_blosc2(torch, workspace):
@@ -233,3 +244,53 @@ def test_version2_bitshuffle_leftover_rule(torch, workspace):
         assert (e, out) == expected(c, 16384)
     for (c, d), (e, out) in zip(cases, got):
         assert e == 0 and out == d
+
+
+def test_zstd_streams_match_oracle(torch, workspace):
+    """zstd-coded blosc2 streams (frames by the real libzstd at levels -5..19, every block form: raw, RLE,
+    Huffman literals with 1 / 4 streams and treeless repeats, predefined / RLE / FSE / repeat sequence
+    tables, multi-block frames), the LZ4 / Snappy streams of the real liblz4 / libsnappy, corrupted zstd
+    streams (the oracle's result), and a frame with a content checksum (not decoded on the device:
+    RDX_BLOSC2_UNSUPPORTED, the host decodes it)."""
+    pa = pytest.importorskip("pyarrow")
+    xxhash = pytest.importorskip("xxhash")
+    rng = np.random.default_rng(31)
+    chunks = []
+    for kind in ("smooth", "ints", "random", "const"):
+        for n in (13, 4096, 65536 + 13, 300000):
+            d = payload(rng, n, kind)
+            for ts, bs, split, filt in ((1, None, True, (0,) * 6), (4, 16384, True, (0, 0, 0, 0, 0, B.SHUFFLE)),
+                                        (8, 1000, False, (0, 0, 0, 0, 0, B.BITSHUFFLE)), (4, 1 << 18, False, (0,) * 6)):
+                for codec in (B.ZSTD, B.LZ4, B.SNAPPY):
+                    chunks.append(B.build(d, ts, bs, codec, filt, split, enc="lib"))
+    # every zstd level over text-like data (long matches, repeat offsets)
+    text = (b"the quick brown fox jumps over the lazy dog %d " * 8000)[:300000]
+    for level in (-5, 1, 3, 9, 19):
+        st = pa.Codec("zstd", compression_level=level).compress(text, asbytes=True)
+        chunks.append(_one_stream_chunk(st, len(text), B.ZSTD))
+    good = B.build(payload(rng, 70000, "ints"), 4, 16384, B.ZSTD, memcpyed=False)
+    for k in range(30):
+        b = bytearray(good)
+        b[int(rng.integers(32 + 4 * 5, len(b)))] ^= int(rng.integers(1, 256))
+        chunks.append(bytes(b))
+    cap = 300000 + 16 - 300000 % 16
+    got = device_blosc2(torch, workspace, chunks, cap)
+    bad = [i for i, c in enumerate(chunks) if got[i] != expected(c, cap)]
+    assert not bad, [(i, got[i][0], expected(chunks[i], cap)[0]) for i in bad[:8]]
+    # a content checksum: the oracle decodes it, the device hands the chunk to the host
+    d = payload(rng, 5000, "ints")
+    f = bytearray(pa.Codec("zstd").compress(d, asbytes=True))
+    f[4] |= 0x04
+    st = bytes(f) + struct.pack("<I", xxhash.xxh64(d).intdigest() & 0xFFFFFFFF)
+    c = _one_stream_chunk(st, len(d), B.ZSTD)
+    assert oracle.blosc2_decompress(c) == (0, d)
+    assert device_blosc2(torch, workspace, [c], 5008)[0][0] == _abi.BLOSC2_UNSUPPORTED
+
+
+def _one_stream_chunk(stream: bytes, nbytes: int, codec: int) -> bytes:
+    """One block, one stream (typesize 1, no filter) holding `stream`."""
+    base = 32 + 4
+    body = struct.pack("<i", len(stream)) + stream
+    h = struct.pack("<BBBBiii", 5, 1, 0x05 | (codec << 5) | 0x10, 1, nbytes, nbytes, base + len(body))
+    h += bytes(6) + bytes([0, 0]) + bytes(6) + bytes([0, 0])
+    return h + struct.pack("<i", base) + body
