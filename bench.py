@@ -533,14 +533,17 @@ def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
     out = {"workload": "1024 x 4 MiB f32 chunks (random walk quantized to 1/64) as blosc2 chunks: SHUFFLE, "
                        "typesize 4, 64 KiB blocks x 4 streams; batch split over ranks, one "
                        "rdx_decompress_batch_device launch per codec; lone = one chunk per call",
-           "kernel": "k_blosc2_decode + k_blosc2_filter", "unit": "GB/s decompressed (this rank)",
+           "kernel": "k_blosc2_decode (+ k_blosc2_zstd for zstd) + k_blosc2_filter", "unit": "GB/s decompressed (this rank)",
            "bound": "serial token chain per wavefront (one stream each), not HBM"}
     d_out = torch.empty(max(1, n) * raw_len, dtype=torch.uint8, device="cuda")
     d_len = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
     d_err = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
     chunks_by_codec = {}
-    for name, codec in (("lz4", B.LZ4), ("blosclz", B.BLOSCLZ)):
-        chunks = [B.build(r, 4, 1 << 16, codec, (0, 0, 0, 0, 0, B.SHUFFLE), memcpyed=False) for r in raws]
+    # lz4 / blosclz: this repo's writer's streams; lz4_lib / zstd: streams by the real liblz4 / libzstd
+    # (pyarrow's bundled codecs; zstd level 3), decoded by k_blosc2_decode / k_blosc2_zstd
+    for name, codec, enc in (("lz4", B.LZ4, "repo"), ("blosclz", B.BLOSCLZ, "repo"), ("lz4_lib", B.LZ4, "lib"),
+                             ("zstd", B.ZSTD, "lib")):
+        chunks = [B.build(r, 4, 1 << 16, codec, (0, 0, 0, 0, 0, B.SHUFFLE), memcpyed=False, enc=enc) for r in raws]
         chunks_by_codec[name] = chunks
         offs, total = [], 0
         for c in chunks:
@@ -591,6 +594,41 @@ def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
                                                          f"(oracle_blosc2_decompress, g++ -O2; NOT c-blosc2 / blusc, "
                                                          f"whose SIMD decoders are absent from the image) over all "
                                                          f"{n_total} lz4 chunks on a {threads}-thread pool, {tz:.2f} s"}
+        # zstd: the real libzstd (the reference's codec: zstd-sys 1.5.7) on every stream of the zstd chunks,
+        # through pyarrow (releases the GIL), on the same pool; a bounded sample of 128 chunks
+        import pyarrow as pa
+        import struct as S
+        zchunks = chunks_by_codec["zstd"]
+        streams = []
+        for c in zchunks:
+            nb, bs = S.unpack_from("<ii", c, 4)
+            nblk = (nb + bs - 1) // bs
+            for j in range(nblk):
+                pos = S.unpack_from("<i", c, 32 + 4 * j)[0]
+                for k in range(4):
+                    cs = S.unpack_from("<i", c, pos)[0]
+                    pos += 4
+                    streams.append((c[pos:pos + cs], bs // 4) if 0 < cs < bs // 4 else None)
+                    pos += cs if cs > 0 else (1 if cs < 0 else 0)
+        per_chunk = len(streams) // len(zchunks)
+        sample = 128
+
+        def zone(i):
+            base = (i % distinct) * per_chunk
+            for st in streams[base:base + per_chunk]:
+                if st is not None:
+                    pa.decompress(st[0], decompressed_size=st[1], codec="zstd")
+
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(zone, range(threads)))
+            c0 = time.perf_counter()
+            list(ex.map(zone, range(sample)))
+            tz = time.perf_counter() - c0
+        out["cpu_baseline_zstd"] = {"value": round(sample * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
+                                    "kind": "library", "sample": f"the real libzstd (pyarrow's bundled codec) on "
+                                                                 f"every zstd stream of {sample} of the chunks (one "
+                                                                 f"call per 16 KiB stream; raw streams skipped), "
+                                                                 f"{threads}-thread pool, {tz:.2f} s"}
     return out
 
 

@@ -161,7 +161,7 @@ __device__ Hdr parse(const uint8_t *src, uint64_t len, uint64_t cap, bool zlib) 
 
 // Wave-cooperative copy of n bytes (dst any alignment, src any alignment): dword stores once dst is
 // 4-byte aligned, each lane's dword assembled from two aligned source dwords.
-__device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t head = (4 - ((uintptr_t)dst & 3)) & 3;
     if (head > n) head = n;
@@ -183,7 +183,7 @@ __device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
 }
 
 // Fill n bytes with one byte value: 16-byte stores once dst is aligned.
-__device__ void wave_fill(uint8_t *dst, uint64_t n, uint8_t v) {
+__device__ __forceinline__ void wave_fill(uint8_t *dst, uint64_t n, uint8_t v) {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
     if (head > n) head = n;
@@ -246,7 +246,7 @@ struct LzStream {
     }
 
     // write [flushed, flushed + m) of the ring to HBM (m <= kFlush)
-    __device__ void flush(uint32_t m) {
+    __device__ __forceinline__ void flush(uint32_t m) {
         constexpr uint32_t kSl = kFlush / 64;
         wave_sync();
         const uint32_t base = (uint32_t)(flushed & kRingMask);
@@ -258,7 +258,7 @@ struct LzStream {
             for (uint32_t k = 0; k < kSl / 16; ++k)
                 gst<uint4>(d + 16 * k, *reinterpret_cast<const uint4 *>(&L.win[base + lo + 16 * k]));
         } else {
-            for (uint32_t k = 0; k < cnt; ++k) d[k] = L.win[(base + lo + k) & kRingMask];
+            for (uint32_t k = 0; k < cnt; ++k) gst<uint8_t>(d + k, L.win[(base + lo + k) & kRingMask]);
         }
         flushed += m;
         // far match sources read these bytes back: their stores must be in L2 first
@@ -275,7 +275,7 @@ struct LzStream {
         return (uint8_t)(w >> (8 * (a & 3)));
     }
     // literal run of `run` bytes from input position ip
-    __device__ void literals(uint32_t ip, uint32_t run) {
+    __device__ __forceinline__ void literals(uint32_t ip, uint32_t run) {
         for (uint32_t s = 0; s < run; s += 64) {
             ensure(ip + s + 64);
             room();
@@ -286,7 +286,7 @@ struct LzStream {
         }
     }
     // match of len bytes at distance dist (1 <= dist <= op)
-    __device__ void match(uint32_t len, uint32_t dist) {
+    __device__ __forceinline__ void match(uint32_t len, uint32_t dist) {
         for (uint32_t s = 0; s < len; s += 64) {
             room();
             const uint32_t k = len - s < 64 ? len - s : 64;
@@ -300,12 +300,12 @@ struct LzStream {
             asm volatile("" ::: "memory");
         }
     }
-    __device__ void finish() {
+    __device__ __forceinline__ void finish() {
         while (op > flushed) flush(op - flushed < kFlush ? (uint32_t)(op - flushed) : kFlush);
     }
     // stage a new source (zstd: raw literals in the input, or decoded literals in HBM): `avail` bytes at p;
     // returns the aligned-coordinate position of p's first byte (the ip literals() takes)
-    __device__ uint32_t source(const uint8_t *p, uint32_t avail) {
+    __device__ __forceinline__ uint32_t source(const uint8_t *p, uint32_t avail) {
         const uint32_t skew = (uint32_t)((uintptr_t)p & 3);
         srcw = reinterpret_cast<const uint32_t *>(p - skew);
         end = skew + avail;
@@ -315,7 +315,7 @@ struct LzStream {
         return skew;
     }
     // len copies of byte b (zstd RLE blocks)
-    __device__ void run(uint8_t b, uint32_t len) {
+    __device__ __forceinline__ void run(uint8_t b, uint32_t len) {
         for (uint32_t s = 0; s < len; s += 64) {
             room();
             const uint32_t k = len - s < 64 ? len - s : 64;
@@ -527,7 +527,7 @@ struct ZWin {
     uint32_t nw, lane;
     int32_t wd0;
     uint32_t v;
-    __device__ void load(int32_t d0) {
+    __device__ __forceinline__ void load(int32_t d0) {
         wd0 = d0;
         const int32_t d = d0 + (int32_t)lane;
         v = (d >= 0 && (uint32_t)d < nw) ? gld<uint32_t>(w + d) : 0u;
@@ -546,7 +546,7 @@ struct ZBits {
     uint32_t sb;       // skew bits
     uint64_t nbytes;
     int64_t off;       // backward: bits left; forward: next bit
-    __device__ void setup(const uint8_t *p, uint64_t n, uint32_t lane) {
+    __device__ __forceinline__ void setup(const uint8_t *p, uint64_t n, uint32_t lane) {
         const uint32_t skew = (uint32_t)((uintptr_t)p & 3);
         win.w = reinterpret_cast<const uint32_t *>(p - skew);
         win.nw = (uint32_t)((skew + n + 3) / 4);
@@ -567,7 +567,7 @@ struct ZBits {
         return k >= 32 ? v : v & ((1u << k) - 1);
     }
     __device__ __forceinline__ uint32_t byte(uint64_t i) { return at(8 * i, 8, false); }
-    __device__ bool init_back(const uint8_t *p, uint64_t n, uint32_t lane) {
+    __device__ __forceinline__ bool init_back(const uint8_t *p, uint64_t n, uint32_t lane) {
         setup(p, n, lane);
         if (n == 0) return false;
         const uint32_t last = at(8 * (n - 1), 8, true);
@@ -594,18 +594,31 @@ struct ZBits {
     }
 };
 
+// weight wv of symbol s into lane s % 64 of w[s / 64]
+__device__ __forceinline__ void zput(uint32_t lane, uint32_t s, uint32_t wv, uint32_t &w0, uint32_t &w1, uint32_t &w2,
+                                     uint32_t &w3) {
+    const uint32_t k = s >> 6;
+    if (lane == (s & 63)) {
+        if (k == 0) w0 = wv;
+        else if (k == 1) w1 = wv;
+        else if (k == 2) w2 = wv;
+        else w3 = wv;
+    }
+}
+
 struct ZDec {
     ZLds &Z;
-    LzStream &z;
+    LzStream z;   // by value (a reference member kept the stream in scratch and its LDS accesses flat)
     const uint32_t lane;
     bool have_huf = false, have_ll = false, have_of = false, have_ml = false;
+    bool pre_ll = false, pre_of = false, pre_ml = false;   // the LDS table holds the predefined distribution
     uint32_t huf_bits = 0, ll_log = 0, of_log = 0, ml_log = 0;
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
 
     // FSE decode table from a per-lane distribution (lane s: symbol s's normalised count; nsym <= 64):
     // the spread by one lane's LDS stores, then the states' bits / baselines in order with the per-symbol
     // counters in a VGPR (lane s), entries assembled in VGPRs and stored coalesced.
-    __device__ bool fse_build(uint32_t *tab, int freq_v, uint32_t nsym, uint32_t log) {
+    __device__ __forceinline__ bool fse_build(uint32_t *tab, int freq_v, uint32_t nsym, uint32_t log) {
         const uint32_t size = 1u << log;
         uint32_t high = size;
         for (uint32_t s = 0; s < nsym; ++s) {
@@ -648,7 +661,7 @@ struct ZDec {
     }
 
     // FSE table description (forward bits at b.off); symbols <= max_sym (< 64), accuracy <= max_log.
-    __device__ bool fse_read(ZBits &b, uint32_t *tab, uint32_t max_log, uint32_t max_sym, uint32_t &log_out) {
+    __device__ __forceinline__ bool fse_read(ZBits &b, uint32_t *tab, uint32_t max_log, uint32_t max_sym, uint32_t &log_out) {
         bool ok = true;
         const uint32_t log = 5 + b.fwd(4, ok);
         if (!ok || log > max_log) return false;
@@ -692,22 +705,14 @@ struct ZDec {
     }
 
     // Huffman tree description at stream bytes [p, p + n) -> Z.huf; returns the bytes used (0: corrupt)
-    __device__ uint32_t huf_read(const uint8_t *p, uint64_t n) {
+    __device__ __forceinline__ uint32_t huf_read(const uint8_t *p, uint64_t n) {
         ZBits h;
         h.setup(p, n, lane);
         if (n < 1) return 0;
         const uint32_t hdr = h.byte(0);
         uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;   // weight of symbol 64k + lane in wk
         uint32_t nw = 0, used;
-        auto put = [&](uint32_t s, uint32_t wv) {
-            const uint32_t k = s >> 6;
-            if (lane == (s & 63)) {
-                if (k == 0) w0 = wv;
-                else if (k == 1) w1 = wv;
-                else if (k == 2) w2 = wv;
-                else w3 = wv;
-            }
-        };
+#define put(s_, wv_) zput(lane, (s_), (wv_), w0, w1, w2, w3)
         if (hdr >= 128) {
             nw = hdr - 127;
             const uint32_t bytes = (nw + 1) / 2;
@@ -801,10 +806,11 @@ struct ZDec {
         huf_bits = maxbits;
         have_huf = true;
         return used;
+#undef put
     }
 
     // One Huffman stream of `count` symbols into dst[0..count) (consumed exactly)
-    __device__ bool huf_stream(const uint8_t *p, uint64_t n, uint8_t *dst, uint64_t count) {
+    __device__ __forceinline__ bool huf_stream(const uint8_t *p, uint64_t n, uint8_t *dst, uint64_t count) {
         ZBits b;
         if (!b.init_back(p, n, lane)) return false;
         const uint32_t mb = huf_bits;
@@ -814,21 +820,55 @@ struct ZDec {
             const uint32_t e = rfl((uint32_t)Z.huf[idx]);
             b.off = save - (int64_t)(e >> 8);
             if (b.off < 0) return false;
-            if (lane == 0) dst[i] = (uint8_t)e;
+            if (lane == 0) gst<uint8_t>(dst + i, (uint8_t)e);
         }
         return b.off == 0;
     }
 
+    // Four Huffman streams side by side (4X literals): one symbol of each per step, their four table
+    // reads in flight together, and one byte store per step (lane k stores stream k's symbol).
+    __device__ __forceinline__ bool huf_stream4(const uint8_t *d, uint64_t s1, uint64_t s2, uint64_t s3, uint64_t s4,
+                                                uint8_t *dst, uint64_t seg, uint64_t last) {
+        ZBits b0, b1, b2, b3;
+        if (!b0.init_back(d, s1, lane) || !b1.init_back(d + s1, s2, lane) || !b2.init_back(d + s1 + s2, s3, lane) ||
+            !b3.init_back(d + s1 + s2 + s3, s4, lane))
+            return false;
+        const uint32_t mb = huf_bits;
+        uint8_t *mine = dst + (uint64_t)(lane & 3) * seg;
+        bool bad = false;
+        for (uint64_t i = 0; i < seg; ++i) {
+            const bool has3 = i < last;
+            const int64_t v0 = b0.off, v1 = b1.off, v2 = b2.off, v3 = b3.off;
+            const uint32_t i0 = b0.get(mb), i1 = b1.get(mb), i2 = b2.get(mb), i3 = has3 ? b3.get(mb) : 0u;
+            const uint32_t e0 = rfl((uint32_t)Z.huf[i0]), e1 = rfl((uint32_t)Z.huf[i1]), e2 = rfl((uint32_t)Z.huf[i2]),
+                           e3 = rfl((uint32_t)Z.huf[i3]);
+            b0.off = v0 - (int64_t)(e0 >> 8);
+            b1.off = v1 - (int64_t)(e1 >> 8);
+            b2.off = v2 - (int64_t)(e2 >> 8);
+            b3.off = has3 ? v3 - (int64_t)(e3 >> 8) : v3;
+            bad |= (b0.off < 0) | (b1.off < 0) | (b2.off < 0) | (b3.off < 0);
+            const uint32_t v = lane == 0 ? e0 : lane == 1 ? e1 : lane == 2 ? e2 : e3;
+            if (lane < 3 || (lane == 3 && has3)) gst<uint8_t>(mine + i, (uint8_t)v);
+            if (bad) return false;
+        }
+        return b0.off == 0 && b1.off == 0 && b2.off == 0 && b3.off == 0;
+    }
+
     // a sequence table: mode 0 predefined, 1 RLE, 2 FSE, 3 repeat; bytes used at p (or -1)
-    __device__ int64_t seq_table(uint32_t mode, const uint8_t *p, uint64_t n, uint32_t *tab, uint32_t &log, bool &have,
-                                 const int16_t *def, uint32_t ndef, uint32_t deflog, uint32_t maxlog, uint32_t maxsym) {
+    __device__ __forceinline__ int64_t seq_table(uint32_t mode, const uint8_t *p, uint64_t n, uint32_t *tab, uint32_t &log, bool &have,
+                                 bool &predef, const int16_t *def, uint32_t ndef, uint32_t deflog, uint32_t maxlog,
+                                 uint32_t maxsym) {
         if (mode == 0) {
-            const int fv = lane < ndef ? (int)def[lane] : 0;
-            if (!fse_build(tab, fv, ndef, deflog)) return -1;
+            if (!predef) {   // (the table keeps the predefined distribution until another mode replaces it)
+                const int fv = lane < ndef ? (int)def[lane] : 0;
+                if (!fse_build(tab, fv, ndef, deflog)) return -1;
+                predef = true;
+            }
             log = deflog;
             have = true;
             return 0;
         }
+        if (mode != 3) predef = false;
         if (mode == 1) {
             if (n < 1) return -1;
             ZBits h;
@@ -852,7 +892,7 @@ struct ZDec {
     }
 
     // A compressed block [p, p + n): output appended at z.op; frame output started at fstart
-    __device__ bool compressed_block(const uint8_t *p, uint64_t n, uint64_t fstart) {
+    __device__ __forceinline__ bool compressed_block(const uint8_t *p, uint64_t n, uint64_t fstart) {
         ZBits h;
         h.setup(p, n, lane);
         if (n < 1) return false;
@@ -935,11 +975,7 @@ struct ZDec {
                 const uint64_t total = csize - lp - 6;
                 if (s1 + s2 + s3 > total) return false;
                 const uint64_t s4 = total - s1 - s2 - s3, seg = (regen + 3) / 4;
-                const uint8_t *d = ls + lp + 6;
-                if (!huf_stream(d, s1, tail, seg) || !huf_stream(d + s1, s2, tail + seg, seg) ||
-                    !huf_stream(d + s1 + s2, s3, tail + 2 * seg, seg) ||
-                    !huf_stream(d + s1 + s2 + s3, s4, tail + 3 * seg, regen - 3 * seg))
-                    return false;
+                if (!huf_stream4(ls + lp + 6, s1, s2, s3, s4, tail, seg, regen - 3 * seg)) return false;
             }
             lit = tail;
             q += csize;
@@ -967,13 +1003,13 @@ struct ZDec {
             if (q >= n) return false;
             const uint32_t modes = h.byte(q++);
             if (modes & 3) return false;
-            int64_t u = seq_table(modes >> 6, p + q, n - q, Z.ll, ll_log, have_ll, kZLLDef, 36, 6, 9, 35);
+            int64_t u = seq_table(modes >> 6, p + q, n - q, Z.ll, ll_log, have_ll, pre_ll, kZLLDef, 36, 6, 9, 35);
             if (u < 0) return false;
             q += (uint64_t)u;
-            u = seq_table((modes >> 4) & 3, p + q, n - q, Z.of, of_log, have_of, kZOFDef, 29, 5, 8, 31);
+            u = seq_table((modes >> 4) & 3, p + q, n - q, Z.of, of_log, have_of, pre_of, kZOFDef, 29, 5, 8, 31);
             if (u < 0) return false;
             q += (uint64_t)u;
-            u = seq_table((modes >> 2) & 3, p + q, n - q, Z.ml, ml_log, have_ml, kZMLDef, 53, 6, 9, 52);
+            u = seq_table((modes >> 2) & 3, p + q, n - q, Z.ml, ml_log, have_ml, pre_ml, kZMLDef, 53, 6, 9, 52);
             if (u < 0) return false;
             q += (uint64_t)u;
             if (q >= n) return false;
@@ -1039,7 +1075,7 @@ struct ZDec {
     }
 
     // ZSTD_decompressDCtx over [p, p + n) into z (capacity z.n): 0, RDX_BLOSC2_FAILED or _UNSUPPORTED
-    __device__ uint32_t stream(const uint8_t *p, uint64_t n) {
+    __device__ __forceinline__ uint32_t stream(const uint8_t *p, uint64_t n) {
         ZBits h;
         h.setup(p, n, lane);
         uint64_t q = 0;
@@ -1341,15 +1377,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_zstd(const KBlosc2Args a
         const uint64_t len = rfl64(gld<uint64_t>(a.z_len + row));
         uint8_t *dst = reinterpret_cast<uint8_t *>(rfl64((uint64_t)gld<uint8_t *>(a.z_out + row)));
         const uint64_t cap = rfl64(gld<uint64_t>(a.z_cap + row));
-        LzStream z{LZ[wave].w, lane};
-        z.dst = dst;
-        z.n = (uint32_t)cap;
-        z.op = z.flushed = 0;
-        ZDec zd{LZ[wave], z, lane};
+        ZDec zd{LZ[wave], LzStream{LZ[wave].w, lane}, lane};
+        zd.z.dst = dst;
+        zd.z.n = (uint32_t)cap;
+        zd.z.op = zd.z.flushed = 0;
         const uint32_t e = zd.stream(src, len);
-        if (e == 0) z.finish();
+        if (e == 0) zd.z.finish();
         if (lane == 0) {
-            a.z_out_len[row] = e == 0 ? z.op : 0;
+            a.z_out_len[row] = e == 0 ? zd.z.op : 0;
             a.z_err[row] = e;
         }
     }

@@ -1,6 +1,7 @@
 """Device blosc2 decode timing (k_blosc2): a batch of 4 MiB f32 chunks and a lone chunk per call, for
 both LZ codecs and a few block sizes.  One JSON line per case.
-    python tools/probe_blosc2.py [n_chunks]"""
+    python tools/probe_blosc2.py [n_chunks] [codec,codec,...]   (lz4 blosclz zstd lz4_lib; zstd / lz4_lib: streams
+    by the real libzstd / liblz4 through pyarrow)"""
 import json
 import sys
 from pathlib import Path
@@ -27,9 +28,12 @@ def main():
     d_out = torch.empty(n * raw_len, dtype=torch.uint8, device="cuda")
     d_len = torch.zeros(n, dtype=torch.int64, device="cuda")
     d_err = torch.zeros(n, dtype=torch.int32, device="cuda")
-    for name, codec in (("lz4", B.LZ4), ("blosclz", B.BLOSCLZ)):
+    want = sys.argv[2].split(",") if len(sys.argv) > 2 else ["lz4", "blosclz"]
+    codecs = {"lz4": (B.LZ4, "repo"), "blosclz": (B.BLOSCLZ, "repo"), "zstd": (B.ZSTD, "lib"), "lz4_lib": (B.LZ4, "lib")}
+    for name in want:
+        codec, enc = codecs[name]
         for bs in (1 << 15, 1 << 16, 1 << 18):
-            chunks = [B.build(r, 4, bs, codec, (0, 0, 0, 0, 0, B.SHUFFLE), memcpyed=False) for r in raws]
+            chunks = [B.build(r, 4, bs, codec, (0, 0, 0, 0, 0, B.SHUFFLE), memcpyed=False, enc=enc) for r in raws]
             offs, total = [], 0
             for c in chunks:
                 offs.append(total)
