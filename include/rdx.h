@@ -42,7 +42,7 @@ typedef enum rdx_status {
     RDX_E_NAN_UNORDERED = 7,       /* operations.rs:181-183,355-357 NaN in min/max — reference panics with
                                       "unexpected undefined order error for min"                            */
     RDX_E_UNSUPPORTED = 8,         /* a blosc2 codec / filter not decoded on the device (RDX_BLOSC2_UNSUPPORTED:
-                                      zstd, dictionaries, delta) / rank > 32 / views of >= 2^32
+                                      dictionaries, delta, checksummed zstd frames) / rank > 32 / views of >= 2^32
                                       elements: the cause is rdx_last_unsupported_reason()             */
     RDX_E_DEVICE = 9,              /* HIP runtime error                                                      */
     RDX_E_OUT_OF_MEMORY = 10,      /* device or pinned allocation failed                                     */
@@ -73,7 +73,7 @@ typedef enum rdx_inflate_error {
     RDX_BLOSC2_INVALID = 12,         /* "invalid blosc2 compressed data": blosc2_cbuffer_sizes -> nbytes 0 */
     RDX_BLOSC2_FAILED = 13,          /* "failed to decompress blosc2 data": blosc2_decompress <= 0        */
     RDX_BLOSC2_SIZE = 14,            /* "unexpected decompressed size for blosc2 data"                     */
-    RDX_BLOSC2_UNSUPPORTED = 15      /* a codec / flag not decoded here (zstd, dictionaries,
+    RDX_BLOSC2_UNSUPPORTED = 15      /* a codec / flag not decoded here (checksummed zstd frames, dictionaries,
                                         user-defined codecs or filters, delta): status RDX_E_UNSUPPORTED */
 } rdx_inflate_error;
 
@@ -82,7 +82,7 @@ typedef enum rdx_inflate_error {
  * the reference serves that this engine does not plan (run the reference's CPU path for it). */
 typedef enum rdx_unsupported_reason {
     RDX_UNSUPPORTED_NONE = 0,
-    RDX_UNSUPPORTED_BLOSC2_CODEC = 1, /* RDX_BLOSC2_UNSUPPORTED: zstd, dictionaries, delta, user codecs         */
+    RDX_UNSUPPORTED_BLOSC2_CODEC = 1, /* RDX_BLOSC2_UNSUPPORTED: dictionaries, delta, user codecs, zstd checksums */
     RDX_UNSUPPORTED_RANK = 2,         /* request rank above RDX_MAX_NDIM                                    */
     RDX_UNSUPPORTED_VIEW_SIZE = 3,    /* a view of 2^32 or more elements, or a dim of 2^32 or more            */
     RDX_UNSUPPORTED_VIEW_DIMS = 4,    /* more than 16 dims left after canonicalisation                       */

@@ -570,7 +570,9 @@ __device__ __forceinline__ void accept_record(const uint64_t *P, uint64_t (&g)[k
 #pragma unroll
         for (int j = 0; j < kG; ++j)
             if ((uint32_t)(g[j] >> 48) != tag) {
-                g[j] = poll_granule(P + j * stride, tag);
+                // one spin budget per lane: after a granule timed out, a faulted launch does not poll again
+                // (so many missing records cost one kSpinLimit period, not one each)
+                if (!fault) g[j] = poll_granule(P + j * stride, tag);
                 fault |= (uint32_t)(g[j] >> 48) != tag;
             }
     }
@@ -591,7 +593,7 @@ __device__ __forceinline__ void collect(const uint64_t *P, Red<T, OP> &r, uint32
 #pragma unroll
         for (int j = 0; j < kG; ++j)
             if ((uint32_t)(g[j] >> 48) != tag) {
-                g[j] = poll_granule(P + j * stride, tag);
+                if (!fault) g[j] = poll_granule(P + j * stride, tag);   // (one spin budget per lane)
                 fault |= (uint32_t)(g[j] >> 48) != tag;
             }
     }
@@ -855,7 +857,7 @@ __device__ inline void finalize_count(int64_t cnt, int64_t *dst, uint32_t *statu
     for (uint32_t j = threadIdx.x; j < nblocks; j += kBlock) {
         uint64_t v = __hip_atomic_load(partials + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__builtin_expect((uint32_t)(v >> 48) != epoch, 0)) {
-            v = poll_granule(partials + j, epoch);
+            if (!fault) v = poll_granule(partials + j, epoch);   // (one spin budget per lane)
             fault |= (uint32_t)(v >> 48) != epoch;
         }
         t += (int64_t)(v & kPayload);
