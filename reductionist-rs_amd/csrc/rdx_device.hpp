@@ -642,9 +642,30 @@ __device__ __forceinline__ void xor_merge(Red<T, OP> &r, int m) {
     r.merge(other);
 }
 
+// Float min/max without a zero in the wave: only the value, count and NaN words move (the ±0 ranks
+// stay at their identity in every lane, so merging them is a no-op).
+template <typename T, int OP>
+__device__ __forceinline__ void xor_merge_noranks(Red<T, OP> &r, int m) {
+    uint64_t w[kPartialWords], o[kPartialWords];
+    r.to_words(w);
+#pragma unroll
+    for (int i = 0; i < kPartialWords; ++i) o[i] = (i == 0 || i == 2 || i == 5) ? shfl_xor_u64(w[i], m) : w[i];
+    Red<T, OP> other;
+    other.from_words(o);
+    r.merge(other);
+}
+
 // Deterministic butterfly over the 64 lanes; every lane ends with the wave total.
 template <typename T, int OP>
 __device__ __forceinline__ void wave_reduce(Red<T, OP> &r) {
+    if constexpr (Red<T, OP>::kRank) {
+        const int64_t id = OP == OP_MAX ? -1 : INT64_MAX;
+        if (!__builtin_amdgcn_ballot_w64(r.zp != id || r.zn != id)) {   // wave-uniform: no zero seen
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) xor_merge_noranks(r, m);
+            return;
+        }
+    }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) xor_merge(r, m);
 }

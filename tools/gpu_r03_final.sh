@@ -10,3 +10,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 timeout -k 10 500 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c2trace -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --primary-only > $OUT/c2trace.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc -o run --output-format csv -- python3 bench.py --steps 20 --warmup 4 --primary-only > $OUT/pmc.log 2>&1
+[ $? -eq 0 ] && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw -o run --output-format csv -- python3 bench.py --steps 20 --warmup 4 --primary-only > $OUT/pmcw.log 2>&1
