@@ -76,6 +76,7 @@ struct Tuning {
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
     int fold_last = env_int("RDX_FOLD_LAST", 1);                       // A/B: 0 = arrival counters everywhere
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
+    int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
 };
 
 const Tuning &tuning() {
@@ -145,6 +146,8 @@ constexpr uint64_t kSlotWords = 3;   // rdx_device.hpp put_host_slot: value lo, 
 struct Job;
 struct Lane {
     rdx_workspace *ws = nullptr;
+    bool owns_ws = true;                     // false: the stream / workspace of `twin` (launch-ahead pairs)
+    Lane *twin = nullptr;                    // the lane sharing this stream, if any
     uint64_t *h_res = nullptr;               // kTableChunks slots, fine-grained page-locked memory
     Job *batch[kTableChunks] = {};
     bool group = false;                      // the launch: one plan over the batch's chunks (else k_multi)
@@ -1439,15 +1442,23 @@ rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease) {
 
 void destroy_lane(Lane *L) {
     if (!L) return;
-    if (L->ws) destroy_workspace(L->ws);   // synchronises its stream first
+    if (L->ws && L->owns_ws) destroy_workspace(L->ws);   // synchronises its stream first
     if (L->h_res) (void)hipHostFree(L->h_res);
     delete L;
 }
 
-rdx_status create_lane(int device, Lane **out) {
+// A lane: its own stream / workspace, or (`share`) the stream of another lane, so that a second launch
+// queues behind the first on the device instead of waiting for its results on the host (launch-ahead).
+rdx_status create_lane(int device, Lane **out, Lane *share = nullptr) {
     auto *L = new (std::nothrow) Lane();
     if (!L) return RDX_E_OUT_OF_MEMORY;
-    rdx_status st = create_workspace(device, &L->ws);
+    rdx_status st = RDX_OK;
+    if (share) {
+        L->ws = share->ws;
+        L->owns_ws = false;
+    } else {
+        st = create_workspace(device, &L->ws);
+    }
     if (!st) {
         // fine-grained (coherent): the kernel's system-scope stores land in host memory directly
         hipError_t e = hipHostMalloc((void **)&L->h_res, kTableChunks * kSlotWords * sizeof(uint64_t),
@@ -1459,6 +1470,10 @@ rdx_status create_lane(int device, Lane **out) {
         destroy_lane(L);
         return st;
     }
+    if (share) {
+        L->twin = share;
+        share->twin = L;
+    }
     *out = L;
     return RDX_OK;
 }
@@ -1468,8 +1483,12 @@ rdx_status create_lane(int device, Lane **out) {
 rdx_status launch_lane(Lane &L) {
     rdx_workspace *ws = L.ws;
     // the epoch wraps at 2^16 launches: clear the slots so that no stale slot can carry a current tag (the
-    // lane is idle here; its stream orders the next launch after everything before)
-    if (ws->epoch + 1 > 0xffffu) std::memset(L.h_res, 0, kTableChunks * kSlotWords * sizeof(uint64_t));
+    // lane, and its twin on the same stream, are idle here: the dispatcher waits for that at a wrap; the
+    // stream orders the next launch after everything before)
+    if (ws->epoch + 1 > 0xffffu) {
+        std::memset(L.h_res, 0, kTableChunks * kSlotWords * sizeof(uint64_t));
+        if (L.twin) std::memset(L.twin->h_res, 0, kTableChunks * kSlotWords * sizeof(uint64_t));
+    }
     rdx_status st;
     const hipStream_t s = ws->own_stream;
     if (L.group) {   // one plan, the chunks in the kernel arguments, chunk i's result into slot i
@@ -1642,11 +1661,19 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
         bool progressed = false;
         // launch on free lanes (created up to coalesce_lanes)
         while (!pending.empty()) {
+            // a free lane on an idle stream first, then (launch-ahead pairs) a free lane whose twin is in
+            // flight; at an epoch wrap only a lane whose twin is idle too
             Lane *lane = nullptr;
             for (Lane *l : e->lanes)
-                if (l->n == 0) { lane = l; break; }
+                if (l->n == 0 && (!l->twin || l->twin->n == 0)) { lane = l; break; }
+            if (!lane) {
+                for (Lane *l : e->lanes)
+                    if (l->n == 0 && l->ws->epoch + 1 <= 0xffffu) { lane = l; break; }
+            }
             if (!lane && e->lanes.size() < ctx->cfg.coalesce_lanes) {
-                if (create_lane(e->device, &lane) == RDX_OK) e->lanes.push_back(lane);
+                // with RDX_COALESCE_DEPTH=2 every second lane shares the stream of the one before
+                Lane *share = tuning().coalesce_depth >= 2 && e->lanes.size() % 2 == 1 ? e->lanes.back() : nullptr;
+                if (create_lane(e->device, &lane, share) == RDX_OK) e->lanes.push_back(lane);
                 else lane = nullptr;
             }
             if (!lane) {
@@ -1681,7 +1708,7 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
         for (Lane *l : e->lanes) {
             if (l->n == 0) continue;
             bool kernel_done = false;
-            if (++l->polls % 64 == 0) {   // the lane's stream holds nothing but this launch
+            if (++l->polls % 64 == 0) {   // the lane's stream holds nothing but this launch (and its twin's)
                 const hipError_t q = hipStreamQuery(l->ws->own_stream);
                 kernel_done = q != hipErrorNotReady;
             }
