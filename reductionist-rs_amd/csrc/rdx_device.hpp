@@ -769,12 +769,38 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
             const uint32_t j = threadIdx.x + 64u * u;
             if (j < nrec) load_record<T, OP>(P + (uint64_t)j * kR, g[u]);
         }
+        // Records not yet visible (the folder's own streaming often ends before the last publisher's): every
+        // stale granule of the wave is re-read in the same round — one round trip per retry for all of
+        // them, not one per granule in turn — until all carry the tag or the spin budget is spent.
+        for (uint32_t it = 0;; ++it) {
+            bool stale = false;
+#pragma unroll
+            for (int u = 0; u < kWaveFold; ++u) {
+                const bool live = threadIdx.x + 64u * u < nrec;
+#pragma unroll
+                for (int q = 0; q < kR; ++q) stale |= live && (uint32_t)(g[u][q] >> 48) != out.epoch;
+            }
+            if (!__builtin_amdgcn_ballot_w64(stale)) break;
+            if (it >= kSpinLimit) {
+                fault = stale ? 1u : 0u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int u = 0; u < kWaveFold; ++u) {
+                const uint32_t j = threadIdx.x + 64u * u;
+#pragma unroll
+                for (int q = 0; q < kR; ++q)
+                    if (j < nrec && (uint32_t)(g[u][q] >> 48) != out.epoch)
+                        g[u][q] = __hip_atomic_load(P + (uint64_t)j * kR + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < kWaveFold; ++u) {
             const uint32_t j = threadIdx.x + 64u * u;
             if (j >= nrec) continue;
             Red<T, OP> o;
-            accept_record<T, OP>(P + (uint64_t)j * kR, g[u], o, out.epoch, fault);
+            decode<T, OP>(g[u], o);
             acc.merge(o);
         }
         wave_reduce(acc);
