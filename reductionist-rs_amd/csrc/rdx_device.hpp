@@ -785,7 +785,11 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
                 fault = stale ? 1u : 0u;
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            // backing off: a folder whose publishers are far from done (a batch launch that fills the chip)
+            // must not flood the fabric with re-reads while they stream
+            if (it < 2) __builtin_amdgcn_s_sleep(1);
+            else if (it < 6) __builtin_amdgcn_s_sleep(8);
+            else __builtin_amdgcn_s_sleep(32);
 #pragma unroll
             for (int u = 0; u < kWaveFold; ++u) {
                 const uint32_t j = threadIdx.x + 64u * u;
