@@ -625,6 +625,11 @@ def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
             list(ex.map(zone, range(sample)))
             tz = time.perf_counter() - c0
         zbytes = sum(zjobs[i % distinct][1] for i in range(sample))
+        # one chunk on one thread (a lone request: the reference decodes it on the request's own thread)
+        t1 = time.perf_counter()
+        for i in range(20):
+            zone(i)
+        lone_cpu = (time.perf_counter() - t1) / 20
         out["cpu_baseline_zstd"] = {"value": round(sample * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
                                     "kind": "library", "sample": f"the real libzstd (pyarrow's bundled codec) on "
                                                                  f"the zstd streams of {sample} chunks, each chunk's "
@@ -634,7 +639,8 @@ def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
                                                                  f"counts) / that time: the raw / run streams are not "
                                                                  f"copied, which favours the CPU ({zbytes >> 20} MiB "
                                                                  f"decoded by libzstd)",
-                                    "zstd_stream_GBs": round(zbytes / tz / 1e9, 2)}
+                                    "zstd_stream_GBs": round(zbytes / tz / 1e9, 2),
+                                    "lone_chunk_one_thread_us": round(lone_cpu * 1e6, 1)}
     return out
 
 

@@ -780,15 +780,16 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
 #pragma unroll
                 for (int q = 0; q < kR; ++q) stale |= live && (uint32_t)(g[u][q] >> 48) != out.epoch;
             }
-            if (!__builtin_amdgcn_ballot_w64(stale)) break;
+            const uint64_t waiting = __builtin_amdgcn_ballot_w64(stale);
+            if (!waiting) break;
             if (it >= kSpinLimit) {
                 fault = stale ? 1u : 0u;
                 break;
             }
-            // backing off: a folder whose publishers are far from done (a batch launch that fills the chip)
-            // must not flood the fabric with re-reads while they stream
-            if (it < 2) __builtin_amdgcn_s_sleep(1);
-            else if (it < 6) __builtin_amdgcn_s_sleep(8);
+            // backing off by how much is missing: lanes still waiting on many records (a batch launch that
+            // fills the chip, publishers far from done) must not flood the fabric with re-reads while they
+            // stream; the last few records are re-read at once
+            if (__builtin_popcountll(waiting) <= 8) __builtin_amdgcn_s_sleep(1);
             else __builtin_amdgcn_s_sleep(32);
 #pragma unroll
             for (int u = 0; u < kWaveFold; ++u) {
