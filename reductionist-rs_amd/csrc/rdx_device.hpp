@@ -767,7 +767,7 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
 #pragma unroll
         for (int u = 0; u < kWaveFold; ++u) {
             const uint32_t j = threadIdx.x + 64u * u;
-            if (j < nrec) load_record<T, OP>(P + j, g[u], nrec);
+            if (j < nrec) load_record<T, OP>(P + (uint64_t)j * kR, g[u]);
         }
         // Records not yet visible (the folder's own streaming often ends before the last publisher's): every
         // stale granule of the wave is re-read in the same round — one round trip per retry for all of
@@ -780,16 +780,15 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
 #pragma unroll
                 for (int q = 0; q < kR; ++q) stale |= live && (uint32_t)(g[u][q] >> 48) != out.epoch;
             }
-            const uint64_t waiting = __builtin_amdgcn_ballot_w64(stale);
-            if (!waiting) break;
+            if (!__builtin_amdgcn_ballot_w64(stale)) break;
             if (it >= kSpinLimit) {
                 fault = stale ? 1u : 0u;
                 break;
             }
-            // backing off by how much is missing: lanes still waiting on many records (a batch launch that
-            // fills the chip, publishers far from done) must not flood the fabric with re-reads while they
-            // stream; the last few records are re-read at once
-            if (__builtin_popcountll(waiting) <= 8) __builtin_amdgcn_s_sleep(1);
+            // backing off: a folder whose publishers are far from done (a batch launch that fills the chip)
+            // must not flood the fabric with re-reads while they stream
+            if (it < 2) __builtin_amdgcn_s_sleep(1);
+            else if (it < 6) __builtin_amdgcn_s_sleep(8);
             else __builtin_amdgcn_s_sleep(32);
 #pragma unroll
             for (int u = 0; u < kWaveFold; ++u) {
@@ -797,7 +796,7 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
 #pragma unroll
                 for (int q = 0; q < kR; ++q)
                     if (j < nrec && (uint32_t)(g[u][q] >> 48) != out.epoch)
-                        g[u][q] = __hip_atomic_load(P + (uint64_t)q * nrec + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        g[u][q] = __hip_atomic_load(P + (uint64_t)j * kR + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
 #pragma unroll
@@ -819,13 +818,13 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
     for (uint32_t j0 = threadIdx.x; j0 < nrec; j0 += 2 * kBlock) {
         const uint32_t j1 = j0 + kBlock;
         uint64_t g0[kMaxGranules] = {}, g1[kMaxGranules] = {};
-        load_record<T, OP>(P + j0, g0, nrec);
-        if (j1 < nrec) load_record<T, OP>(P + j1, g1, nrec);
+        load_record<T, OP>(P + (uint64_t)j0 * kR, g0);
+        if (j1 < nrec) load_record<T, OP>(P + (uint64_t)j1 * kR, g1);
         Red<T, OP> o;
-        accept_record<T, OP>(P + j0, g0, o, out.epoch, fault, nrec);
+        accept_record<T, OP>(P + (uint64_t)j0 * kR, g0, o, out.epoch, fault);
         acc.merge(o);
         if (j1 < nrec) {
-            accept_record<T, OP>(P + j1, g1, o, out.epoch, fault, nrec);
+            accept_record<T, OP>(P + (uint64_t)j1 * kR, g1, o, out.epoch, fault);
             acc.merge(o);
         }
     }
@@ -876,9 +875,7 @@ __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uin
 #else
     constexpr bool drop = false;
 #endif
-    // granule-major records (granule q of block b at P[q * bpc + b]): the folder's loads of one granule
-    // for 64 consecutive records are one contiguous 512-byte read instead of 64 scattered ones
-    if (threadIdx.x == 0 && !drop) publish<T, OP>(out.partials + (uint64_t)chunk * bpc * kR + b, r, out.epoch, bpc);
+    if (threadIdx.x == 0 && !drop) publish<T, OP>(out.partials + ((uint64_t)chunk * bpc + b) * kR, r, out.epoch);
     if (out.fold_last && b != bpc - 1) {   // only the folder goes on (no arrival to count)
         RDX_STAMP(2);
         return;

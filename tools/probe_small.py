@@ -51,6 +51,23 @@ for op in ("min", "sum"):
     creq = _abi.CRequest(op, "float64", shape=[128, 128, 128], selection=sel, missing_kind="missing_value",
                          missing_values=np.float64(-9999.0).tobytes(), n_missing=1)
     print(json.dumps({"cfg": f"c3_{op}", "bpc": bpc, "us": round(dev_time(creq, c3, 128 ** 3 * 8) * 1e6, 2)}))
+creq = _abi.CRequest("min", "float64", shape=[128, 128, 128], selection=sel, missing_kind="missing_value",
+                     missing_values=np.float64(-9999.0).tobytes(), n_missing=1)
+out = torch.zeros(20, dtype=torch.float64, device="cuda")
+cnt = torch.zeros(20, dtype=torch.int64, device="cuda")
+stt = torch.zeros(20, dtype=torch.int32, device="cuda")
+ptrs = [b.data_ptr() for b in c3]
+for i in range(5):
+    ws.execute_batch_device(creq, ptrs, 128 ** 3 * 8, out.data_ptr(), cnt.data_ptr(), stt.data_ptr(), stream.cuda_stream)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(stream)
+for i in range(50):
+    ws.execute_batch_device(creq, ptrs, 128 ** 3 * 8, out.data_ptr(), cnt.data_ptr(), stt.data_ptr(), stream.cuda_stream)
+e1.record(stream)
+torch.cuda.synchronize()
+assert int(stt.abs().sum()) == 0
+print(json.dumps({"cfg": "c3_min_batch20", "bpc": bpc, "us": round(e0.elapsed_time(e1) / 50 * 1e3, 2)}))
 creq = _abi.CRequest("min", "float64", selection=[[0, 688128, 1]], shape=[128 ** 3])
 print(json.dumps({"cfg": "c3sized_contig_min", "bpc": bpc, "us": round(dev_time(creq, c3, 128 ** 3 * 8) * 1e6, 2)}))
 v1 = rng.random(1 << 20, dtype=np.float32)
