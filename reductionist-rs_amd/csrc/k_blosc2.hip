@@ -498,6 +498,28 @@ struct LzStream {
 // (RDX_BLOSC2_UNSUPPORTED: the host decodes that chunk); neither are dictionaries (a failure, as libzstd).
 constexpr uint32_t kZHufMax = 11;   // Max_Number_of_Bits
 
+// Probe builds: per-row phase cycles of k_blosc2_zstd (s_memtime) and event counts, read back by
+// rdx_probe_zprof_read: [0] row total, [1] literals section, [2] sequence tables, [3] sequence loop,
+// [4] of which literal copies, [5] of which match copies, [6] sequences, [7] far match steps,
+// [8] literal bytes (regenerated), [9] match bytes, [10] ring flushes, [11] compressed blocks.
+#if RDX_PROBES
+constexpr uint32_t kZProfRows = 4096, kZProfK = 12;
+static __device__ uint64_t g_zprof[kZProfRows * kZProfK];
+#define ZP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define ZP_ADD(k, v) prof[k] += __builtin_amdgcn_s_memtime() - (v)
+#define ZP_CNT(k, x) prof[k] += (x)
+#else
+#define ZP_T(v) \
+    do {        \
+    } while (0)
+#define ZP_ADD(k, v) \
+    do {             \
+    } while (0)
+#define ZP_CNT(k, x) \
+    do {             \
+    } while (0)
+#endif
+
 struct __attribute__((aligned(16))) ZLds {
     WaveLds w;                                   // output ring + staged literal source
     uint32_t ll[512], of[256], ml[512];          // FSE decode entries: symbol | nb << 8 | base << 16
@@ -614,6 +636,9 @@ struct ZDec {
     bool pre_ll = false, pre_of = false, pre_ml = false;   // the LDS table holds the predefined distribution
     uint32_t huf_bits = 0, ll_log = 0, of_log = 0, ml_log = 0;
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+#if RDX_PROBES
+    uint64_t prof[kZProfK] = {};
+#endif
 
     // FSE decode table from a per-lane distribution (lane s: symbol s's normalised count; nsym <= 64):
     // the spread by one lane's LDS stores, then the states' bits / baselines in order with the per-symbol
@@ -809,49 +834,76 @@ struct ZDec {
 #undef put
     }
 
-    // One Huffman stream of `count` symbols into dst[0..count) (consumed exactly)
-    __device__ __forceinline__ bool huf_stream(const uint8_t *p, uint64_t n, uint8_t *dst, uint64_t count) {
-        ZBits b;
-        if (!b.init_back(p, n, lane)) return false;
-        const uint32_t mb = huf_bits;
-        for (uint64_t i = 0; i < count; ++i) {
-            const int64_t save = b.off;
-            const uint32_t idx = b.get(mb);
-            const uint32_t e = rfl((uint32_t)Z.huf[idx]);
-            b.off = save - (int64_t)(e >> 8);
-            if (b.off < 0) return false;
-            if (lane == 0) gst<uint8_t>(dst + i, (uint8_t)e);
-        }
-        return b.off == 0;
-    }
-
-    // Four Huffman streams side by side (4X literals): one symbol of each per step, their four table
-    // reads in flight together, and one byte store per step (lane k stores stream k's symbol).
-    __device__ __forceinline__ bool huf_stream4(const uint8_t *d, uint64_t s1, uint64_t s2, uint64_t s3, uint64_t s4,
-                                                uint8_t *dst, uint64_t seg, uint64_t last) {
-        ZBits b0, b1, b2, b3;
-        if (!b0.init_back(d, s1, lane) || !b1.init_back(d + s1, s2, lane) || !b2.init_back(d + s1 + s2, s3, lane) ||
-            !b3.init_back(d + s1 + s2 + s3, s4, lane))
-            return false;
-        const uint32_t mb = huf_bits;
-        uint8_t *mine = dst + (uint64_t)(lane & 3) * seg;
+    // Huffman literal streams, decoded SIMT-style: 1X in lane 0, 4X in lanes 0-3 (stream k in lane k, one
+    // symbol of each per step).  Each lane keeps its own backward bit position and reads its stream from a
+    // 512-byte LDS window (its quarter of the staged-input area, which the sequences restage afterwards);
+    // the whole wave restages the windows when any lane's next read would fall below its own.  Table reads
+    // are per-lane LDS gathers, symbols per-lane byte stores.  (The first form ran one wave-uniform bit
+    // reader per stream in scalar code: ~500 cycles per literal byte, profiles/r03_zstd_phase_probe.jsonl.)
+    // Stream k is [d + o_k, d + o_k + n_k) with o_k the sum of the lengths before it; it yields `seg`
+    // symbols (stream 3 of 4X: `last`), consumed exactly.
+    __device__ __forceinline__ bool huf_lanes(const uint8_t *d, uint32_t ns, uint32_t s1, uint32_t s2, uint32_t s3,
+                                              uint32_t s4, uint8_t *dst, uint32_t seg, uint32_t last) {
+        const uint32_t k = lane & 3;
+        const bool mine = lane < ns;
+        const uint32_t o_k = k == 0 ? 0u : k == 1 ? s1 : k == 2 ? s1 + s2 : s1 + s2 + s3;
+        const uint32_t n_k = k == 0 ? s1 : k == 1 ? s2 : k == 2 ? s3 : s4;
+        const uint32_t cnt = !mine ? 0u : (ns == 1 || k < 3 ? seg : last);
         bool bad = false;
-        for (uint64_t i = 0; i < seg; ++i) {
-            const bool has3 = i < last;
-            const int64_t v0 = b0.off, v1 = b1.off, v2 = b2.off, v3 = b3.off;
-            const uint32_t i0 = b0.get(mb), i1 = b1.get(mb), i2 = b2.get(mb), i3 = has3 ? b3.get(mb) : 0u;
-            const uint32_t e0 = rfl((uint32_t)Z.huf[i0]), e1 = rfl((uint32_t)Z.huf[i1]), e2 = rfl((uint32_t)Z.huf[i2]),
-                           e3 = rfl((uint32_t)Z.huf[i3]);
-            b0.off = v0 - (int64_t)(e0 >> 8);
-            b1.off = v1 - (int64_t)(e1 >> 8);
-            b2.off = v2 - (int64_t)(e2 >> 8);
-            b3.off = has3 ? v3 - (int64_t)(e3 >> 8) : v3;
-            bad |= (b0.off < 0) | (b1.off < 0) | (b2.off < 0) | (b3.off < 0);
-            const uint32_t v = lane == 0 ? e0 : lane == 1 ? e1 : lane == 2 ? e2 : e3;
-            if (lane < 3 || (lane == 3 && has3)) gst<uint8_t>(mine + i, (uint8_t)v);
-            if (bad) return false;
+        int32_t pos = 0;
+        if (mine) {   // below the last byte's highest set bit
+            const uint32_t lb = n_k ? (uint32_t)gld<uint8_t>(d + o_k + n_k - 1) : 0u;
+            if (lb == 0) bad = true;
+            else pos = (int32_t)(8 * n_k) - (int32_t)(8 - zhibit(lb));
         }
-        return b0.off == 0 && b1.off == 0 && b2.off == 0 && b3.off == 0;
+        if (__builtin_amdgcn_ballot_w64(bad)) return false;
+        const uint32_t mb = rfl(huf_bits);
+        uint32_t *win = Z.w.in;   // stream k: words [128 k, 128 k + 128) = stream bytes [wb, wb + 512)
+        int32_t wb = 1 << 30;     // nothing staged yet
+        uint8_t *out = dst + (uint64_t)k * seg;
+        const uint32_t q = lane >> 4, j = lane & 15;   // restaging: lane copies 32 B of stream q's window
+        const uint32_t o_q = q == 0 ? 0u : q == 1 ? s1 : q == 2 ? s1 + s2 : s1 + s2 + s3;
+        const uint32_t n_q = q == 0 ? s1 : q == 1 ? s2 : q == 2 ? s3 : s4;
+        const uintptr_t lo_w = (uintptr_t)(d + o_q) & ~(uintptr_t)3, hi_b = (uintptr_t)(d + o_q + n_q);
+        for (uint32_t i = 0; i < seg; ++i) {
+            const bool act = i < cnt;
+            const int32_t p = pos - (int32_t)mb, pc = p > 0 ? p : 0;
+            if (__builtin_amdgcn_ballot_w64(act && (pc >> 3) < wb)) {
+                if (mine) {
+                    const int32_t nwb = ((pos + 7) >> 3) - 500;
+                    wb = (nwb > 0 ? nwb : 0) & ~3;
+                }
+                const int32_t wq = __shfl(wb, (int)q, 64);
+                if (q < ns) {
+                    const uint8_t *a = d + o_q + wq + 32 * j;
+                    const uint32_t skew = (uint32_t)((uintptr_t)a & 3);
+                    const uint32_t *aw = reinterpret_cast<const uint32_t *>(a - skew);
+                    uint32_t w[9];
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) {
+                        const uintptr_t ad = (uintptr_t)(aw + t);
+                        w[t] = ad >= lo_w && ad < hi_b ? gld<uint32_t>(aw + t) : 0u;
+                    }
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        win[128 * q + 8 * j + t] = skew ? __builtin_amdgcn_alignbyte(w[t + 1], w[t], skew) : w[t];
+                }
+                wave_sync();
+            }
+            if (act) {
+                const uint32_t wi = (uint32_t)((pc >> 3) - wb) >> 2;
+                const uint64_t qv = (uint64_t)win[128 * k + wi + 1] << 32 | win[128 * k + wi];
+                const uint32_t sh = (uint32_t)(pc - 8 * (wb + 4 * (int32_t)wi));
+                const uint32_t nbits = (uint32_t)(pos - pc);   // mb, or what is left near the stream start
+                const uint32_t v = ((uint32_t)(qv >> sh) & ((1u << nbits) - 1u)) << (uint32_t)(pc - p);
+                const uint32_t e = Z.huf[v];
+                pos -= (int32_t)(e >> 8);
+                bad |= pos < 0;
+                gst<uint8_t>(out + i, (uint8_t)e);
+            }
+            if (__builtin_amdgcn_ballot_w64(bad)) return false;
+        }
+        return __builtin_amdgcn_ballot_w64(mine && pos != 0) == 0;
     }
 
     // a sequence table: mode 0 predefined, 1 RLE, 2 FSE, 3 repeat; bytes used at p (or -1)
@@ -942,6 +994,9 @@ struct ZDec {
         // literals: raw ones stay in the input; decoded ones go to the tail of the output region
         const uint8_t *lit = nullptr;
         uint64_t q = hl;
+        ZP_T(t_lit);
+        ZP_CNT(8, regen);
+        ZP_CNT(11, 1);
         if (regen > (uint64_t)z.n - z.op) return false;
         uint8_t *tail = z.dst + z.n - regen;
         if (ltype == 0) {
@@ -965,7 +1020,7 @@ struct ZDec {
             }
             if (lp > csize) return false;
             if (nstreams == 1) {
-                if (!huf_stream(ls + lp, csize - lp, tail, regen)) return false;
+                if (!huf_lanes(ls + lp, 1, (uint32_t)(csize - lp), 0, 0, 0, tail, (uint32_t)regen, 0)) return false;
             } else {
                 if (csize - lp < 10 || regen < 6) return false;
                 ZBits jt;
@@ -975,7 +1030,9 @@ struct ZDec {
                 const uint64_t total = csize - lp - 6;
                 if (s1 + s2 + s3 > total) return false;
                 const uint64_t s4 = total - s1 - s2 - s3, seg = (regen + 3) / 4;
-                if (!huf_stream4(ls + lp + 6, s1, s2, s3, s4, tail, seg, regen - 3 * seg)) return false;
+                if (!huf_lanes(ls + lp + 6, 4, (uint32_t)s1, (uint32_t)s2, (uint32_t)s3, (uint32_t)s4, tail, (uint32_t)seg,
+                               (uint32_t)(regen - 3 * seg)))
+                    return false;
             }
             lit = tail;
             q += csize;
@@ -985,6 +1042,7 @@ struct ZDec {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         const uint32_t lip = regen ? z.source(lit, (uint32_t)regen) : 0;
+        ZP_ADD(1, t_lit);
         // sequences
         if (q >= n) return false;
         uint64_t nseq = h.byte(q++);
@@ -1003,6 +1061,7 @@ struct ZDec {
             if (q >= n) return false;
             const uint32_t modes = h.byte(q++);
             if (modes & 3) return false;
+            ZP_T(t_tab);
             int64_t u = seq_table(modes >> 6, p + q, n - q, Z.ll, ll_log, have_ll, pre_ll, kZLLDef, 36, 6, 9, 35);
             if (u < 0) return false;
             q += (uint64_t)u;
@@ -1013,6 +1072,9 @@ struct ZDec {
             if (u < 0) return false;
             q += (uint64_t)u;
             if (q >= n) return false;
+            ZP_ADD(2, t_tab);
+            ZP_T(t_seq);
+            ZP_CNT(6, nseq);
             ZBits b;
             if (!b.init_back(p + q, n - q, lane)) return false;
             uint32_t sll = b.get(ll_log), sof = b.get(of_log), sml = b.get(ml_log);
@@ -1059,11 +1121,18 @@ struct ZDec {
                 }
                 if (b.off < 0) return false;
                 if (ll > regen - lpos || ll > (uint64_t)z.n - z.op) return false;
+                ZP_T(t_l);
                 if (ll) z.literals(lip + (uint32_t)lpos, (uint32_t)ll);
+                ZP_ADD(4, t_l);
                 lpos += ll;
                 if (off > (uint64_t)z.op - fstart || ml > (uint64_t)z.n - z.op) return false;
+                ZP_T(t_m);
                 z.match((uint32_t)ml, (uint32_t)off);
+                ZP_ADD(5, t_m);
+                ZP_CNT(9, ml);
+                ZP_CNT(7, off > kRing - 64 ? (ml + 63) / 64 : 0);
             }
+            ZP_ADD(3, t_seq);
             if (b.off != 0) return false;
         } else if (q != n) {
             return false;
@@ -1381,14 +1450,31 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_zstd(const KBlosc2Args a
         zd.z.dst = dst;
         zd.z.n = (uint32_t)cap;
         zd.z.op = zd.z.flushed = 0;
+        ZP_T(t_row);
         const uint32_t e = zd.stream(src, len);
         if (e == 0) zd.z.finish();
         if (lane == 0) {
             a.z_out_len[row] = e == 0 ? zd.z.op : 0;
             a.z_err[row] = e;
         }
+#if RDX_PROBES
+        zd.prof[0] += __builtin_amdgcn_s_memtime() - t_row;
+        zd.prof[10] = zd.z.flushed / kFlush;
+        if (lane == 0 && r < kZProfRows)
+            for (uint32_t k = 0; k < kZProfK; ++k) g_zprof[r * kZProfK + k] = zd.prof[k];
+#endif
     }
 }
+
+#if RDX_PROBES
+}  // namespace rdx
+// probe builds: k_blosc2_zstd's per-row phase cycles and counts of the last launch (g_zprof above)
+extern "C" int rdx_probe_zprof_read(uint64_t *host, uint32_t n) {
+    if (n > rdx::kZProfRows * rdx::kZProfK) n = rdx::kZProfRows * rdx::kZProfK;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rdx::g_zprof), n * sizeof(uint64_t)) == hipSuccess ? 0 : 1;
+}
+namespace rdx {
+#endif
 
 hipError_t launch_blosc2_zstd(const KBlosc2Args &a, hipStream_t s) {
     if (!a.z_capacity) return hipSuccess;
