@@ -616,6 +616,39 @@ struct ZBits {
     }
 };
 
+// Backward reader with a 64-bit container (the sequence section): c holds the stream's bits [cb - 64, cb),
+// bits below the stream start reading as 0.  A field comes out of the container with 64-bit scalar shifts;
+// the window is touched once per refill (every ~57 bits) instead of once or twice per field.
+struct ZBitC {
+    ZBits b;   // window, skew; b.off = the read position (bits left), negative once overread
+    uint64_t c;
+    int64_t cb;
+    // bytes [B, B + 8) of the stream, B >= 0 (bytes past the window's dwords read as 0)
+    __device__ __forceinline__ uint64_t read8(int64_t B) {
+        const uint64_t a = b.sb + 8 * (uint64_t)B;
+        const int32_t d = (int32_t)(a >> 5);
+        const uint32_t sh = (uint32_t)(a & 31);
+        const uint64_t w01 = (uint64_t)b.win.dw(d, true) | (uint64_t)b.win.dw(d + 1, true) << 32;
+        if (!sh) return w01;
+        return (w01 >> sh) | (uint64_t)b.win.dw(d + 2, true) << (64 - sh);
+    }
+    __device__ __forceinline__ void refill() {
+        const int64_t nb = (b.off + 7) >> 3;   // c = bytes [nb - 8, nb)
+        cb = 8 * nb;
+        const int64_t B = nb - 8;
+        if (B >= 0) c = read8(B);
+        else if (B > -8) c = read8(0) << (8 * (uint32_t)(-B));
+        else c = 0;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t k) {   // k <= 32
+        if (k == 0) return 0;
+        if (b.off - (int64_t)k < cb - 64) refill();
+        b.off -= k;
+        const uint32_t v = (uint32_t)(c >> (uint32_t)(b.off - (cb - 64)));
+        return k >= 32 ? v : v & ((1u << k) - 1u);
+    }
+};
+
 // weight wv of symbol s into lane s % 64 of w[s / 64]
 __device__ __forceinline__ void zput(uint32_t lane, uint32_t s, uint32_t wv, uint32_t &w0, uint32_t &w1, uint32_t &w2,
                                      uint32_t &w3) {
@@ -1075,8 +1108,9 @@ struct ZDec {
             ZP_ADD(2, t_tab);
             ZP_T(t_seq);
             ZP_CNT(6, nseq);
-            ZBits b;
-            if (!b.init_back(p + q, n - q, lane)) return false;
+            ZBitC b;
+            if (!b.b.init_back(p + q, n - q, lane)) return false;
+            b.refill();
             uint32_t sll = b.get(ll_log), sof = b.get(of_log), sml = b.get(ml_log);
             for (uint64_t i = 0; i < nseq; ++i) {
                 const uint32_t ell = rfl(Z.ll[sll]), eof = rfl(Z.of[sof]), eml = rfl(Z.ml[sml]);
@@ -1119,7 +1153,7 @@ struct ZDec {
                     sml = (eml >> 16) + b.get((eml >> 8) & 0xffu);
                     sof = (eof >> 16) + b.get((eof >> 8) & 0xffu);
                 }
-                if (b.off < 0) return false;
+                if (b.b.off < 0) return false;
                 if (ll > regen - lpos || ll > (uint64_t)z.n - z.op) return false;
                 ZP_T(t_l);
                 if (ll) z.literals(lip + (uint32_t)lpos, (uint32_t)ll);
@@ -1133,7 +1167,7 @@ struct ZDec {
                 ZP_CNT(7, off > kRing - 64 ? (ml + 63) / 64 : 0);
             }
             ZP_ADD(3, t_seq);
-            if (b.off != 0) return false;
+            if (b.b.off != 0) return false;
         } else if (q != n) {
             return false;
         }
