@@ -40,10 +40,12 @@ constexpr uint32_t kRing = 8192, kRingMask = kRing - 1, kFlush = kRing / 4;
 constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4, kStage = 1024;
 constexpr uint32_t kUnit = 4096;   // memcpy'ed / special chunks: bytes per work item
 
-struct __attribute__((aligned(16))) WaveLds {
-    uint8_t win[kRing];
+template <uint32_t R>
+struct __attribute__((aligned(16))) WaveLdsT {
+    uint8_t win[R];
     uint32_t in[kInWords];
 };
+using WaveLds = WaveLdsT<kRing>;
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
@@ -195,8 +197,11 @@ __device__ __forceinline__ void wave_fill(uint8_t *dst, uint64_t n, uint8_t v) {
     for (uint64_t i = head + 16 * nq + lane; i < n; i += 64) dst[i] = v;
 }
 
-struct LzStream {
-    WaveLds &L;
+template <uint32_t R>   // output ring bytes (power of two)
+struct LzStreamT {
+    static constexpr uint32_t kR = R, kRM = R - 1, kF = R / 4;
+    static_assert(R >= 4096 && (R & (R - 1)) == 0, "flush() stores 16-byte slices: kF / 64 >= 16");
+    WaveLdsT<R> &L;
     const uint32_t lane;
     const uint32_t *srcw;   // stream as dwords from its 4-byte aligned base
     // positions are 32-bit: a stream is at most a block (BLOSC2_MAXBLOCKSIZE < 2^29), and the token
@@ -245,11 +250,11 @@ struct LzStream {
         return (uint8_t)(L.in[(p >> 2) & (kInWords - 1)] >> ((p & 3) * 8));
     }
 
-    // write [flushed, flushed + m) of the ring to HBM (m <= kFlush)
+    // write [flushed, flushed + m) of the ring to HBM (m <= kF)
     __device__ __forceinline__ void flush(uint32_t m) {
-        constexpr uint32_t kSl = kFlush / 64;
+        constexpr uint32_t kSl = kF / 64;
         wave_sync();
-        const uint32_t base = (uint32_t)(flushed & kRingMask);
+        const uint32_t base = (uint32_t)(flushed & kRM);
         const uint32_t lo = lane * kSl;
         const uint32_t cnt = lo >= m ? 0 : (m - lo < kSl ? m - lo : kSl);
         uint8_t *d = dst + flushed + lo;
@@ -258,7 +263,7 @@ struct LzStream {
             for (uint32_t k = 0; k < kSl / 16; ++k)
                 gst<uint4>(d + 16 * k, *reinterpret_cast<const uint4 *>(&L.win[base + lo + 16 * k]));
         } else {
-            for (uint32_t k = 0; k < cnt; ++k) gst<uint8_t>(d + k, L.win[(base + lo + k) & kRingMask]);
+            for (uint32_t k = 0; k < cnt; ++k) gst<uint8_t>(d + k, L.win[(base + lo + k) & kRM]);
         }
         flushed += m;
         // far match sources read these bytes back: their stores must be in L2 first
@@ -266,7 +271,7 @@ struct LzStream {
         wave_sync();
     }
     __device__ __forceinline__ void room() {
-        if (op - flushed > kRing - 64) flush(kFlush);
+        if (op - flushed > kR - 64) flush(kF);
     }
     __device__ __forceinline__ uint8_t far_byte(uint32_t q) const {
         const uintptr_t a = (uintptr_t)(dst + q);
@@ -280,7 +285,7 @@ struct LzStream {
             ensure(ip + s + 64);
             room();
             const uint32_t k = run - s < 64 ? run - s : 64;
-            if (lane < k) L.win[(op + lane) & kRingMask] = in_byte(ip + s + lane);
+            if (lane < k) L.win[(op + lane) & kRM] = in_byte(ip + s + lane);
             op += k;
             asm volatile("" ::: "memory");
         }
@@ -293,15 +298,15 @@ struct LzStream {
             if (lane < k) {
                 const uint32_t m = dist < 64 ? lane % (uint32_t)dist : lane;
                 const uint32_t back = dist - m, q = op - back;
-                const uint8_t v = back <= kRing - 64 ? L.win[q & kRingMask] : far_byte(q);
-                L.win[(op + lane) & kRingMask] = v;
+                const uint8_t v = back <= kR - 64 ? L.win[q & kRM] : far_byte(q);
+                L.win[(op + lane) & kRM] = v;
             }
             op += k;
             asm volatile("" ::: "memory");
         }
     }
     __device__ __forceinline__ void finish() {
-        while (op > flushed) flush(op - flushed < kFlush ? (uint32_t)(op - flushed) : kFlush);
+        while (op > flushed) flush(op - flushed < kF ? (uint32_t)(op - flushed) : kF);
     }
     // stage a new source (zstd: raw literals in the input, or decoded literals in HBM): `avail` bytes at p;
     // returns the aligned-coordinate position of p's first byte (the ip literals() takes)
@@ -319,7 +324,7 @@ struct LzStream {
         for (uint32_t s = 0; s < len; s += 64) {
             room();
             const uint32_t k = len - s < 64 ? len - s : 64;
-            if (lane < k) L.win[(op + lane) & kRingMask] = b;
+            if (lane < k) L.win[(op + lane) & kRM] = b;
             op += k;
             asm volatile("" ::: "memory");
         }
@@ -485,6 +490,7 @@ struct LzStream {
         return op == want;
     }
 };
+using LzStream = LzStreamT<kRing>;
 
 // ---- zstd (codec 4): RFC 8878, restated from oracle/oracle_zstd.cpp -------------------------------------
 // One wavefront per zstd-coded stream (a row of the stream table, rows [z_capacity, z_capacity + count)),
@@ -520,8 +526,21 @@ static __device__ uint64_t g_zprof[kZProfRows * kZProfK];
     } while (0)
 #endif
 
+// zstd waves: a 4 KiB output ring (matches farther back read the flushed output from HBM) and two waves per
+// workgroup, so the LDS (15.6 KiB per wave) admits 10 waves per CU instead of 8
+#ifndef RDX_ZRING
+#define RDX_ZRING 4096
+#endif
+#ifndef RDX_ZWAVES
+#define RDX_ZWAVES 2
+#endif
+#ifndef RDX_ZWPE
+#define RDX_ZWPE 3
+#endif
+constexpr uint32_t kZRing = RDX_ZRING, kZWaves = RDX_ZWAVES;
+
 struct __attribute__((aligned(16))) ZLds {
-    WaveLds w;                                   // output ring + staged literal source
+    WaveLdsT<kZRing> w;                                  // output ring + staged literal source
     uint32_t ll[512], of[256], ml[512];          // FSE decode entries: symbol | nb << 8 | base << 16
     uint32_t wt[64];                             // the FSE table of the Huffman weights (accuracy <= 6)
     uint16_t huf[1 << kZHufMax];                 // Huffman: symbol | nb << 8
@@ -663,7 +682,7 @@ __device__ __forceinline__ void zput(uint32_t lane, uint32_t s, uint32_t wv, uin
 
 struct ZDec {
     ZLds &Z;
-    LzStream z;   // by value (a reference member kept the stream in scratch and its LDS accesses flat)
+    LzStreamT<kZRing> z;   // by value (a reference member kept the stream in scratch and its LDS accesses flat)
     const uint32_t lane;
     bool have_huf = false, have_ll = false, have_of = false, have_ml = false;
     bool pre_ll = false, pre_of = false, pre_ml = false;   // the LDS table holds the predefined distribution
@@ -1164,7 +1183,7 @@ struct ZDec {
                 z.match((uint32_t)ml, (uint32_t)off);
                 ZP_ADD(5, t_m);
                 ZP_CNT(9, ml);
-                ZP_CNT(7, off > kRing - 64 ? (ml + 63) / 64 : 0);
+                ZP_CNT(7, off > kZRing - 64 ? (ml + 63) / 64 : 0);
             }
             ZP_ADD(3, t_seq);
             if (b.b.off != 0) return false;
@@ -1469,18 +1488,19 @@ __global__ __launch_bounds__(256) void k_blosc2_zcheck(const KBlosc2Args a) {
 }
 
 // zstd rows of the stream table: one wavefront per row, looping over the rows registered by k_blosc2_decode
-__global__ __launch_bounds__(64 * kWaves) void k_blosc2_zstd(const KBlosc2Args a) {
-    __shared__ ZLds LZ[kWaves];
+__global__ __launch_bounds__(64 * kZWaves) __attribute__((amdgpu_waves_per_eu(RDX_ZWPE))) void k_blosc2_zstd(
+    const KBlosc2Args a) {
+    __shared__ ZLds LZ[kZWaves];
     const uint32_t wave = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t cnt = rfl(__hip_atomic_load(a.z_count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const uint64_t n = cnt < a.z_capacity ? cnt : a.z_capacity;
-    for (uint64_t r = (uint64_t)blockIdx.x * kWaves + wave; r < n; r += (uint64_t)gridDim.x * kWaves) {
+    for (uint64_t r = (uint64_t)blockIdx.x * kZWaves + wave; r < n; r += (uint64_t)gridDim.x * kZWaves) {
         const uint64_t row = a.z_capacity + r;
         const uint8_t *src = reinterpret_cast<const uint8_t *>(rfl64((uint64_t)gld<const uint8_t *>(a.z_in + row)));
         const uint64_t len = rfl64(gld<uint64_t>(a.z_len + row));
         uint8_t *dst = reinterpret_cast<uint8_t *>(rfl64((uint64_t)gld<uint8_t *>(a.z_out + row)));
         const uint64_t cap = rfl64(gld<uint64_t>(a.z_cap + row));
-        ZDec zd{LZ[wave], LzStream{LZ[wave].w, lane}, lane};
+        ZDec zd{LZ[wave], LzStreamT<kZRing>{LZ[wave].w, lane}, lane};
         zd.z.dst = dst;
         zd.z.n = (uint32_t)cap;
         zd.z.op = zd.z.flushed = 0;
@@ -1493,7 +1513,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_blosc2_zstd(const KBlosc2Args a
         }
 #if RDX_PROBES
         zd.prof[0] += __builtin_amdgcn_s_memtime() - t_row;
-        zd.prof[10] = zd.z.flushed / kFlush;
+        zd.prof[10] = zd.z.flushed / (kZRing / 4);
         if (lane == 0 && r < kZProfRows)
             for (uint32_t k = 0; k < kZProfK; ++k) g_zprof[r * kZProfK + k] = zd.prof[k];
 #endif
@@ -1512,8 +1532,8 @@ namespace rdx {
 
 hipError_t launch_blosc2_zstd(const KBlosc2Args &a, hipStream_t s) {
     if (!a.z_capacity) return hipSuccess;
-    const uint64_t wgs = std::min<uint64_t>((a.z_capacity + kWaves - 1) / kWaves, 1024);   // workgroups loop over rows
-    hipLaunchKernelGGL(k_blosc2_zstd, dim3((uint32_t)wgs), dim3(64 * kWaves), 0, s, a);
+    const uint64_t wgs = std::min<uint64_t>((a.z_capacity + kZWaves - 1) / kZWaves, 2048);   // workgroups loop over rows
+    hipLaunchKernelGGL(k_blosc2_zstd, dim3((uint32_t)wgs), dim3(64 * kZWaves), 0, s, a);
     return hipGetLastError();
 }
 
