@@ -66,6 +66,9 @@ def main():
     a = np.frombuffer(buf, dtype=np.uint64).reshape(rows, K).astype(np.float64)
     print(json.dumps({"case": "lone", "block": bs, "chunk_bytes": len(chunk), "lone_ms": round(lone_ms, 3),
                       "rows": rows, "max_row_cycles": int(a[:, 0].max())}), flush=True)
+    order = np.argsort(-a[:, 0])
+    for r in list(order[:4]) + list(order[rows // 2:rows // 2 + 2]):
+        print(json.dumps({"case": "row", "row": int(r), **{nm: int(a[r, k]) for k, nm in enumerate(NAMES)}}), flush=True)
     for plane in range(4):
         sel = a[np.arange(rows) % 4 == plane]
         rec = {"case": "plane", "plane": plane}
