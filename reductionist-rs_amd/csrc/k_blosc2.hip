@@ -636,20 +636,44 @@ struct ZBits {
 };
 
 // Backward reader with a 64-bit container (the sequence section): c holds the stream's bits [cb - 64, cb),
-// bits below the stream start reading as 0.  A field comes out of the container with 64-bit scalar shifts;
-// the window is touched once per refill (every ~57 bits) instead of once or twice per field.
+// bits below the stream start reading as 0.  A field comes out of the container with 64-bit shifts; a
+// refill (every ~57 bits) reads three dwords of a 256-byte LDS window of the stream (the Huffman weights'
+// table area, free once the literals are decoded), which the wave restages when the read position leaves it.
 struct ZBitC {
-    ZBits b;   // window, skew; b.off = the read position (bits left), negative once overread
+    ZBits b;   // init_back only; b.off = the read position (bits left), negative once overread
     uint64_t c;
     int64_t cb;
-    // bytes [B, B + 8) of the stream, B >= 0 (bytes past the window's dwords read as 0)
-    __device__ __forceinline__ uint64_t read8(int64_t B) {
-        const uint64_t a = b.sb + 8 * (uint64_t)B;
-        const int32_t d = (int32_t)(a >> 5);
-        const uint32_t sh = (uint32_t)(a & 31);
-        const uint64_t w01 = (uint64_t)b.win.dw(d, true) | (uint64_t)b.win.dw(d + 1, true) << 32;
+    const uint8_t *sp;   // the stream [sp, sp + sn)
+    uint32_t sn;
+    uint32_t *lw;        // LDS: stream bytes [wb, wb + 256)
+    int32_t wb;
+    __device__ __forceinline__ void setup(const uint8_t *p, uint32_t n, uint32_t *lds) {
+        sp = p;
+        sn = n;
+        lw = lds;
+        wb = 1 << 30;   // nothing staged
+    }
+    __device__ __forceinline__ void stage(int32_t B) {
+        const int32_t nw = B - 240;
+        wb = (nw > 0 ? nw : 0) & ~3;
+        const uint32_t lane = b.win.lane;
+        const uint8_t *a = sp + wb;
+        const uint32_t sk = (uint32_t)((uintptr_t)a & 3);
+        const uint32_t *aw = reinterpret_cast<const uint32_t *>(a - sk) + lane;
+        const uintptr_t lo_w = (uintptr_t)sp & ~(uintptr_t)3, hi_b = (uintptr_t)(sp + sn);
+        const uint32_t w0 = (uintptr_t)aw >= lo_w && (uintptr_t)aw < hi_b ? gld<uint32_t>(aw) : 0u;
+        const uint32_t w1 = (uintptr_t)(aw + 1) >= lo_w && (uintptr_t)(aw + 1) < hi_b ? gld<uint32_t>(aw + 1) : 0u;
+        lw[lane] = sk ? __builtin_amdgcn_alignbyte(w1, w0, sk) : w0;
+        wave_sync();
+    }
+    // bytes [B, B + 8) of the stream, B >= 0
+    __device__ __forceinline__ uint64_t read8(int64_t B64) {
+        const int32_t B = (int32_t)B64;
+        if (B < wb || B + 12 > wb + 256) stage(B);
+        const uint32_t rel = (uint32_t)(B - wb), i = rel >> 2, sh = (rel & 3) * 8;
+        const uint64_t w01 = (uint64_t)lw[i] | (uint64_t)lw[i + 1] << 32;
         if (!sh) return w01;
-        return (w01 >> sh) | (uint64_t)b.win.dw(d + 2, true) << (64 - sh);
+        return (w01 >> sh) | (uint64_t)lw[i + 2] << (64 - sh);
     }
     __device__ __forceinline__ void refill() {
         const int64_t nb = (b.off + 7) >> 3;   // c = bytes [nb - 8, nb)
@@ -1129,6 +1153,7 @@ struct ZDec {
             ZP_CNT(6, nseq);
             ZBitC b;
             if (!b.b.init_back(p + q, n - q, lane)) return false;
+            b.setup(p + q, (uint32_t)(n - q), Z.wt);
             b.refill();
             uint32_t sll = b.get(ll_log), sof = b.get(of_log), sml = b.get(ml_log);
             for (uint64_t i = 0; i < nseq; ++i) {
