@@ -296,7 +296,10 @@ struct LzStreamT {
             room();
             const uint32_t k = len - s < 64 ? len - s : 64;
             if (lane < k) {
-                const uint32_t m = dist < 64 ? lane % (uint32_t)dist : lane;
+                // lane % dist for dist < 64 without an integer division: (lane + 0.5) / dist stays >= 0.5 / 63
+                // away from an integer, far beyond v_rcp_f32's error
+                const uint32_t m =
+                    dist < 64 ? lane - dist * (uint32_t)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)dist)) : lane;
                 const uint32_t back = dist - m, q = op - back;
                 const uint8_t v = back <= kR - 64 ? L.win[q & kRM] : far_byte(q);
                 L.win[(op + lane) & kRM] = v;
@@ -1157,7 +1160,10 @@ struct ZDec {
             b.refill();
             uint32_t sll = b.get(ll_log), sof = b.get(of_log), sml = b.get(ml_log);
             for (uint64_t i = 0; i < nseq; ++i) {
-                const uint32_t ell = rfl(Z.ll[sll]), eof = rfl(Z.of[sof]), eml = rfl(Z.ml[sml]);
+                // the three table reads issued together (the scheduler otherwise waits on each before the next)
+                const uint32_t rll = Z.ll[sll], rof = Z.of[sof], rml = Z.ml[sml];
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t ell = rfl(rll), eof = rfl(rof), eml = rfl(rml);
                 const uint32_t ofc = eof & 0xffu, mlc = eml & 0xffu, llc = ell & 0xffu;
                 if (ofc > 31 || mlc > 52 || llc > 35) return false;
                 uint64_t ofv = (1ull << ofc);
