@@ -207,7 +207,8 @@ typedef struct rdx_context_config {
     uint64_t coalesce_max_bytes;    /* rdx_execute_resident chunks up to this many bytes coalesce (0: 64 MiB)  */
     uint64_t coalesce_host_max_bytes; /* rdx_execute / _owned host chunks up to this many (0: 1 MiB)           */
 } rdx_context_config;
-/* Applies to requests issued after it returns (call it before the context is shared). */
+/* Call it before the context is shared: once a request has been placed the configuration is frozen and
+ * this returns RDX_E_INVALID_ARGUMENT (the dispatchers and the placement read it without a lock). */
 rdx_status rdx_context_configure(rdx_context *ctx, const rdx_context_config *cfg);
 
 /* Bookkeeping of pool entry `index` (0 .. n_devices-1). */
@@ -221,6 +222,13 @@ typedef struct rdx_device_stats {
     uint64_t coalesced_launches;    /* k_multi launches issued by the coalescer                               */
     uint64_t outstanding_bytes;     /* chunk bytes of the requests in flight on this entry now                */
     uint64_t waits;                 /* requests that waited for a free workspace                              */
+    uint64_t direct_requests;       /* coalescible requests that found the coalescer idle and launched on the
+                                       caller's own thread (the idle-queue fast path; not in coalesced_*)      */
+    uint64_t placed_bytes;          /* chunk bytes of all requests placed on this entry (the placement key,
+                                       summed over time)                                                       */
+    uint64_t peak_outstanding_bytes;/* high-water mark of outstanding_bytes (each request weighs its chunk
+                                       bytes + 64 KiB): least-outstanding placement keeps it near
+                                       ceil(concurrent requests / entries) requests' weight                    */
 } rdx_device_stats;
 rdx_status rdx_context_stats(rdx_context *ctx, uint32_t index, rdx_device_stats *out);
 

@@ -182,6 +182,9 @@ pub struct RdxDeviceStats {
     pub coalesced_launches: u64,
     pub outstanding_bytes: u64,
     pub waits: u64,
+    pub direct_requests: u64,
+    pub placed_bytes: u64,
+    pub peak_outstanding_bytes: u64,
 }
 
 pub enum RdxContext {}
@@ -330,7 +333,7 @@ const _: () = assert!(size_of::<RdxResponseInfo>() == 280);
 const _: () = assert!(size_of::<RdxMultiItem>() == 48);
 const _: () = assert!(size_of::<RdxResult>() == 312);
 const _: () = assert!(size_of::<RdxContextConfig>() == 32);
-const _: () = assert!(size_of::<RdxDeviceStats>() == 56);
+const _: () = assert!(size_of::<RdxDeviceStats>() == 80);
 const _: () = assert!(offset_of!(RdxContextConfig, coalesce_max_bytes) == 16);
 const _: () = assert!(offset_of!(RdxDeviceStats, requests) == 16);
 const _: () = assert!(offset_of!(RdxRequest, op) == 4);

@@ -77,6 +77,11 @@ struct Tuning {
     int fold_last = env_int("RDX_FOLD_LAST", 1);                       // A/B: 0 = arrival counters everywhere
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
+    int direct_max = env_int("RDX_DIRECT_MAX", 1);                     // idle-queue fast path: callers launching at once
+    int idle_passes = env_int("RDX_DISPATCH_IDLE_PASSES", 512);        // dispatcher: empty polls before it naps
+#if RDX_PROBES
+    int epoch_start = env_int("RDX_EPOCH_START", 0);                   // tests: start workspaces' tags near the wrap
+#endif
 };
 
 const Tuning &tuning() {
@@ -131,6 +136,9 @@ struct rdx_workspace {
     DevBuf<uint8_t> cbor;
     DevBuf<uint64_t> cbor_len;
     uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
+    // the coalescer's idle-queue fast path: this workspace's own page-locked result slots (a one-request
+    // lane launched on the caller's thread; rdx_device.hpp put_host_slot)
+    uint64_t *h_slot = nullptr;
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
     hipEvent_t piece_ev[8] = {};
@@ -177,9 +185,13 @@ struct Job {
     void *h_body = nullptr;        // host destinations
     int64_t *h_counts = nullptr;
     rdx_status st = RDX_OK;
-    std::atomic<uint32_t> done{0};       // futex word: 0 pending, 1 done
-    std::atomic<uint32_t> sleeping{0};   // the caller gave up spinning and waits on the futex
+    // futex word: kJobPending -> (the caller gives up spinning) kJobSleeping -> kJobDone.  Whoever completes
+    // the job writes `st` and the outputs, then exchanges kJobDone in; after that exchange it touches no
+    // field of the Job (the caller may already have returned and its stack frame be reused): a wake-up
+    // passes only the word's address to the kernel.
+    std::atomic<uint32_t> state{0};
 };
+constexpr uint32_t kJobPending = 0, kJobSleeping = 1, kJobDone = 2;
 
 // One entry of the context's device pool.
 struct PoolEntry {
@@ -200,6 +212,10 @@ struct PoolEntry {
     uint64_t n_launch = 0, n_done = 0;
     std::atomic<uint64_t> outstanding{0};        // chunk bytes in flight (placement key)
     uint64_t requests = 0, coalesced = 0, launches = 0, waits = 0;
+    uint32_t direct_active = 0;                  // idle-queue fast-path launches in flight (<= RDX_DIRECT_MAX)
+    uint64_t direct = 0;                         // requests served by the fast path
+    uint64_t placed_bytes = 0;                   // chunk bytes placed here, cumulative
+    uint64_t peak_outstanding = 0;               // high-water mark of `outstanding`
 };
 
 }  // namespace
@@ -210,6 +226,7 @@ struct rdx_context {
     rdx_context_config cfg{};
     std::mutex mu;                               // the pinned response pool
     std::atomic<uint64_t> rr{0};                 // tie-break start of the placement scan
+    std::atomic<bool> served{false};             // a request has been placed: the configuration is frozen
     // page-locked response buffers of rdx_execute_owned (size class -> free blocks; block -> class)
     std::map<uint64_t, std::vector<void *>> pinned_free;
     std::map<void *, uint64_t> pinned_class;
@@ -710,6 +727,9 @@ rdx_status create_workspace(int device, rdx_workspace **out) {
     auto *ws = new (std::nothrow) rdx_workspace();
     if (!ws) return RDX_E_OUT_OF_MEMORY;
     ws->device = device;
+#if RDX_PROBES
+    if (tuning().epoch_start > 0) ws->epoch = (uint32_t)std::min(tuning().epoch_start, 0xffff);
+#endif
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ws->cus = prop.multiProcessorCount;
@@ -762,6 +782,7 @@ void destroy_workspace(rdx_workspace *ws) {
     for (hipEvent_t e : ws->piece_ev)
         if (e) (void)hipEventDestroy(e);
     if (ws->zback) (void)hipHostFree(ws->zback);
+    if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
     if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
@@ -1383,9 +1404,12 @@ bool place(rdx_context *ctx, uint64_t bytes, int device, Placement &pl) {
     if (best == n) return false;
     pl.e = ctx->entries[best].get();
     pl.weight = bytes + (64u << 10);
-    pl.e->outstanding.fetch_add(pl.weight, std::memory_order_relaxed);
+    const uint64_t now = pl.e->outstanding.fetch_add(pl.weight, std::memory_order_relaxed) + pl.weight;
+    if (!ctx->served.load(std::memory_order_relaxed)) ctx->served.store(true, std::memory_order_relaxed);
     std::lock_guard<std::mutex> g(pl.e->mu);
     ++pl.e->requests;
+    pl.e->placed_bytes += bytes;
+    pl.e->peak_outstanding = std::max(pl.e->peak_outstanding, now);
     return true;
 }
 
@@ -1407,10 +1431,14 @@ struct WsLease {
     }
 };
 
-rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease) {
+const rdx_status kBusy = static_cast<rdx_status>(255);   // internal: no workspace free right now
+
+// `wait` false: kBusy instead of waiting when every workspace is busy (the fast path's try).
+rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease, bool wait = true) {
     std::unique_lock<std::mutex> lk(e.mu);
     bool waited = false;
     while (e.free_ws.empty() && e.all_ws.size() + e.creating >= ctx->cfg.max_workspaces) {
+        if (!wait) return kBusy;
         if (!waited) ++e.waits;
         waited = true;
         e.ws_cv.wait(lk);
@@ -1541,27 +1569,30 @@ rdx_status launch_lane(Lane &L) {
     return RDX_OK;
 }
 
-// Completion: the result is in the caller's buffers; release it, and wake it only if it is asleep
-// (seq_cst on both sides: either the caller sees `done` before it sleeps, or this sees `sleeping`).
+// Completion: the result is in the caller's buffers; release it, and wake it only if it is asleep.  One
+// atomic word: the exchange both publishes the result and tells whether the caller went to sleep, and it
+// is the last access to the Job (the futex wake-up names the address; it reads no memory there).
 void finish_job(Job &j, rdx_status st) {
     j.st = st;
-    j.done.store(1, std::memory_order_seq_cst);
-    if (j.sleeping.load(std::memory_order_seq_cst))
-        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&j.done), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    uint32_t *const word = reinterpret_cast<uint32_t *>(&j.state);
+    if (j.state.exchange(kJobDone, std::memory_order_acq_rel) == kJobSleeping)
+        syscall(SYS_futex, word, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
 }
 
 // The caller's wait: spin (no system call: a result arrives within tens of microseconds of its launch),
-// then sleep on the futex (RDX_WAIT_SPIN iterations of the spin; 0 = sleep at once).
+// then announce the sleep with a CAS pending -> sleeping and sleep on the futex (RDX_WAIT_SPIN iterations
+// of the spin; 0 = sleep at once).  A failed CAS means the job is done.
 void wait_job(Job &j) {
     const int spin = tuning().wait_spin;
     for (int i = 0; i < spin; ++i) {
-        if (j.done.load(std::memory_order_acquire)) return;
+        if (j.state.load(std::memory_order_acquire) == kJobDone) return;
         __builtin_ia32_pause();
     }
-    j.sleeping.store(1, std::memory_order_seq_cst);
-    while (!j.done.load(std::memory_order_seq_cst)) {
+    uint32_t expect = kJobPending;
+    if (!j.state.compare_exchange_strong(expect, kJobSleeping, std::memory_order_acq_rel)) return;
+    while (j.state.load(std::memory_order_acquire) != kJobDone) {
         const timespec ts{0, 1000000};   // re-check every millisecond whatever happens
-        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&j.done), FUTEX_WAIT_PRIVATE, 0, &ts, nullptr, 0);
+        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&j.state), FUTEX_WAIT_PRIVATE, kJobSleeping, &ts, nullptr, 0);
     }
 }
 
@@ -1643,7 +1674,7 @@ void form_batch(std::deque<Job *> &pending, Lane &L) {
 void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
     (void)hipSetDevice(e->device);
     std::deque<Job *> pending;
-    uint32_t in_flight = 0;
+    uint32_t in_flight = 0, idle = 0;
     for (;;) {
         {
             std::unique_lock<std::mutex> lk(e->mu);
@@ -1721,8 +1752,65 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
             }
             if (l->remaining != before) progressed = true;
         }
-        if (!progressed) std::this_thread::yield();
+        // nothing arrived and nothing completed: yield, and after RDX_DISPATCH_IDLE_PASSES such passes in a
+        // row (a long launch in flight) nap between polls instead of keeping a core busy
+        if (progressed) {
+            idle = 0;
+        } else if (++idle < (uint32_t)tuning().idle_passes) {
+            std::this_thread::yield();
+        } else {
+            const timespec ts{0, 20000};
+            nanosleep(&ts, nullptr);
+        }
     }
+}
+
+// The idle-queue fast path: a coalescible request arriving while its entry's coalescer has nothing queued
+// does not hand over to the dispatcher thread (a wake-up, a launch, a completion and a wake-up: 21-33 us
+// at one caller where a direct launch takes 16-18 us).  The caller launches it itself as a one-request
+// batched launch on its own workspace's stream — the same kernels and the same tagged page-locked result
+// slot as a coalescer lane (rdx_device.hpp put_host_slot) — and spins on the slot.  At most RDX_DIRECT_MAX
+// callers per entry take it at once; the rest (a loaded server) queue and coalesce.
+bool claim_direct(PoolEntry &e) {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!e.jobs.empty() || e.direct_active >= (uint32_t)std::max(0, tuning().direct_max)) return false;
+    ++e.direct_active;
+    return true;
+}
+
+void release_direct(PoolEntry &e, bool served) {
+    std::lock_guard<std::mutex> g(e.mu);
+    --e.direct_active;
+    if (served) ++e.direct;
+}
+
+rdx_status run_direct(rdx_workspace *ws, Job &job) {
+    RDX_HIP(hipSetDevice(ws->device));
+    constexpr size_t slot_bytes = kTableChunks * kSlotWords * sizeof(uint64_t);
+    if (!ws->h_slot) {
+        void *p = nullptr;
+        RDX_HIP(hipHostMalloc(&p, slot_bytes, hipHostMallocCoherent));
+        std::memset(p, 0, slot_bytes);
+        ws->h_slot = static_cast<uint64_t *>(p);
+    }
+    Lane L;   // a one-request lane over the caller's workspace
+    L.ws = ws;
+    L.owns_ws = false;
+    L.h_res = ws->h_slot;
+    L.group = true;
+    L.batch[0] = &job;
+    L.n = 1;
+    rdx_status st = launch_lane(L);
+    if (st) return st;
+    // the slot's tag arrives with the fold; the stream query (every 64th poll) catches a launch that ended
+    // without writing it (a device fault: RDX_E_DEVICE)
+    for (uint32_t polls = 1;; ++polls) {
+        const bool kernel_done = polls % 64 == 0 && hipStreamQuery(ws->own_stream) != hipErrorNotReady;
+        if (poll_lane(L, kernel_done)) break;
+        if (polls < 4096) __builtin_ia32_pause();
+        else std::this_thread::yield();
+    }
+    return job.st;
 }
 
 // Queue the request on its entry's coalescer and wait for its result (spinning: the result comes back
@@ -1815,7 +1903,18 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
     };
     if (resident) {
         Job job;
-        if (coalescible(chunk, job)) return coalesce(ctx, entry, job);
+        if (coalescible(chunk, job)) {
+            if (claim_direct(entry)) {
+                WsLease lease;
+                if (acquire_ws(ctx, entry, lease, false) == RDX_OK) {
+                    st = run_direct(lease.ws, job);
+                    release_direct(entry, true);
+                    return st;
+                }
+                release_direct(entry, false);
+            }
+            return coalesce(ctx, entry, job);
+        }
     }
     WsLease lease;
     if ((st = acquire_ws(ctx, entry, lease))) return st;
@@ -1836,8 +1935,13 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
             src = ws->chunk.p;
             Job job;
-            if (coalescible(src, job)) {   // the chunk is in HBM once the copy completes
-                RDX_HIP(hipStreamSynchronize(s));
+            if (coalescible(src, job)) {
+                if (claim_direct(entry)) {   // launched behind the copy on the same stream
+                    r = run_direct(ws, job);
+                    release_direct(entry, true);
+                    return r;
+                }
+                RDX_HIP(hipStreamSynchronize(s));   // the chunk is in HBM once the copy completes
                 return coalesce(ctx, entry, job);
             }
         }
@@ -2063,6 +2167,9 @@ rdx_status rdx_execute_resident(rdx_context *ctx, int device, const rdx_request 
 
 rdx_status rdx_context_configure(rdx_context *ctx, const rdx_context_config *cfg) {
     if (!ctx || !cfg || cfg->coalesce > 1) return RDX_E_INVALID_ARGUMENT;
+    // the dispatchers, the placement and acquire_ws read the configuration without a lock: it is frozen
+    // once the first request has been placed (rdx.h: configure before the context is shared)
+    if (ctx->served.load(std::memory_order_relaxed)) return RDX_E_INVALID_ARGUMENT;
     ctx->cfg = effective_config(*cfg);
     return RDX_OK;
 }
@@ -2081,6 +2188,9 @@ rdx_status rdx_context_stats(rdx_context *ctx, uint32_t index, rdx_device_stats 
     out->coalesced_launches = e.launches;
     out->outstanding_bytes = e.outstanding.load(std::memory_order_relaxed);
     out->waits = e.waits;
+    out->direct_requests = e.direct;
+    out->placed_bytes = e.placed_bytes;
+    out->peak_outstanding_bytes = e.peak_outstanding;
     return RDX_OK;
 }
 

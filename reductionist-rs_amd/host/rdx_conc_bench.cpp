@@ -2,17 +2,21 @@
 // issues them — one process (app_state.rs:21-37), every Tokio / Rayon worker running one request at a time
 // to completion (src/app.rs:147-152, thread_limit = num_cpus - 1, src/app_state.rs:22).
 //
-//   rdx_conc_bench <config c1|c2|c3|c4> <threads> <requests per thread> [path] [devices] [lanes]
+//   rdx_conc_bench <config c1|c2|c3|c4|s1> <threads> <requests per thread> [path] [devices] [lanes]
+//     config  s1: a 1 MiB f32 contiguous sum (a host chunk at the default coalesce_host_max_bytes)
 //     path    device:   each thread its own rdx_workspace + stream, rdx_execute_device on an HBM-resident
 //                       chunk + a stream synchronize (independent launches; round-2 form)
 //             resident: rdx_execute_resident on an HBM-resident chunk, response into host memory; small
 //                       all-axes requests coalesce into shared k_multi launches (the context's pool)
 //             host:     rdx_execute from page-locked host chunks (PCIe-bound)
+//             owned:    rdx_execute_owned from page-locked host chunks (the plugin's own call: the response in
+//                       a pooled page-locked block, freed after each request)
 //     devices comma-separated HIP ordinals of ONE context (default 0): the in-process multi-GPU server;
 //             host / resident requests are placed by the pool (least outstanding bytes)
 //     lanes   coalescer launches in flight per device (default: the engine's)
 // Chunks rotate over buffers larger than the Infinity Cache (per device).  Prints one JSON line.
 #include <hip/hip_runtime.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <atomic>
@@ -65,6 +69,11 @@ static Config make_config(const std::string &n) {
         c.filters = {{RDX_FILTER_SHUFFLE, 0, 4}};
         c.bytes = 64u << 20;
         c.alg_bytes = c.bytes;
+    } else if (n == "s1") {  // a small chunk: 1 MiB f32, native order, sum
+        c.op = RDX_OP_SUM;
+        c.dtype = RDX_DTYPE_FLOAT32;
+        c.bytes = 1u << 20;
+        c.alg_bytes = c.bytes;
     } else if (n == "c4") {  // configs[3]'s chunk: f32 4 MiB, shuffle es=4, native order, sum
         c.op = RDX_OP_SUM;
         c.dtype = RDX_DTYPE_FLOAT32;
@@ -94,7 +103,8 @@ int main(int argc, char **argv) {
     const int T = std::max(1, std::atoi(argv[2]));
     const int R = std::max(1, std::atoi(argv[3]));
     const std::string path = argc > 4 ? argv[4] : "device";
-    const bool host = path == "host", resident = path == "resident";
+    const bool owned = path == "owned";
+    const bool host = path == "host" || owned, resident = path == "resident";
     std::vector<int> devs;
     {
         std::stringstream ss(argc > 5 ? argv[5] : "0");
@@ -185,7 +195,11 @@ int main(int argc, char **argv) {
             const int k = (i * T + t) % nbuf;
             rdx_response_info out{};
             rdx_status st;
-            if (host) {
+            if (owned) {
+                rdx_result *r = nullptr;
+                st = rdx_execute_owned(ctx, &req, bufs[0][k], cfg.bytes, &r);
+                if (st == RDX_OK) rdx_result_free(ctx, r);
+            } else if (host) {
                 st = rdx_execute(ctx, &req, bufs[0][k], cfg.bytes, body.data(), body.size(), counts.data(), counts.size(),
                                  &out);
             } else if (resident) {
@@ -218,15 +232,21 @@ int main(int argc, char **argv) {
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) th.emplace_back(worker, t);
     while (ready.load() < T) std::this_thread::yield();
+    rusage ru0{}, ru1{};
+    getrusage(RUSAGE_SELF, &ru0);
     go.store(true, std::memory_order_release);
     for (auto &x : th) x.join();
+    getrusage(RUSAGE_SELF, &ru1);
+    auto tv = [](const timeval &t) { return t.tv_sec * 1e6 + t.tv_usec; };
+    // host CPU time of the whole process over the timed region (callers, dispatchers, HIP's threads)
+    const double cpu_us = tv(ru1.ru_utime) - tv(ru0.ru_utime) + tv(ru1.ru_stime) - tv(ru0.ru_stime);
     // the timed region: from the start signal to the last thread's last completed request (teardown excluded)
     double el = 0;
     for (double v : per_thread_us) el = std::max(el, v * R / 1e6);
     const double reqs = (double)T * R;
     double lat = 0;
     for (double v : per_thread_us) lat += v / T;
-    uint64_t creq = 0, claunch = 0, waits = 0, wsn = 0;
+    uint64_t creq = 0, claunch = 0, waits = 0, wsn = 0, direct = 0;
     std::string per_dev;
     for (int d = 0; d < D; ++d) {
         rdx_device_stats st{};
@@ -234,21 +254,24 @@ int main(int argc, char **argv) {
             creq += st.coalesced_requests;
             claunch += st.coalesced_launches;
             waits += st.waits;
+            direct += st.direct_requests;
             wsn += st.workspaces;
             per_dev += (d ? "," : "") + std::to_string(st.requests);
         }
     }
-    const char *pname = host ? "rdx_execute (page-locked host chunk)"
+    const char *pname = owned ? "rdx_execute_owned (page-locked host chunk)"
+                        : host ? "rdx_execute (page-locked host chunk)"
                         : resident ? "rdx_execute_resident (coalesced)" : "rdx_execute_device + synchronize";
     std::printf("{\"config\": \"%s\", \"path\": \"%s\", \"devices\": %d, \"threads\": %d, \"requests\": %.0f, "
                 "\"requests_per_s\": %.1f, \"us_per_request_aggregate\": %.3f, \"us_per_request_per_thread\": %.3f, "
                 "\"GBs_alg\": %.1f, \"GiBs_chunk\": %.1f, \"roofline_frac\": %.4f, \"coalesced_requests\": %llu, "
-                "\"coalesced_launches\": %llu, \"workspaces\": %llu, \"waits\": %llu, \"requests_per_device\": [%s], "
-                "\"errors\": %d}\n",
+                "\"coalesced_launches\": %llu, \"direct_requests\": %llu, \"workspaces\": %llu, \"waits\": %llu, "
+                "\"requests_per_device\": [%s], \"cpu_us_per_request\": %.2f, \"cpu_cores_busy\": %.2f, \"errors\": %d}\n",
                 cfg.name.c_str(), pname, D, T, reqs, reqs / el, el / reqs * 1e6, lat, reqs * cfg.alg_bytes / el / 1e9,
                 reqs * cfg.bytes / el / (1024.0 * 1024 * 1024), reqs * cfg.alg_bytes / el / 1e9 / (8000.0 * D),
-                (unsigned long long)creq, (unsigned long long)claunch, (unsigned long long)wsn,
-                (unsigned long long)waits, per_dev.c_str(), errors.load());
+                (unsigned long long)creq, (unsigned long long)claunch, (unsigned long long)direct,
+                (unsigned long long)wsn, (unsigned long long)waits, per_dev.c_str(), cpu_us / reqs, cpu_us / (el * 1e6),
+                errors.load());
     for (size_t d = 0; d < bufs.size(); ++d)
         for (auto &b : bufs[d]) {
             if (host) rdx_host_free(ctx, b);

@@ -100,7 +100,9 @@ class rdx_context_config(C.Structure):
 class rdx_device_stats(C.Structure):
     _fields_ = [("device", C.c_int32), ("workspaces", C.c_uint32), ("workspaces_busy", C.c_uint32),
                 ("max_workspaces", C.c_uint32), ("requests", C.c_uint64), ("coalesced_requests", C.c_uint64),
-                ("coalesced_launches", C.c_uint64), ("outstanding_bytes", C.c_uint64), ("waits", C.c_uint64)]
+                ("coalesced_launches", C.c_uint64), ("outstanding_bytes", C.c_uint64), ("waits", C.c_uint64),
+                ("direct_requests", C.c_uint64), ("placed_bytes", C.c_uint64),
+                ("peak_outstanding_bytes", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -113,7 +113,8 @@ def test_resident_threads_coalesce_bit_exact(torch, lanes):
         _check_one(case, *r)
     s = eng.stats(0)
     assert s["requests"] == _plannable(cases) and s["outstanding_bytes"] == 0 and s["workspaces_busy"] == 0
-    assert 0 < s["coalesced_requests"] < s["requests"]        # all-axes ones only (axis / select run alone)
+    assert 0 < s["coalesced_requests"] + s["direct_requests"] < s["requests"]   # all-axes ones only
+    assert s["coalesced_requests"] > 0                        # 8 callers: the queue is not always idle
     assert 0 < s["coalesced_launches"] <= s["coalesced_requests"]
     eng.close()
 
@@ -143,7 +144,7 @@ def test_resident_large_allaxes_and_c_shapes(torch):
         for case, r in zip(cases, res):
             _check_one(case, *r)
         s = eng.stats(0)
-        assert s["coalesced_requests"] == (len(cases) if coalesce else 0)
+        assert s["coalesced_requests"] + s["direct_requests"] == (len(cases) if coalesce else 0)
         eng.close()
 
 
@@ -199,6 +200,7 @@ def test_back_pressure_one_workspace(torch):
         _check_one(case, *r)
     s = eng.stats(0)
     assert s["workspaces"] == 1 and s["max_workspaces"] == 1 and s["waits"] > 0 and s["coalesced_requests"] == 0
+    assert s["direct_requests"] == 0
     eng.close()
 
 
@@ -246,5 +248,121 @@ def test_resident_same_plan_groups(torch):
     for case, r in zip(cases, res):
         _check_one(case, *r)
     s = eng.stats(0)
-    assert s["coalesced_requests"] == len(cases) and s["coalesced_launches"] < len(cases)
+    assert s["coalesced_requests"] + s["direct_requests"] == len(cases)
+    assert s["coalesced_launches"] + s["direct_requests"] < len(cases)
+    eng.close()
+
+
+def _config_cases():
+    """Distinct chunks of the BASELINE request shapes with their oracle results: C1 (f32 4 MiB sum, D-int),
+    C3 (f64 [128,128,128] hyperslab min / max, missing_value -9999 at 5 %) and C4's chunk (f32 4 MiB
+    shuffled sum, D-int)."""
+    cases = []
+    for i in range(4):
+        v1 = np.random.default_rng(0x5EED0001 + 32 * i).integers(-8, 9, 1 << 20).astype(np.float32)
+        creq = _abi.CRequest("sum", "float32")
+        cases.append(("sum", {}, v1.tobytes(), creq, oracle.execute(creq, v1.tobytes())))
+        rng = np.random.default_rng(0x5EED0005 + 32 * i)
+        v3 = rng.standard_normal(128 ** 3) * 100
+        v3[rng.random(v3.size) < 0.05] = -9999.0
+        req = {"dtype": "float64", "shape": [128, 128, 128], "selection": [[8, 120, 1], [0, 128, 2], [16, 112, 1]],
+               "missing": {"missing_value": -9999.0}}
+        op = "min" if i % 2 == 0 else "max"
+        creq = make_request(op, req, oracle.convert)
+        cases.append((op, req, v3.tobytes(), creq, oracle.execute(creq, v3.tobytes())))
+        v4 = np.random.default_rng(0x5EED1000 + i).integers(-8, 9, 1 << 20).astype(np.float32)
+        req = {"dtype": "float32", "filters": [{"id": "shuffle", "element_size": 4}]}
+        data = oracle.shuffle(v4.tobytes(), 4)
+        creq = make_request("sum", req, oracle.convert)
+        cases.append(("sum", req, data, creq, oracle.execute(creq, data)))
+    return cases
+
+
+def test_direct_path_single_caller(torch):
+    """One caller at a time (a lightly loaded server): every coalescible request finds the coalescer idle and
+    launches on the caller's own thread (the idle-queue fast path, rdx_device_stats.direct_requests), for
+    resident chunks and for host chunks up to coalesce_host_max_bytes; bit-exact vs the oracle, and no
+    coalesced launch is issued."""
+    eng = Engine([0])
+    conf = _config_cases()
+    cases = conf + _cases(7800, 120, allaxes_only=True)
+    bufs = _to_device(torch, cases)
+    for i, case in enumerate(cases):
+        _check_one(case, *eng.execute_resident(case[3], 0, bufs[i].data_ptr(), len(case[2])))
+        if i == len(conf) - 1:
+            assert eng.stats(0)["direct_requests"] == len(conf)
+    s = eng.stats(0)
+    assert s["requests"] == _plannable(cases) and s["coalesced_requests"] == 0 and s["coalesced_launches"] == 0
+    assert s["direct_requests"] > len(conf), s
+    small = [c for c in cases if len(c[2]) <= 1 << 20]
+    for case in small:
+        _check_one(case, *eng.execute_raw(case[3], case[2]))
+    s2 = eng.stats(0)
+    assert s2["direct_requests"] > s["direct_requests"] and s2["coalesced_requests"] == 0
+    assert s2["workspaces_busy"] == 0 and s2["outstanding_bytes"] == 0
+    eng.close()
+
+
+@pytest.mark.parametrize("n_threads", [15, 60])
+def test_pool_eight_entries_one_gpu(torch, n_threads):
+    """rdx_context_create([0] * 8): the shape an 8-GPU node runs (app_state.rs:21-37, one pool entry per
+    device), here eight entries on one GPU — eight dispatcher threads, placement over eight entries, teardown.
+
+    Mixed: 15 / 60 threads of C1 / C3 / C4 requests, resident and (every fifth) from host memory, each
+    bit-exact vs the oracle, every entry used.
+    Balance.  Placement keys on OUTSTANDING bytes (resource_manager.rs:54-89 bounds memory in flight), so
+    what it balances is work in flight, not cumulative bytes: an entry whose requests finish more slowly
+    (here: streams of eight entries share the GPU's 4 hardware queues) is given fewer.  The bound it keeps:
+    a request goes to the entry with the least in flight, so with T callers no entry ever holds more than
+    ceil(T / 8) requests' weight, plus one for placements racing on the relaxed loads.  Uniform (the
+    server's shape: every chunk arrives in host memory, chunk_store.rs:124-150): C4 chunks from host memory
+    at 15 threads, every entry's peak_outstanding_bytes <= 3 x (4 MiB + 64 KiB), and every entry serves.
+    The context is destroyed with the dispatchers idle and returns."""
+    eng = Engine([0] * 8)
+    base = _config_cases()
+    bufs = _to_device(torch, base)
+    n_req = 40 * n_threads if n_threads <= 15 else 16 * n_threads
+    work = [(i % len(base), i % 5 == 4) for i in range(n_req)]        # every fifth from host memory
+
+    def one(w):
+        k, host = w
+        case = base[k]
+        r = eng.execute_raw(case[3], case[2]) if host else \
+            eng.execute_resident(case[3], 0, bufs[k].data_ptr(), len(case[2]))
+        return k, r
+
+    def placed(before=None):
+        st = [eng.stats(i) for i in range(8)]
+        b = [s["placed_bytes"] for s in st]
+        return st, (b if before is None else [x - y for x, y in zip(b, before)])
+
+    res = _threaded(n_threads, work, one)
+    for k, r in res:
+        _check_one(base[k], *r)
+    stats, pb = placed()
+    reqs = [s["requests"] for s in stats]
+    assert sum(reqs) == n_req and sum(pb) == sum(len(base[k][2]) for k, _ in work)
+    mean = sum(pb) / 8
+    print("mixed: requests per entry", reqs, "placed MiB", [round(b / 2**20) for b in pb])
+    assert all(r > 0 for r in reqs) and all(0.25 * mean <= b <= 2.5 * mean for b in pb), (reqs, pb)
+    assert all(s["device"] == 0 and s["workspaces_busy"] == 0 and s["outstanding_bytes"] == 0 for s in stats)
+    assert all(s["workspaces"] <= s["max_workspaces"] for s in stats)
+    assert sum(s["coalesced_requests"] + s["direct_requests"] for s in stats) > 0
+
+    c4 = [k for k in range(len(base)) if base[k][1].get("filters")]
+    uni = [(c4[i % len(c4)], True) for i in range(1500)]
+    res = _threaded(15, uni, one)
+    for k, r in res:
+        _check_one(base[k], *r)
+    eng.close()
+    eng = Engine([0] * 8)
+    res = _threaded(15, uni, one)
+    for k, r in res:
+        _check_one(base[k], *r)
+    st2, pb2 = placed()
+    peaks = [s["peak_outstanding_bytes"] for s in st2]
+    weight = (4 << 20) + (64 << 10)
+    print("uniform host C4: placed MiB", [round(b / 2**20) for b in pb2], "peak in flight (requests)",
+          [round(p / weight, 2) for p in peaks])
+    assert all(b > 0 for b in pb2) and all(p <= 3 * weight for p in peaks), (pb2, peaks)
     eng.close()
