@@ -313,6 +313,24 @@ def leg_c2(cx):
     if args.primary_only:
         return out
     extra = out["extra"]
+    # the same number of steps again, each launch between its own pair of HIP events: the spread of the
+    # per-launch kernel time behind the timed region's average (the first steps after the warm-up, the
+    # box's run-to-run variation)
+    evs = [cx.events() for _ in range(args.steps)]
+    cx.barrier()
+    torch.cuda.synchronize()
+    for i in range(args.steps):
+        evs[i][0].record(cx.stream)
+        batch_step(i)
+        evs[i][1].record(cx.stream)
+    torch.cuda.synchronize()
+    per = [round(a.elapsed_time(b) * 1e3, 2) for a, b in evs]
+    srt = sorted(per)
+    extra["headline_per_step"] = {
+        "kernel_us": per, "min_us": srt[0], "median_us": srt[len(srt) // 2], "max_us": srt[-1],
+        "timed_region_avg_us": round(kern_avg_s * 1e6, 3),
+        "note": "one event pair per launch over --steps launches after the timed region (same chunks, same stream)"}
+    check_results()
     for i in range(max(args.warmup, N_BUF)):   # every chunk at least once, whatever --warmup is
         single_step(i)
     check_results()
@@ -509,6 +527,65 @@ def leg_inflate(cx, with_cpu, n_total=1024, distinct=16, reps=3):
         out["cpu_baseline"] = {"value": round(n_total * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
                                "kind": "library", "sample": f"CPython zlib.decompress of all {n_total} streams on a "
                                                             f"{threads}-thread pool, {tz:.2f} s"}
+    out["lone"] = leg_inflate_lone(cx, streams, raws, with_cpu)
+    return out
+
+
+def leg_inflate_lone(cx, streams, raws, with_cpu, reps=20):
+    """ONE compressed request (compression.rs:60-82): a lone 4 MiB zlib level-1 chunk of the c4z data decoded
+    by the whole device (k_pinflate: block starts found, blocks and the symbols inside them decoded in
+    parallel), against one host core's zlib (the reference decodes a request on its own thread).  Device:
+    rdx_decompress_one_device on the HBM-resident stream, wall clock per synchronous call (two host round
+    trips included), median of `reps`.  End to end: rdx_execute_owned of the compressed chunk as the plugin
+    sends it (shuffled f32 sum: H2D of the compressed bytes, device decode, unshuffle + sum, result back)
+    against the former route (host zlib on the request's thread, then rdx_execute_owned of the raw chunk)."""
+    import zlib
+    import numpy as np
+    torch, _abi = cx.torch, cx.abi
+    s, raw = streams[0], raws[0]
+    d_in = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
+    d_out = torch.empty(len(raw) + 16, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    err, n, path = cx.ws.decompress_one_device("zlib", d_in.data_ptr(), len(s), d_out.data_ptr(), len(raw) + 16)
+    assert err == 0 and n == len(raw) and path == 2, (err, n, path)
+    assert d_out[:n].cpu().numpy().tobytes() == raw
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        cx.ws.decompress_one_device("zlib", d_in.data_ptr(), len(s), d_out.data_ptr(), len(raw) + 16)
+        ts.append(time.perf_counter() - t0)
+    dev = float(np.median(ts))
+    out = {"workload": "one 4 MiB shuffled N(0,1) f32 chunk, zlib level 1 (ratio %.3f: 191 stored + 20 Huffman "
+                       "blocks), decoded by the whole device (k_pinflate)" % (len(raw) / len(s)),
+           "device_ms": round(dev * 1e3, 3), "device_GBs": round(len(raw) / dev / 1e9, 2),
+           "timing": "rdx_decompress_one_device on the HBM-resident stream, wall clock per synchronous call, "
+                     f"median of {reps}", "path": "k_pinflate (rdx_inflate_last_path 2)"}
+    creq = _abi.CRequest("sum", "float32", filters=[{"id": "shuffle", "element_size": 4}], compression="zlib")
+    creq_raw = _abi.CRequest("sum", "float32", filters=[{"id": "shuffle", "element_size": 4}])
+    st, *_ = cx.eng.execute_owned(creq, s)
+    assert st == 0
+    te, tr = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        st, *_ = cx.eng.execute_owned(creq, s)
+        te.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        st2, *_ = cx.eng.execute_owned(creq_raw, zlib.decompress(s))
+        tr.append(time.perf_counter() - t0)
+        assert st == st2 == 0
+    out["request_device_decode_ms"] = round(1e3 * float(np.median(te)), 3)
+    out["request_host_decode_ms"] = round(1e3 * float(np.median(tr)), 3)
+    if with_cpu:
+        hs = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            zlib.decompress(s)
+            hs.append(time.perf_counter() - t0)
+        host = float(np.median(hs))
+        out["cpu_baseline"] = {"value": round(host * 1e3, 3), "unit": "ms per chunk", "cores": 1, "kind": "library",
+                               "sample": f"CPython zlib.decompress (the C library) of the same stream on one thread, "
+                                         f"median of {reps}", "GBs": round(len(raw) / host / 1e9, 2)}
+        out["speedup_vs_one_core"] = round(host / dev, 2)
     return out
 
 
@@ -630,6 +707,29 @@ def leg_blosc2(cx, with_cpu, n_total=1024, distinct=16, reps=3):
         for i in range(20):
             zone(i)
         lone_cpu = (time.perf_counter() - t1) / 20
+        # LZ4: the real liblz4 (the system's liblz4.so.1: LZ4_decompress_safe, c-blosc2's LZ4 codec) on the
+        # lz4_lib chunks' streams, then the block unshuffle (oracle/cpu_baselines.cpp, -O3 -mavx2), on the same
+        # pool over all chunks, and one chunk on one thread
+        if L.cpu_lz4lib_available():
+            lchunks = chunks_by_codec["lz4_lib"]
+            keep = [C.create_string_buffer(c, len(c)) for c in lchunks]
+            cp = (C.c_void_p * distinct)(*[C.cast(k, C.c_void_p) for k in keep])
+            cl = (C.c_uint64 * distinct)(*[len(c) for c in lchunks])
+            sec, nb = C.c_double(), C.c_uint64()
+            res = {}
+            for mode in (1, 0):
+                assert L.cpu_blosc2_lz4lib(cp, cl, C.c_uint64(distinct), C.c_uint64(n_total), C.c_uint32(threads),
+                                           C.c_uint64(raw_len), mode, C.byref(sec), C.byref(nb)) == 0
+                res[mode] = n_total * raw_len / sec.value / 1e9
+            assert L.cpu_blosc2_lz4lib(cp, cl, C.c_uint64(distinct), C.c_uint64(20), C.c_uint32(1),
+                                       C.c_uint64(raw_len), 1, C.byref(sec), C.byref(nb)) == 0
+            out["cpu_baseline_lz4_lib"] = {
+                "value": round(res[1], 2), "unit": "GB/s", "cores": threads, "kind": "library",
+                "sample": f"the real liblz4 (liblz4.so.1 LZ4_decompress_safe) on the lz4_lib chunks' streams + the "
+                          f"block unshuffle (oracle/cpu_baselines.cpp, -O3 -mavx2), all {n_total} chunks on a "
+                          f"{threads}-thread pool; device leg to compare: lz4_lib",
+                "lz4_streams_only_GBs": round(res[0], 2),
+                "lone_chunk_one_thread_us": round(sec.value / 20 * 1e6, 1)}
         out["cpu_baseline_zstd"] = {"value": round(sample * raw_len / tz / 1e9, 2), "unit": "GB/s", "cores": threads,
                                     "kind": "library", "sample": f"the real libzstd (pyarrow's bundled codec) on "
                                                                  f"the zstd streams of {sample} chunks, each chunk's "
@@ -1085,8 +1185,8 @@ def cpu_baseline_c4(threads, distinct=256):
         list(ex.map(one, range(C4_CHUNKS)))
         el = time.perf_counter() - t0
     return {"value": round(C4_CHUNKS * 4 * C4_ELEMS / el / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "port", "sample": f"all {C4_CHUNKS} chunks ({distinct} distinct = {distinct * 4} MiB, cycled: "
-                                      f"not cache-resident), {threads} worker threads, oracle g++ -O2, {el:.2f} s"}
+            "kind": "port", "sample": f"all {C4_CHUNKS} chunks ({distinct} distinct = {distinct * 4} MiB, cycled), "
+                                      f"{threads} worker threads, oracle g++ -O2, {el:.2f} s"}
 
 
 def devices_used(cx):
@@ -1150,6 +1250,9 @@ def main():
         extra["c4_batch"] = leg_c4(cx)
         if solo and not args.no_cpu_baseline:
             extra["c4_batch"]["cpu_baseline"] = cpu_baseline_c4(pool_threads())
+            # the same with 64 distinct chunks (256 MiB: a chunk the downloader has just written is often
+            # still in the host's L3); the headline ratios in DESIGN.md use the DRAM-bound value above
+            extra["c4_batch"]["cpu_baseline_cache_resident"] = cpu_baseline_c4(pool_threads(), distinct=64)
     if not args.no_f64:
         steps = max(10, args.steps // 4)
         extra["f64_64mib"] = leg_f64(cx, 8 * 1024 * 1024, N_BUF, steps)

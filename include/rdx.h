@@ -246,6 +246,17 @@ rdx_status rdx_missing_from_f64(uint32_t dtype, double v, void *out);
 /* Message for an rdx_inflate_error, and the detail of this thread's last RDX_E_DECOMPRESSION. */
 const char *rdx_inflate_error_string(uint32_t code);
 uint32_t rdx_inflate_last_error(void);
+/* How this thread's last compressed request was decompressed: a lone gzip / zlib stream is decoded by the
+ * whole device (k_pinflate: block starts found, blocks and the symbols inside them decoded in parallel);
+ * a stream that path does not accept (errors, a block chain it cannot follow) is decoded again by the
+ * sequential k_inflate, whose result and error are the reference's. */
+typedef enum rdx_inflate_path {
+    RDX_INFLATE_PATH_NONE = 0,
+    RDX_INFLATE_PATH_SERIAL = 1,            /* k_inflate (one wavefront per stream) / k_blosc2             */
+    RDX_INFLATE_PATH_PARALLEL = 2,          /* k_pinflate                                                   */
+    RDX_INFLATE_PATH_PARALLEL_FALLBACK = 3  /* k_pinflate declined, then k_inflate                          */
+} rdx_inflate_path;
+uint32_t rdx_inflate_last_path(void);
 /* The rdx_unsupported_reason of this thread's last RDX_E_UNSUPPORTED. */
 uint32_t rdx_last_unsupported_reason(void);
 /* blosc2_cbuffer_sizes (src/compression.rs:33, blusc 0.0.2 / c-blosc2): the sizes a blosc chunk's
@@ -373,6 +384,16 @@ rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, 
                                        const void *const *h_in_ptrs, const uint64_t *h_in_lens,
                                        void *d_out, uint64_t out_capacity,
                                        uint64_t *d_out_lens, uint32_t *d_errors, void *stream);
+
+/* One device-resident gzip / zlib stream (d_in, len bytes), decoded by the whole device — the lone
+ * compressed request of compression.rs:60-82 (k_pinflate; a stream it does not accept is decoded by
+ * k_inflate, whose result and error are the reference's) — SYNCHRONOUSLY on `stream`.  *out_len (host) =
+ * the decompressed size; *error (host) = rdx_inflate_error: RDX_INFLATE_OUTPUT_OVERFLOW when that size
+ * exceeds out_cap (nothing written), else the bytes are in d_out.  rdx_inflate_last_path() tells which
+ * decoder produced them. */
+rdx_status rdx_decompress_one_device(rdx_workspace *ws, uint32_t compression, const void *d_in, uint64_t len,
+                                     void *d_out, uint64_t out_cap, uint64_t *out_len, uint32_t *error,
+                                     void *stream);
 
 /* ---- response serialisation ------------------------------------------------------------------- *
  * The HTTP body of a successful request: serde_cbor::to_vec(&CBORResponse::new(&response))

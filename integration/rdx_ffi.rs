@@ -22,6 +22,8 @@
 //!                                     new: device-resident, batched and heterogeneous entry points
 //!   rdx_decompress_batch_device       compression.rs:18-27 `decompress` for a batch of device streams
 //!   rdx_inflate_last_error / _string  the detail of RDX_E_DECOMPRESSION (error.rs:33-41)
+//!   rdx_decompress_one_device         compression.rs:60-82 for ONE device stream, decoded by the whole device
+//!   rdx_inflate_last_path             which decoder ran (k_pinflate, or k_inflate after it declined)
 //!   rdx_last_unsupported_reason       the cause of RDX_E_UNSUPPORTED: a blosc2 codec (host decompression)
 //!                                     or a request only the reference CPU path plans (operations.rs)
 //!   rdx_execute_cbor                  app.rs:163-183 + app.rs:33-40: the response leaves the engine as
@@ -206,6 +208,7 @@ extern "C" {
     pub fn rdx_missing_from_f64(dtype: u32, v: f64, out: *mut c_void) -> c_int;
     pub fn rdx_inflate_error_string(code: u32) -> *const c_char;
     pub fn rdx_inflate_last_error() -> u32;
+    pub fn rdx_inflate_last_path() -> u32;
     pub fn rdx_last_unsupported_reason() -> u32;
     pub fn rdx_blosc2_cbuffer_sizes(
         src: *const c_void,
@@ -287,6 +290,17 @@ extern "C" {
         stream: *mut c_void,
         statuses: *mut u32,
         infos: *mut RdxResponseInfo,
+    ) -> c_int;
+    pub fn rdx_decompress_one_device(
+        ws: *mut RdxWorkspace,
+        compression: u32,
+        d_in: *const c_void,
+        len: u64,
+        d_out: *mut c_void,
+        out_cap: u64,
+        out_len: *mut u64,
+        error: *mut u32,
+        stream: *mut c_void,
     ) -> c_int;
     pub fn rdx_decompress_batch_device(
         ws: *mut RdxWorkspace,

@@ -1,0 +1,1259 @@
+// k_pinflate — ONE gzip / zlib stream decoded by the whole chip: a lone compressed request
+// (src/filter_pipeline.rs:23-25 -> src/compression.rs:60-82; the reference's docs name decompression the
+// heaviest stage, docs/architecture.md:225-228).  k_inflate decodes a batch of streams one wavefront
+// each; on a single stream that leaves one wavefront busy for 100-220 ms per 4 MiB.  Here the DEFLATE
+// blocks of the stream, and the symbols inside each block, are decoded in parallel:
+//
+//  1. k_pinf_find   every bit offset is tested for a dynamic-Huffman block header as a zlib encoder writes
+//                   it (BTYPE 2, HLIT / HDIST in range, a complete code-length code, a complete literal /
+//                   length code with an end-of-block code, a complete or one-code distance code) and every
+//                   byte offset for a stored block (LEN = ~NLEN, zero bits before it): the candidates
+//                   (every such block start, plus rare false ones).
+//  2. k_pinf_block  one workgroup per candidate parses its header with the oracle's checks, builds the
+//                   decode tables in LDS and decodes the block body with 256 lanes at once: lane k starts
+//                   at an arbitrary bit of the body (Huffman decoding resynchronises within a few
+//                   symbols), stops at its first symbol boundary past its range, and is valid once its
+//                   start equals the exit of lane k-1; a mismatched lane re-decodes from that exit, in
+//                   rounds, then by a sequential walk if the data keeps the parses apart.  Per candidate:
+//                   the end-of-block position, the output size, every lane's verified start and bytes.
+//  3. k_pinf_chain  from the stream header, each block's end names the next block's start; the chain of
+//                   candidates to BFINAL is followed (successors by binary search over the sorted
+//                   candidates in LDS) and the output offsets assigned.  A block start that is no
+//                   candidate (a fixed-Huffman block, a header the finder does not accept) goes back to
+//                   the host, which decodes that candidate alone and chains again.
+//  4. k_pinf_emit   one workgroup per chain block re-decodes its lanes from their verified starts and
+//                   writes every output byte as a 32-bit SOURCE: a literal (flag | byte) or the position
+//                   the byte copies (o - dist; inside an overlapping match, (j mod dist) into the bytes
+//                   before it).
+//  5. k_pinf_resolve  pointer jumping over the sources, in place (each pass chases up to 16 links per
+//                   byte; a link always points to a byte with the same final value), until every byte is
+//                   a literal.
+//  6. k_pinf_finish / k_pinf_check  the bytes, Adler-32 / CRC-32 over segments combined by weights /
+//                   GF(2) shifts, the trailer.
+//
+// The path only ever ACCEPTS a stream the sequential decoder accepts, with the same bytes: any error on
+// the chain, a chain that cannot be followed, an unresolved byte or a checksum mismatch reports "not
+// decoded" and the host runs k_inflate on the stream, which gives the exact error (oracle_inflate).
+#include <algorithm>
+
+#include "rdx_device.hpp"
+#include "rdx_kernels.hpp"
+#include "rdx_pinflate.h"
+
+namespace rdx {
+namespace {
+
+constexpr uint32_t kLanes = kPinfLanes;    // decode lanes (threads) per block
+#ifndef RDX_PINF_MINBITS
+#define RDX_PINF_MINBITS 512
+#endif
+constexpr uint64_t kMinLaneBits = RDX_PINF_MINBITS;   // a lane's share of a block body, at least
+constexpr uint32_t kRoot = 10, kDRoot = 8; // LDS root tables: literal/length, distance
+constexpr uint32_t kFlag = 0x80000000u;    // a source that is a literal byte
+constexpr uint32_t kRounds = 6;            // resync rounds before a sequential walk
+constexpr uint64_t kMaxSpan = 1ull << 21;  // bits a candidate may decode (a zlib block is < 1.6 M bits)
+constexpr uint32_t kWinDwords = 8192;      // LDS window of the stream per block workgroup (32 KiB)
+
+// decode-table entry: value in bits 0-15, code length 16-19 (0: longer than the root), extra bits 20-23,
+// type 24-25 (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol)
+constexpr uint32_t kTyLen = 1u << 24, kTyEob = 2u << 24, kTyBad = 3u << 24;
+
+__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                     193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// ---- the stream as dwords from its 4-byte aligned base (bit positions in those coordinates) ------------
+struct Stream {
+    const uint32_t *w;
+    uint64_t nw;        // dwords holding stream bytes
+    uint32_t lmask;     // valid bytes of the last one
+    // a window of the stream staged in LDS (dwords [l0, l0 + ln)), read instead of L2 where it covers
+    const uint32_t *lds;
+    uint64_t l0;
+    uint32_t ln;
+    __device__ __forceinline__ uint32_t ldg(uint64_t i) const {
+        if (i >= nw) return 0;
+        const uint32_t v = gld<uint32_t>(w + i);
+        return i + 1 == nw ? v & lmask : v;
+    }
+    __device__ __forceinline__ uint32_t ld(uint64_t i) const {
+        const uint64_t k = i - l0;
+        if (k < ln) return lds[k];
+        return ldg(i);
+    }
+    // all threads of the workgroup: stage up to `cap` dwords from dword i0 into `buf`, then read from it
+    __device__ __forceinline__ void stage(uint32_t *buf, uint32_t cap, uint64_t i0, uint64_t i1) {
+        const uint32_t n = (uint32_t)min<uint64_t>(cap, i1 > i0 ? i1 - i0 : 0);
+        for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) buf[k] = ldg(i0 + k);
+        lds = buf;
+        l0 = i0;
+        ln = n;
+        __syncthreads();
+    }
+    // 32 bits from bit position p
+    __device__ __forceinline__ uint32_t at(uint64_t p) const {
+        const uint64_t i = p >> 5;
+        const uint32_t sh = (uint32_t)p & 31;
+        const uint64_t v = (uint64_t)ld(i) | (uint64_t)ld(i + 1) << 32;
+        return (uint32_t)(v >> sh);
+    }
+    __device__ __forceinline__ uint32_t byte(uint64_t q) const { return (ld(q >> 2) >> (8 * (q & 3))) & 0xffu; }
+};
+
+__device__ __forceinline__ Stream make_stream(const PinfArgs &a) {
+    Stream s;
+    s.w = a.w;
+    s.nw = a.nw;
+    s.lmask = a.lmask;
+    s.lds = nullptr;
+    s.l0 = 0;
+    s.ln = 0;
+    return s;
+}
+
+// A lane's bit reader: 64-bit buffer, refilled one dword at a time.
+struct Bits {
+    uint64_t bb;
+    uint32_t bc;
+    uint64_t nxt;
+    __device__ __forceinline__ void seek(const Stream &S, uint64_t p) {
+        nxt = p >> 5;
+        const uint32_t sh = (uint32_t)p & 31;
+        const uint64_t v = (uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32;
+        nxt += 2;
+        bb = v >> sh;
+        bc = 64 - sh;
+    }
+    __device__ __forceinline__ uint64_t pos() const { return nxt * 32 - bc; }
+    __device__ __forceinline__ void refill(const Stream &S) {
+        if (bc <= 32) {
+            bb |= (uint64_t)S.ld(nxt++) << bc;
+            bc += 32;
+        }
+    }
+    __device__ __forceinline__ void drop(uint32_t n) {
+        bb >>= n;
+        bc -= n;
+    }
+};
+
+// ---- Huffman tables in LDS --------------------------------------------------------------------------
+struct Tabs {
+    uint32_t lit[1u << kRoot];
+    uint32_t dist[1u << kDRoot];
+    uint16_t lcount[16], dcount[16];
+    uint16_t lsym[288], dsym[32];
+    uint8_t lens[320];
+};
+
+__device__ __forceinline__ uint32_t entry_of(uint32_t s, bool litlen) {
+    if (litlen) {
+        if (s < 256) return s;
+        if (s == 256) return kTyEob;
+        if (s < 286) return c_lbase[s - 257] | (uint32_t)c_lext[s - 257] << 20 | kTyLen;
+        return kTyBad;
+    }
+    if (s < 30) return c_dbase[s] | (uint32_t)c_dext[s] << 20;
+    return kTyBad;
+}
+
+// Canonical code of n lengths -> root table + count[] / sym[] (for codes longer than the root), built by
+// one wavefront (ballot ranks).  Returns puff's `left`: 0 complete, > 0 incomplete, < 0 over-subscribed.
+__device__ int build(const uint8_t *lens, uint32_t n, uint32_t *tab, uint32_t root, uint16_t *count, uint16_t *sym,
+                     bool litlen, uint32_t lane) {
+    uint32_t cnt[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) cnt[l] = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const uint32_t s = b0 + lane;
+        const uint32_t l = s < n ? lens[s] : 16;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cnt[q] += (uint32_t)__popcll(__ballot(l == (uint32_t)q));
+    }
+    int left = 1;
+    bool over = false;
+    uint32_t offs[16], next[16];
+    offs[0] = 0;
+    offs[1] = 0;
+    next[0] = 0;
+    uint32_t code = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) {
+        left <<= 1;
+        left -= (int)cnt[l];
+        over |= left < 0;
+        if (l < 15) offs[l + 1] = offs[l] + cnt[l];
+        code = (code + (l == 1 ? 0 : cnt[l - 1])) << 1;
+        next[l] = code;
+    }
+    for (uint32_t i = lane; i < (1u << root); i += 64) tab[i] = 0;
+    if (lane < 16) count[lane] = (uint16_t)cnt[lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (over) return -1;
+    if (cnt[0] == n) return left;   // no codes at all
+    uint32_t run[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) run[l] = 0;
+    const uint64_t lt = (1ull << lane) - 1;
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const uint32_t s = b0 + lane;
+        const uint32_t l = s < n ? lens[s] : 0;
+        uint32_t rank = 0, off = 0, nx = 0;
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const uint64_t m = __ballot(l == (uint32_t)q);
+            if (l == (uint32_t)q) {
+                rank = run[q] + (uint32_t)__popcll(m & lt);
+                off = offs[q];
+                nx = next[q];
+            }
+            run[q] += (uint32_t)__popcll(m);
+        }
+        if (l) {
+            sym[off + rank] = (uint16_t)s;
+            if (l <= root) {
+                const uint32_t c = nx + rank;
+                const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
+                const uint32_t e = entry_of(s, litlen) | l << 16;
+                for (uint32_t k = r; k < (1u << root); k += 1u << l) tab[k] = e;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return left;
+}
+
+// A code longer than the root (or no code): the canonical bit-serial walk (puff's decode()) over the bits
+// in `bb`; returns the entry with its length set, or kTyBad.
+__device__ __noinline__ uint32_t slow_decode(uint64_t bb, const uint16_t *count, const uint16_t *sym, bool litlen) {
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len < 16; ++len) {
+        code |= (int)((bb >> (len - 1)) & 1);
+        const int c = count[len];
+        if (code - c < first) return entry_of(sym[index + (code - first)], litlen) | (uint32_t)len << 16;
+        index += c;
+        first += c;
+        first <<= 1;
+        code <<= 1;
+    }
+    return kTyBad | 1u << 16;
+}
+
+// A lane's sources, written four at a time: entries gather in registers for the aligned quad that holds
+// the next position and leave as one 16-byte store once the quad is full (a lane's first and last quads,
+// which it may share with its neighbours, go out entry by entry).
+struct SrcOut {
+    uint32_t *p;
+    uint64_t o, o0;                // next position, the lane's first
+    uint32_t b0, b1, b2, b3;
+    __device__ __forceinline__ void put(uint32_t v) {
+        const uint32_t k = (uint32_t)o & 3;
+        b0 = k == 0 ? v : b0;
+        b1 = k == 1 ? v : b1;
+        b2 = k == 2 ? v : b2;
+        b3 = k == 3 ? v : b3;
+        ++o;
+        if ((o & 3) == 0) {
+            const uint64_t q = o - 4;
+            if (q >= o0) {
+                gst<uint4>(p + q, make_uint4(b0, b1, b2, b3));
+            } else {
+                if (q + 0 >= o0) p[q + 0] = b0;
+                if (q + 1 >= o0) p[q + 1] = b1;
+                if (q + 2 >= o0) p[q + 2] = b2;
+                p[q + 3] = b3;
+            }
+        }
+    }
+    __device__ __forceinline__ void finish() {   // the partial last quad
+        const uint64_t q = o & ~3ull;
+        const uint32_t k = (uint32_t)o & 3;
+        if (k > 0 && q + 0 >= o0) p[q + 0] = b0;
+        if (k > 1 && q + 1 >= o0) p[q + 1] = b1;
+        if (k > 2 && q + 2 >= o0) p[q + 2] = b2;
+    }
+    // n positions written by someone else (a long match k_pinf_expand fills): flush, restart past them
+    __device__ __forceinline__ void skip(uint64_t n) {
+        finish();
+        o += n;
+        o0 = o;
+    }
+};
+constexpr uint32_t kLongMatch = 32;   // matches at least this long are expanded by k_pinf_expand
+
+// One lane: decode symbols from the reader's position until the first symbol boundary at or past `stop`
+// (0), the end-of-block code (1, *exit after it) or an error (2).  *bytes = output bytes of the symbols
+// decoded.  EMIT: also write each byte's source at src[o0 + ...] (and check distances against o0).
+template <bool EMIT>
+__device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t stop, uint64_t end_bits,
+                             uint64_t *exit, uint64_t *bytes, uint32_t *src, uint64_t o0, const PinfArgs *pa = nullptr) {
+    SrcOut out;
+    if (EMIT) {
+        out.p = src;
+        out.o = out.o0 = o0;
+        out.b0 = out.b1 = out.b2 = out.b3 = 0;
+    }
+    uint64_t nb = 0;
+    uint32_t r = 0;
+    for (;;) {
+        const uint64_t p = br.pos();
+        if (p > end_bits) {
+            r = 2;
+            break;
+        }
+        if (p >= stop) break;
+        br.refill(S);
+        uint32_t e = T.lit[(uint32_t)br.bb & ((1u << kRoot) - 1)];
+        if (((e >> 16) & 15) == 0) e = slow_decode(br.bb, T.lcount, T.lsym, true);
+        br.drop((e >> 16) & 15);
+        const uint32_t ty = e & (3u << 24);
+        if (ty == 0) {
+            if (EMIT) out.put(kFlag | (e & 0xff));
+            ++nb;
+            continue;
+        }
+        if (ty == kTyEob) {
+            r = br.pos() > end_bits ? 2 : 1;
+            break;
+        }
+        if (ty == kTyBad) {
+            r = 2;
+            break;
+        }
+        const uint32_t lx = (e >> 20) & 15;
+        const uint32_t len = (e & 0xffff) + ((uint32_t)br.bb & ((1u << lx) - 1));
+        br.drop(lx);
+        br.refill(S);
+        uint32_t d = T.dist[(uint32_t)br.bb & ((1u << kDRoot) - 1)];
+        if (((d >> 16) & 15) == 0) d = slow_decode(br.bb, T.dcount, T.dsym, false);
+        if ((d & (3u << 24)) == kTyBad) {
+            r = 2;
+            break;
+        }
+        br.drop((d >> 16) & 15);
+        const uint32_t dx = (d >> 20) & 15;
+        const uint32_t dist = (d & 0xffff) + ((uint32_t)br.bb & ((1u << dx) - 1));
+        br.drop(dx);
+        if (EMIT) {
+            const uint64_t q = o0 + nb;
+            if (dist > q) {   // before the start of the output (RDX_INFLATE_DISTANCE)
+                r = 2;
+                break;
+            }
+            const uint32_t base = (uint32_t)(q - dist);
+            uint32_t slot = ~0u;
+            if (len >= kLongMatch) {   // a wavefront of k_pinf_expand writes it, 64 entries per store
+                slot = atomicAdd(&pa->state->n_match, 1u);
+                if (slot < pa->mcap) pa->mlist[slot] = make_uint4((uint32_t)q, len, dist, 0);
+            }
+            if (slot < pa->mcap) {
+                out.skip(len);
+            } else if (dist >= len) {
+                for (uint32_t j = 0; j < len; ++j) out.put(base + j);
+            } else {   // overlapping: byte j repeats byte (j mod dist) of the dist bytes before the match
+                uint32_t m = 0;
+                for (uint32_t j = 0; j < len; ++j) {
+                    out.put(base + m);
+                    m = m + 1 == dist ? 0 : m + 1;
+                }
+            }
+        }
+        nb += len;
+    }
+    if (EMIT) out.finish();
+    *exit = br.pos();
+    *bytes = nb;
+    return r;
+}
+
+template <bool STORE, class SRC>
+__device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint64_t end_bits, uint64_t cb, uint32_t nl,
+                                               uint32_t nd, uint8_t *lens, uint32_t &kl, uint32_t &kd, uint32_t &used_d,
+                                               bool &eob);
+
+// Parse a block header at bit `p` (its BFINAL bit) the way oracle_inflate does; thread 0 only.  type 1:
+// fixed lengths, 2: dynamic (code lengths into T.lens).  Returns false on any error; *body = first bit of
+// the body, *nlen / *ndist the code counts.
+__device__ bool parse_header(const Stream &S, uint64_t p, uint32_t type, uint64_t end_bits, Tabs &T, uint64_t *body,
+                             uint32_t *nlen, uint32_t *ndist) {
+    uint64_t pos = p + 3;
+    if (type == 1) {
+        for (uint32_t s = 0; s < 288; ++s) T.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+        for (uint32_t s = 0; s < 30; ++s) T.lens[288 + s] = 5;
+        *nlen = 288;
+        *ndist = 30;
+        *body = pos;
+        return pos <= end_bits;
+    }
+    const uint32_t h = S.at(pos);
+    const uint32_t nl = (h & 31) + 257, nd = ((h >> 5) & 31) + 1, nc = ((h >> 10) & 15) + 4;
+    pos += 14;
+    if (nl > 286 || nd > 30) return false;
+    const uint64_t cb = ((uint64_t)S.at(pos) | (uint64_t)S.at(pos + 32) << 32) & ((1ull << (3 * nc)) - 1);
+    pos += 3 * nc;
+    uint32_t kl, kd, used_d;
+    bool eob;
+    // (the codes' completeness is judged by build(), as construct() does in the oracle)
+    if (!decode_lengths<true>(S, pos, end_bits, cb, nl, nd, T.lens, kl, kd, used_d, eob) || !eob) return false;
+    *nlen = nl;
+    *ndist = nd;
+    *body = pos;
+    return true;
+}
+
+// The finder's strict dynamic-header test at bit p (a zlib encoder's header: complete codes), in
+// registers only (one thread per bit offset; no per-lane arrays, so no scratch): the code-length code as
+// per-length counts and its symbols packed 5 bits each in (len, symbol) order; the literal / length and
+// distance code lengths are never stored, only summed into their Kraft sums as they are decoded.
+template <class SRC>
+__device__ bool dyn_candidate(const SRC &S, uint64_t p, uint64_t end_bits) {
+    const uint32_t h = S.at(p);
+    if (((h >> 1) & 3) != 2 || ((h >> 3) & 31) > 29 || ((h >> 8) & 31) > 29) return false;
+    const uint32_t nc = ((h >> 13) & 15) + 4;
+    uint64_t cb = (uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32;
+    cb &= (1ull << (3 * nc)) - 1;   // fields past HCLEN + 4 are zero lengths
+    return dyn_candidate_rest(S, p, end_bits, h, cb);
+}
+
+// The header test's Kraft sum of the code-length code (the 3-bit fields of cb): 128 = complete.
+__device__ __forceinline__ uint32_t cl_kraft(uint64_t cb) {
+    uint32_t k = 0;
+#pragma unroll
+    for (int i = 0; i < 19; ++i) {
+        const uint32_t l = (uint32_t)(cb >> (3 * i)) & 7;
+        k += l ? 128u >> l : 0u;
+    }
+    return k;
+}
+
+// The code-length code (19 lengths of 3 bits in cb, field i = symbol c_order[i]) as registers: per-length
+// counts and the symbols packed 5 bits each in (length, symbol) order; then the literal / length and
+// distance code lengths decoded with it, summed into Kraft sums as they come (STORE: also written to
+// lens[]).  The rules are oracle_inflate's: a complete code-length code, no repeat (16) first, no run past
+// HLIT + HDIST.  Returns false on the first violation or an over-subscribed literal / distance code.
+template <bool STORE, class SRC>
+__device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint64_t end_bits, uint64_t cb, uint32_t nl,
+                                               uint32_t nd, uint8_t *lens, uint32_t &kl, uint32_t &kd, uint32_t &used_d,
+                                               bool &eob) {
+    uint32_t cnt[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) cnt[l] = 0;
+#pragma unroll
+    for (int i = 0; i < 19; ++i) {
+        const uint32_t l = (uint32_t)(cb >> (3 * i)) & 7;
+#pragma unroll
+        for (int q = 1; q < 8; ++q) cnt[q] += l == (uint32_t)q ? 1u : 0u;
+    }
+    int left = 1;
+#pragma unroll
+    for (int l = 1; l < 8; ++l) left = (left << 1) - (int)cnt[l];
+    if (left != 0) return false;   // over-subscribed or incomplete (construct() != 0)
+    constexpr int kInv[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+    uint64_t pk0 = 0, pk1 = 0;
+    uint32_t k = 0;
+#pragma unroll
+    for (int l = 1; l < 8; ++l) {
+#pragma unroll
+        for (int sy = 0; sy < 19; ++sy) {
+            const bool hit = ((uint32_t)(cb >> (3 * kInv[sy])) & 7) == (uint32_t)l;
+            const uint64_t v = hit ? (uint64_t)sy : 0;
+            pk0 |= k < 12 ? v << (5 * k) : 0;
+            pk1 |= k >= 12 ? v << (5 * (k - 12)) : 0;
+            k += hit ? 1 : 0;
+        }
+    }
+    const uint32_t total = nl + nd;
+    uint32_t idx = 0, prev = 0;
+    kl = kd = used_d = 0;
+    eob = false;
+    while (idx < total) {
+        if (pos > end_bits) return false;
+        const uint32_t w = S.at(pos);
+        // canonical walk over lengths 1..7 (predicated; a complete code always decodes)
+        int code = 0, first = 0, index = 0, si = -1, len = 0;
+#pragma unroll
+        for (int l = 1; l < 8; ++l) {
+            code |= (int)((w >> (l - 1)) & 1);
+            const int c = (int)cnt[l];
+            if (si < 0 && code - c < first) {
+                si = index + (code - first);
+                len = l;
+            }
+            index += c;
+            first = (first + c) << 1;
+            code <<= 1;
+        }
+        if (si < 0) return false;
+        const uint32_t sym = (uint32_t)((si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31);
+        pos += len;
+        const uint32_t x = w >> len;
+        uint32_t rep = 1, val = sym;
+        if (sym == 16) {
+            if (idx == 0) return false;
+            val = prev;
+            rep = 3 + (x & 3);
+            pos += 2;
+        } else if (sym == 17) {
+            val = 0;
+            rep = 3 + (x & 7);
+            pos += 3;
+        } else if (sym == 18) {
+            val = 0;
+            rep = 11 + (x & 127);
+            pos += 7;
+        }
+        if (idx + rep > total) return false;
+        if (STORE)
+            for (uint32_t r = 0; r < rep; ++r) lens[idx + r] = (uint8_t)val;
+        const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
+        if (idx <= 256 && 256 < idx + nlit) eob = val != 0;
+        if (val) {
+            kl += nlit << (15 - val);
+            kd += ndst << (15 - val);
+            used_d += ndst;
+            if (kl > (1u << 15) || kd > (1u << 15)) return false;
+        }
+        prev = val;
+        idx += rep;
+    }
+    return pos <= end_bits;
+}
+
+template <class SRC>
+__device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb) {
+    const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
+    uint64_t pos = p + 17 + 3 * nc;
+    uint32_t kl, kd, used_d;
+    bool eob;
+    if (!decode_lengths<false>(S, pos, end_bits, cb, nl, nd, nullptr, kl, kd, used_d, eob)) return false;
+    return eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
+}
+
+// ---- 1. candidates ------------------------------------------------------------------------------------
+// A workgroup tests the bit offsets of kFindBytes bytes (4 per thread) and each of those bytes as the LEN of
+// a stored block.  The bytes and the longest header behind them (<= 4500 bits) are staged in LDS first and
+// read from there only (a surviving offset decodes its header symbol by symbol: each dependent read from L2
+// would cost the wave a round trip).  The 32 offsets of a thread are first screened without branches
+// (BTYPE, HLIT, HDIST, the code-length code's Kraft sum); only the rare survivors decode their headers.
+constexpr uint32_t kFindBytes = 1024, kFindLook = 640;
+constexpr uint32_t kFindWin = (kFindBytes + kFindLook) / 4 + 4;
+
+struct WinStream {   // bit reads from the staged window only (positions inside it by construction)
+    const uint32_t *lds;
+    uint64_t l0;
+    __device__ __forceinline__ uint32_t at(uint64_t p) const {
+        const uint32_t i = min((uint32_t)((p >> 5) - l0), kFindWin - 2);
+        const uint64_t v = (uint64_t)lds[i] | (uint64_t)lds[i + 1] << 32;
+        return (uint32_t)(v >> (p & 31));
+    }
+};
+
+__global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
+    __shared__ uint32_t win[kFindWin];
+    const Stream G = make_stream(a);
+    const uint64_t q0 = a.first_byte + (uint64_t)blockIdx.x * kFindBytes;
+    const uint64_t l0 = q0 >= 4 ? (q0 >> 2) - 1 : 0;
+    for (uint32_t k = threadIdx.x; k < kFindWin; k += 256) win[k] = G.ldg(l0 + k);
+    __syncthreads();
+    WinStream S;
+    S.lds = win;
+    S.l0 = l0;
+    PinfState *st = a.state;
+    auto push = [&](uint64_t key) {
+        const uint32_t i = atomicAdd(&st->n_cand, 1u);
+        if (i < kPinfMaxCand) a.cand[i] = key;
+        else atomicOr(&st->overflow, 1u);
+    };
+    // this thread's 4 bytes: q0 + 4t .. q0 + 4t + 3 (consecutive: their bits come from one 64-bit window)
+    const uint64_t qt = q0 + 4 * threadIdx.x;
+    // BTYPE = 2 and HLIT, HDIST <= 29 for all 32 offsets from one 64-bit window (no branches)
+    const uint64_t w64 = (uint64_t)S.at(8 * qt) | (uint64_t)S.at(8 * qt + 32) << 32;
+    uint32_t cheap = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 32; ++b) {
+        const uint32_t h = (uint32_t)(w64 >> b);
+        const bool pass = ((h >> 1) & 3) == 2 && ((h >> 3) & 31) <= 29 && ((h >> 8) & 31) <= 29 && qt + b / 8 < a.end_byte;
+        cheap |= pass ? 1u << b : 0u;
+    }
+    // then the code-length code's Kraft sum (about a fifth of the offsets get here)
+    uint32_t mask = 0;
+    while (cheap) {
+        const uint32_t b = __builtin_ctz(cheap);
+        cheap &= cheap - 1;
+        const uint64_t p = 8 * qt + b;
+        const uint32_t h = (uint32_t)(w64 >> b);
+        const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
+                            ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
+        mask |= cl_kraft(cb) == 128 ? 1u << b : 0u;
+    }
+    while (mask) {
+        const uint32_t b = __builtin_ctz(mask);
+        mask &= mask - 1;
+        const uint64_t p = 8 * qt + b;
+        const uint32_t h = S.at(p);
+        const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
+                            ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
+        if (dyn_candidate_rest(S, p, a.end_bits, h, cb)) push(p << 2 | 2);
+    }
+    // stored: LEN, NLEN at q, q+2; the two bits before q are zero (padding or BTYPE 00); the data fits
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t q = qt + k;
+        if (q >= a.first_byte + 1 && q + 4 <= a.end_byte) {
+            const uint32_t v = S.at(8 * q - 8);   // byte q-1, LEN, NLEN (low 8 bits first)
+            const uint32_t len = (v >> 8) & 0xffff;
+            const uint32_t nlen = S.at(8 * q + 16) & 0xffff;
+            if (len == (~nlen & 0xffff) && ((v >> 6) & 3) == 0 && q + 4 + len <= a.end_byte) push((8 * q) << 2 | 0);
+        }
+    }
+}
+
+// Smallest candidate position strictly after `after` (the end bound of a block's body), or end_bits.
+__device__ uint64_t next_cand(const PinfArgs &a, uint32_t n, uint64_t after, uint64_t *red) {
+    uint64_t best = ~0ull;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t b = a.cand[i] >> 2;
+        if (b > after && b < best) best = b;
+    }
+    // block-wide min
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((long long)best, m, 64);
+        best = o < best ? o : best;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = best;
+    __syncthreads();
+    best = red[0];
+    for (uint32_t k = 1; k < blockDim.x / 64; ++k) best = red[k] < best ? red[k] : best;
+    __syncthreads();
+    return best == ~0ull ? a.end_bits : best;
+}
+
+// RDX_PINF_PROF: per workgroup 8 words — [0] start, [1] tables built, [2] first decode pass, [3] lanes
+// agree, [4] end (wall clock), [5] resync rounds, [6] sequential walks, [7] body extensions
+#define PINF_STAMP(slot, v)                                                                     \
+    do {                                                                                        \
+        if (prof && threadIdx.x == 0) prof[slot] = (v);                                         \
+    } while (0)
+
+// ---- 2. one candidate block per workgroup -------------------------------------------------------------
+__device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
+    uint64_t *const prof = a.prof && blockIdx.x < count ? a.prof + 8ull * (first + blockIdx.x) : nullptr;
+    uint64_t rounds = 0, walks = 0, exts = 0;
+    __shared__ Tabs T;
+    __shared__ uint64_t s_st[kLanes], s_x[kLanes], s_red[kLanes / 64];
+    static_assert(kLanes % 64 == 0 && kLanes <= 1024, "lanes per block");
+    __shared__ uint32_t s_nb[kLanes];
+    __shared__ uint8_t s_ed[kLanes];
+    __shared__ uint64_t s_body;
+    __shared__ uint32_t s_ok, s_nlen, s_ndist, s_first;
+    __shared__ uint32_t win[kWinDwords];
+    const uint32_t n = min(a.state->n_cand, kPinfMaxCand);
+    const uint32_t ci = first + blockIdx.x;
+    if (blockIdx.x >= count || ci >= n) return;
+    Stream S = make_stream(a);
+    const uint32_t t = threadIdx.x;
+    const uint64_t key = a.cand[ci];
+    const uint64_t bit = key >> 2;
+    const uint32_t type = (uint32_t)(key & 3);
+    PinfBlk &B = a.blk[ci];
+    if (type == 0) {   // stored: LEN / NLEN at the byte `bit / 8`
+        if (t == 0) {
+            const uint64_t q = bit / 8;
+            const uint32_t len = S.byte(q) | S.byte(q + 1) << 8, nlen = S.byte(q + 2) | S.byte(q + 3) << 8;
+            const bool ok = len == (~nlen & 0xffff) && q + 4 + len <= a.end_byte;
+            B.end = 8 * (q + 4 + len);
+            B.bytes = len;
+            B.body = 8 * (q + 4);
+            B.nlanes = 0;
+            B.status = ok ? 0 : 1;
+        }
+        return;
+    }
+    // the header and (where it fits) the body from LDS: the window starts at the header's dword
+    S.stage(win, kWinDwords, bit >> 5, a.nw);
+    if (t == 0) {
+        uint64_t body = 0;
+        uint32_t nl = 0, nd = 0;
+        s_ok = parse_header(S, bit, type, a.end_bits, T, &body, &nl, &nd) ? 1 : 0;
+        s_body = body;
+        s_nlen = nl;
+        s_ndist = nd;
+    }
+    __syncthreads();
+    if (t < 64 && s_ok) {
+        const uint32_t nl = s_nlen, nd = s_ndist;
+        int r = build(T.lens, nl, T.lit, kRoot, T.lcount, T.lsym, true, t);
+        bool ok = !(r < 0 || (r > 0 && nl != (uint32_t)T.lcount[0] + T.lcount[1]));
+        r = build(T.lens + nl, nd, T.dist, kDRoot, T.dcount, T.dsym, false, t);
+        ok = ok && !(r < 0 || (r > 0 && nd != (uint32_t)T.dcount[0] + T.dcount[1]));
+        if (t == 0) s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_ok) {
+        if (t == 0) B.status = 1;
+        return;
+    }
+    PINF_STAMP(1, wall_clock64());
+    // keep the code lengths: k_pinf_emit rebuilds the tables from them
+    for (uint32_t i = t; i < 320; i += kLanes) a.lens[(uint64_t)ci * 320 + i] = T.lens[i];
+    const uint64_t body = s_body;
+    uint64_t E = next_cand(a, n, bit, s_red);
+    for (uint32_t ext = 0; ext < 8; ++ext) {
+        if (E <= body) E = body + 1;
+        const uint64_t span = E - body;
+        if (span > kMaxSpan) break;
+        const uint32_t L = (uint32_t)max<uint64_t>(1, min<uint64_t>(kLanes, span / kMinLaneBits));
+        auto lo = [&](uint32_t k) -> uint64_t { return k >= L ? E : body + span * k / L; };
+        auto run = [&](uint32_t k, uint64_t from) {
+            Bits br;
+            br.seek(S, from);
+            uint64_t x, nb;
+            const uint32_t r = run_lane<false>(T, S, br, lo(k + 1), a.end_bits, &x, &nb, nullptr, 0);
+            s_st[k] = from;
+            s_x[k] = x;
+            s_nb[k] = (uint32_t)nb;
+            s_ed[k] = (uint8_t)r;
+        };
+        if (t < L) run(t, lo(t));
+        __syncthreads();
+        PINF_STAMP(2, wall_clock64());
+        for (;;) {
+            // resync rounds: lane k re-decodes from lane k-1's exit when its start differs
+            bool done = false;
+            for (uint32_t round = 0; round < kRounds; ++round) {
+                uint64_t px = 0;
+                bool redo = false;
+                if (t >= 1 && t < L) {
+                    px = s_x[t - 1];
+                    redo = s_ed[t - 1] == 0 && s_st[t] != px;
+                }
+                __syncthreads();
+                if (redo) run(t, px);
+                ++rounds;
+                if (!__syncthreads_or(redo)) {
+                    done = true;
+                    break;
+                }
+            }
+            if (done) break;
+            // the data keeps the parses apart: the first mismatched lane walks on sequentially
+            ++walks;
+            if (t == 0) {
+                uint32_t m = 1;
+                while (m < L && (s_ed[m - 1] != 0 || s_st[m] == s_x[m - 1])) ++m;
+                for (uint32_t j = m; j < L; ++j) {
+                    if (j > m && (s_ed[j - 1] != 0 || s_st[j] == s_x[j - 1])) break;
+                    run(j, s_x[j - 1]);
+                }
+            }
+            __syncthreads();
+        }
+        // the first lane that ended (end of block or error) closes the block
+        if (t == 0) {
+            uint32_t j = 0;
+            while (j < L && s_ed[j] == 0) ++j;
+            s_first = j;
+        }
+        __syncthreads();
+        const uint32_t j = s_first;
+        PINF_STAMP(3, wall_clock64());
+        if (j == L) {   // no end of block before E: extend the body to the next candidate
+            if (E >= a.end_bits) break;
+            E = next_cand(a, n, E, s_red);
+            ++exts;
+            continue;
+        }
+        PINF_STAMP(5, rounds);
+        PINF_STAMP(6, walks);
+        PINF_STAMP(7, exts);
+        if (t == 0) {
+            uint64_t bytes = 0;
+            for (uint32_t k = 0; k <= j; ++k) bytes += s_nb[k];
+            B.end = s_x[j];
+            B.bytes = bytes;
+            B.body = body;
+            B.nlanes = j + 1;
+            B.nlen = s_nlen;
+            B.ndist = s_ndist;
+            B.status = s_ed[j] == 1 ? 0 : 1;
+        }
+        if (t <= j) {
+            a.lst[(uint64_t)ci * kLanes + t] = s_st[t];
+            a.lnb[(uint64_t)ci * kLanes + t] = s_nb[t];
+        }
+        return;
+    }
+    if (t == 0) B.status = 1;   // no end of block within kMaxSpan / the stream
+}
+
+// RDX_PINF_PROF: every workgroup's start / end (wall clock) in a.prof, for tools/probe_pinflate.py
+__global__ __launch_bounds__(kLanes) void k_pinf_block(PinfArgs a, uint32_t first, uint32_t count) {
+    const uint64_t t0 = a.prof ? wall_clock64() : 0;
+    block_body(a, first, count);
+    if (a.prof) {
+        __syncthreads();
+        if (threadIdx.x == 0 && blockIdx.x < count) {
+            a.prof[8 * (first + blockIdx.x)] = t0;
+            a.prof[8 * (first + blockIdx.x) + 4] = wall_clock64();
+        }
+    }
+}
+
+// ---- 3. the chain ---------------------------------------------------------------------------------------
+constexpr uint32_t kChainThreads = 1024;
+
+__global__ __launch_bounds__(kChainThreads) void k_pinf_chain(PinfArgs a) {
+    __shared__ uint64_t sk[kPinfMaxCand];      // (key << 12 | index), sorted
+    __shared__ int32_t succ[kPinfMaxCand];     // sorted index of the next block, or < 0
+    __shared__ uint16_t order[kPinfMaxCand];   // the chain: sorted indices in stream order
+    __shared__ uint8_t fin[kPinfMaxCand];      // BFINAL of that next block
+    __shared__ uint64_t s_scan[kChainThreads / 64];
+    __shared__ int32_t s_head;
+    __shared__ uint32_t s_headfin, s_nc, s_status;
+    __shared__ uint64_t s_p0, s_miss;
+    __shared__ uint32_t s_hok;
+    PinfState *st = a.state;
+    const uint32_t t = threadIdx.x;
+    const Stream S = make_stream(a);
+    if (st->overflow) {
+        if (t == 0) st->status = kPinfFallback;
+        return;
+    }
+    const uint32_t n = min(st->n_cand, kPinfMaxCand);
+    for (uint32_t i = t; i < kPinfMaxCand; i += kChainThreads) sk[i] = i < n ? (a.cand[i] << 12 | i) : ~0ull;
+    // the stream header (thread 0): zlib RFC 1950 / gzip RFC 1952, as oracle_inflate unzlib / gunzip
+    if (t == 0) {
+        uint64_t q = a.first_byte;
+        bool ok = true;
+        if (a.format == RDX_COMPRESSION_ZLIB) {
+            ok = a.end_byte >= q + 2;
+            const uint32_t cmf = S.byte(q), flg = S.byte(q + 1);
+            ok = ok && (cmf & 15) == 8 && (cmf >> 4) <= 7 && (cmf * 256 + flg) % 31 == 0 && !(flg & 0x20);
+            q += 2;
+        } else {
+            ok = a.end_byte >= q + 10 && S.byte(q) == 0x1f && S.byte(q + 1) == 0x8b && S.byte(q + 2) == 8;
+            const uint32_t flg = S.byte(q + 3);
+            q += 10;
+            if (ok && (flg & 4)) {
+                const uint32_t xlen = S.byte(q) | S.byte(q + 1) << 8;
+                q += 2 + xlen;
+            }
+            if (ok && (flg & 8)) {
+                while (q < a.end_byte && S.byte(q) != 0) ++q;
+                ++q;
+            }
+            if (ok && (flg & 16)) {
+                while (q < a.end_byte && S.byte(q) != 0) ++q;
+                ++q;
+            }
+            if (ok && (flg & 2)) q += 2;
+            ok = ok && q < a.end_byte;
+        }
+        s_hok = ok ? 1 : 0;
+        s_p0 = 8 * q;
+    }
+    __syncthreads();
+    // bitonic sort of the candidate keys (only as many as there are, rounded up to a power of two)
+    uint32_t m = 2;
+    while (m < n) m <<= 1;
+    for (uint32_t k = 2; k <= m; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < m; i += kChainThreads) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = sk[i], y = sk[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        sk[i] = y;
+                        sk[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // successor of a block ending at e: the candidate the header at e names (-1: none, a miss; -3: the
+    // stream ends or BTYPE 3)
+    auto find = [&](uint64_t e, uint8_t *f) -> int32_t {
+        if (e + 3 > a.end_bits) return -3;
+        const uint32_t h = S.at(e) & 7;
+        *f = (uint8_t)(h & 1);
+        const uint32_t ty = (h >> 1) & 3;
+        if (ty == 3) return -3;
+        uint64_t k = ty == 0 ? (8 * ((e + 3 + 7) / 8)) << 2 | 0 : e << 2 | ty;
+        uint32_t lo = 0, hi = n;   // first sorted key >= k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if ((sk[mid] >> 12) < k) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < n && (sk[lo] >> 12) == k) return (int32_t)lo;
+        return -1;
+    };
+    for (uint32_t i = t; i < n; i += kChainThreads) {
+        const uint32_t c = (uint32_t)(sk[i] & 4095);
+        const PinfBlk &B = a.blk[c];
+        uint8_t f = 0;
+        succ[i] = B.status ? -2 : find(B.end, &f);
+        fin[i] = f;
+    }
+    if (t == 0) {
+        uint8_t f = 0;
+        s_head = s_hok ? find(s_p0, &f) : -3;
+        s_headfin = f;
+    }
+    __syncthreads();
+    // the walk (thread 0, LDS only): sorted indices in stream order up to the BFINAL block
+    if (t == 0) {
+        int32_t cur = s_head;
+        uint32_t f = s_headfin, nc = 0, status = kPinfFallback;
+        int32_t last = -1;
+        for (;;) {
+            if (cur == -1) {   // a block start that is no candidate: the host decodes it and chains again
+                status = kPinfMiss;
+                break;
+            }
+            if (cur < 0 || nc >= kPinfMaxCand) break;   // an error: the sequential decoder reports it
+            order[nc++] = (uint16_t)cur;
+            if (f) {
+                status = kPinfOk;
+                break;
+            }
+            f = fin[cur];
+            last = cur;
+            cur = succ[cur];
+        }
+        // the position where the walk stopped: a miss's block start
+        s_miss = status == kPinfMiss ? (last < 0 ? s_p0 : a.blk[sk[last] & 4095].end) : 0;
+        s_nc = nc;
+        s_status = status;
+    }
+    __syncthreads();
+    const uint32_t nc = s_nc;
+    // output offsets: an exclusive scan of the chain blocks' bytes, 4 per thread
+    uint64_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t k = 4 * t + q;
+        v[q] = k < nc ? a.blk[sk[order[k]] & 4095].bytes : 0;
+        sum += v[q];
+    }
+    uint64_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_up((long long)incl, d, 64);
+        if ((t & 63) >= (uint32_t)d) incl += o;
+    }
+    if ((t & 63) == 63) s_scan[t / 64] = incl;
+    __syncthreads();
+    uint64_t base = 0;
+    for (uint32_t w = 0; w < t / 64; ++w) base += s_scan[w];
+    uint64_t run = base + incl - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t k = 4 * t + q;
+        if (k < nc) {
+            a.chain[k] = (uint32_t)(sk[order[k]] & 4095);
+            a.coff[k] = run;
+        }
+        run += v[q];
+    }
+    if (t == kChainThreads - 1) {
+        const uint64_t total = run;   // the last thread's running sum: every chain block's bytes
+        uint32_t status = s_status;
+        if (status == kPinfOk) {   // BFINAL: the trailer follows at the next byte boundary
+            const uint64_t e = a.blk[sk[order[nc - 1]] & 4095].end;
+            const uint64_t tb = (e + 7) / 8;
+            const uint64_t need = a.format == RDX_COMPRESSION_ZLIB ? 4 : 8;
+            if (tb + need > a.end_byte || total >= (1ull << 31)) status = kPinfFallback;
+            st->trailer_byte = tb;
+        }
+        if (status == kPinfMiss) {
+            const uint64_t e = s_miss;
+            st->miss_bit = e;
+            st->miss_type = (S.at(e) >> 1) & 3;
+        }
+        st->n_chain = nc;
+        st->total = total;
+        st->status = status;
+    }
+}
+
+// ---- 4. sources of every output byte ----------------------------------------------------------------------
+__device__ void emit_body(const PinfArgs &a) {
+    __shared__ Tabs T;
+    __shared__ uint64_t s_off[kLanes];
+    __shared__ uint32_t win[kWinDwords];
+    const uint32_t t = threadIdx.x;
+    const uint32_t c = a.chain[blockIdx.x];
+    const uint64_t o = a.coff[blockIdx.x];
+    const PinfBlk B = a.blk[c];
+    Stream S = make_stream(a);
+    uint32_t *src = a.src;
+    const uint32_t type = (uint32_t)(a.cand[c] & 3);
+    if (type == 0) {   // stored: four bytes per thread and step, 16-byte stores where the quad is aligned
+        const uint64_t q0 = B.body / 8;
+        for (uint64_t j = 4 * (uint64_t)t; j < B.bytes; j += 4 * kLanes) {
+            const uint32_t w = S.at(8 * (q0 + j));
+            const uint64_t d = o + j;
+            const uint32_t k = (uint32_t)min<uint64_t>(4, B.bytes - j);
+            if (k == 4 && (d & 3) == 0) {
+                gst<uint4>(src + d, make_uint4(kFlag | (w & 0xff), kFlag | ((w >> 8) & 0xff), kFlag | ((w >> 16) & 0xff),
+                                               kFlag | (w >> 24)));
+            } else {
+                for (uint32_t i = 0; i < k; ++i) src[d + i] = kFlag | ((w >> (8 * i)) & 0xff);
+            }
+        }
+        return;
+    }
+    const uint32_t L = B.nlanes;
+    const uint64_t l0 = a.lst[(uint64_t)c * kLanes];
+    S.stage(win, kWinDwords, l0 >> 5, (B.end >> 5) + 2);
+    for (uint32_t i = t; i < 320; i += kLanes) T.lens[i] = a.lens[(uint64_t)c * 320 + i];
+    __syncthreads();
+    if (t < 64) {
+        build(T.lens, B.nlen, T.lit, kRoot, T.lcount, T.lsym, true, t);
+        build(T.lens + B.nlen, B.ndist, T.dist, kDRoot, T.dcount, T.dsym, false, t);
+    }
+    uint64_t *const prof = a.prof ? a.prof + 8ull * (kPinfMaxCand + blockIdx.x) : nullptr;
+    const uint32_t nb = t < L ? a.lnb[(uint64_t)c * kLanes + t] : 0;
+    // exclusive prefix of the lanes' bytes
+    s_off[t] = nb;
+    __syncthreads();
+    for (uint32_t d = 1; d < kLanes; d <<= 1) {
+        const uint64_t v = t >= d ? s_off[t - d] : 0;
+        __syncthreads();
+        s_off[t] += v;
+        __syncthreads();
+    }
+    PINF_STAMP(1, wall_clock64());
+    if (t >= L) return;
+    const uint64_t my = o + s_off[t] - nb;
+    Bits br;
+    br.seek(S, a.lst[(uint64_t)c * kLanes + t]);
+    const uint64_t stop = t + 1 < L ? a.lst[(uint64_t)c * kLanes + t + 1] : ~0ull;
+    uint64_t x, got;
+    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a);
+    const uint32_t want = t + 1 < L ? 0u : 1u;
+    if (r != want || got != nb) atomicOr(&a.state->emit_err, 1u);
+}
+
+__global__ __launch_bounds__(kLanes) void k_pinf_emit(PinfArgs a) {
+    const uint64_t t0 = a.prof ? wall_clock64() : 0;
+    emit_body(a);
+    if (a.prof) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            a.prof[8 * (kPinfMaxCand + blockIdx.x)] = t0;
+            a.prof[8 * (kPinfMaxCand + blockIdx.x) + 4] = wall_clock64();
+        }
+    }
+}
+
+// ---- 4b. long matches: one wavefront per match record ------------------------------------------------
+__global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
+    const uint32_t n = min(a.state->n_match, a.mcap);
+    const uint32_t r = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x & 63;
+    if (r >= n) return;
+    const uint4 m = a.mlist[r];
+    const uint32_t o = m.x, len = m.y, dist = m.z;
+    uint32_t *src = a.src;
+    if (dist >= len) {
+        for (uint32_t j = lane; j < len; j += 64) src[o + j] = o + j - dist;
+    } else {   // overlapping: (j mod dist) into the dist bytes before the match (a float quotient, corrected)
+        const float rd = __builtin_amdgcn_rcpf((float)dist);
+        for (uint32_t j = lane; j < len; j += 64) {
+            const uint32_t q = (uint32_t)((float)j * rd);
+            int32_t rem = (int32_t)(j - q * dist);
+            rem = rem < 0 ? rem + (int32_t)dist : (rem >= (int32_t)dist ? rem - (int32_t)dist : rem);
+            src[o + j] = o - dist + (uint32_t)rem;
+        }
+    }
+}
+
+// ---- 5. pointer jumping ----------------------------------------------------------------------------------
+// One byte per thread; each launch chases up to 8 links per byte and stores where it got to (every link
+// leads to a byte with the same final value, so racing with other threads' stores is harmless).
+__global__ __launch_bounds__(256) void k_pinf_resolve(PinfArgs a, uint32_t round) {
+    PinfState *st = a.state;
+    if (round > 0 && st->unresolved[round - 1] == 0) return;
+    uint32_t *src = a.src;
+    const uint64_t N = st->total;
+    // workgroups are dealt to the 8 XCDs round-robin; give each XCD one contiguous eighth of the bytes, so
+    // the links it chases (<= 32 KiB back) stay in its own L2
+    const uint32_t per = (gridDim.x + 7) / 8;
+    const uint32_t tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    const uint64_t o = (uint64_t)tile * 256 + threadIdx.x;
+    bool any = false;
+    if (o < N) {
+        uint32_t v = src[o];
+        if (!(v & kFlag)) {
+            for (uint32_t h = 0; h < 8 && !(v & kFlag); ++h) v = src[v];
+            src[o] = v;
+            any = !(v & kFlag);
+        }
+    }
+    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(&st->unresolved[round], 1u);
+}
+
+// ---- 6. bytes + checksums -----------------------------------------------------------------------------------
+constexpr uint32_t kAdler = 65521;
+
+__device__ uint32_t multmodp(uint32_t a, uint32_t b) {   // a(x) b(x) mod P (reflected), as zlib
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = b & 1 ? (b >> 1) ^ 0xedb88320u : b >> 1;
+    }
+    return p;
+}
+// x^(8n) mod P
+__device__ uint32_t x8n(uint64_t n) {
+    uint32_t p = 1u << 31, x = 1u << 30;   // x^0, x^1
+    // x^(2^k) for k = 0, 1, 2 (x^8 = x^(2^3)) first
+    for (int k = 0; k < 3; ++k) x = multmodp(x, x);
+    while (n) {
+        if (n & 1) p = multmodp(x, p);
+        n >>= 1;
+        if (n) x = multmodp(x, x);
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_pinf_finish(PinfArgs a) {
+    __shared__ uint32_t crc_tab[256];
+    __shared__ uint64_t r1[4], r2[4];
+    __shared__ uint32_t rc[4];
+    PinfState *st = a.state;
+    const uint32_t t = threadIdx.x;
+    const uint64_t N = st->total;
+    const bool gz = a.format == RDX_COMPRESSION_GZIP;
+    if (gz) {
+        uint32_t c = t;
+        for (int k = 0; k < 8; ++k) c = c & 1 ? (c >> 1) ^ 0xedb88320u : c >> 1;
+        crc_tab[t] = c;
+    }
+    __syncthreads();
+    // segment of this workgroup, slice of this thread (multiples of 4 bytes)
+    const uint64_t seg = ((N + gridDim.x - 1) / gridDim.x + 1023) / 1024 * 1024;
+    const uint64_t s0 = (uint64_t)blockIdx.x * seg;
+    const uint64_t sl = seg / 256;
+    const uint64_t b0 = min(N, s0 + t * sl), b1 = min(N, s0 + (t + 1) * sl);
+    uint64_t sa = 0, sw = 0;
+    uint32_t c = 0xffffffffu;
+    bool bad = false;
+    for (uint64_t o = b0; o < b1; o += 4) {
+        uint32_t word = 0;
+        const uint32_t k = (uint32_t)min<uint64_t>(4, b1 - o);
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t v = a.src[o + i];
+            bad |= !(v & kFlag);
+            const uint32_t by = v & 0xff;
+            word |= by << (8 * i);
+            if (gz) c = crc_tab[(c ^ by) & 0xff] ^ (c >> 8);
+            sa += by;
+            sw += (b1 - (o + i)) * by;   // weight: bytes of the slice from this one to its end
+        }
+        if (k == 4) gst<uint32_t>(a.out + o, word);   // out is 16-byte aligned, o a multiple of 4
+        else for (uint32_t i = 0; i < k; ++i) a.out[o + i] = (uint8_t)(word >> (8 * i));
+    }
+    if (__ballot(bad) && (t & 63) == 0) atomicOr(&st->emit_err, 2u);
+    // fold to the whole stream: Adler s2 gains (bytes after the slice) x s1; CRC shifts by those bytes
+    const uint64_t after = N - b1;
+    uint64_t p1 = sa % kAdler, p2 = (sw % kAdler + (after % kAdler) * p1) % kAdler;
+    uint32_t pc = 0;
+    if (gz) pc = b1 > b0 ? multmodp(x8n(after), c ^ 0xffffffffu) : 0u;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        p1 += (uint64_t)__shfl_xor((long long)p1, m, 64);
+        p2 += (uint64_t)__shfl_xor((long long)p2, m, 64);
+        pc ^= (uint32_t)__shfl_xor((int)pc, m, 64);
+    }
+    if ((t & 63) == 0) {
+        r1[t / 64] = p1 % kAdler;
+        r2[t / 64] = p2 % kAdler;
+        rc[t / 64] = pc;
+    }
+    __syncthreads();
+    if (t == 0) {
+        const uint64_t q1 = (r1[0] + r1[1] + r1[2] + r1[3]) % kAdler, q2 = (r2[0] + r2[1] + r2[2] + r2[3]) % kAdler;
+        a.partial[3 * blockIdx.x + 0] = q1;
+        a.partial[3 * blockIdx.x + 1] = q2;
+        a.partial[3 * blockIdx.x + 2] = rc[0] ^ rc[1] ^ rc[2] ^ rc[3];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_pinf_check(PinfArgs a, uint32_t parts) {
+    PinfState *st = a.state;
+    const uint32_t t = threadIdx.x;
+    const Stream S = make_stream(a);
+    uint64_t s1 = 0, s2 = 0;
+    uint32_t c = 0;
+    for (uint32_t i = t; i < parts; i += 64) {
+        s1 += a.partial[3 * i];
+        s2 += a.partial[3 * i + 1];
+        c ^= (uint32_t)a.partial[3 * i + 2];
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        s1 += (uint64_t)__shfl_xor((long long)s1, m, 64);
+        s2 += (uint64_t)__shfl_xor((long long)s2, m, 64);
+        c ^= (uint32_t)__shfl_xor((int)c, m, 64);
+    }
+    if (t) return;
+    const uint64_t N = st->total, tb = st->trailer_byte;
+    bool ok = st->emit_err == 0;
+    for (uint32_t r = 0; r < kPinfMaxRounds; ++r) ok = ok && (r + 1 < kPinfMaxRounds || st->unresolved[r] == 0);
+    if (a.format == RDX_COMPRESSION_ZLIB) {
+        // Adler-32: s1 starts at 1, so s2 gains N more
+        const uint32_t A1 = (uint32_t)((1 + s1) % kAdler), A2 = (uint32_t)((s2 + N) % kAdler);
+        const uint32_t want = S.byte(tb) << 24 | S.byte(tb + 1) << 16 | S.byte(tb + 2) << 8 | S.byte(tb + 3);
+        ok = ok && want == (A2 << 16 | A1);
+    } else {
+        const uint32_t crc = c;   // XOR of the slices' CRC-32s, each shifted past the bytes after it
+        const uint32_t want = S.byte(tb) | S.byte(tb + 1) << 8 | S.byte(tb + 2) << 16 | S.byte(tb + 3) << 24;
+        const uint32_t isz = S.byte(tb + 4) | S.byte(tb + 5) << 8 | S.byte(tb + 6) << 16 | S.byte(tb + 7) << 24;
+        ok = ok && want == crc && isz == (uint32_t)N;
+    }
+    st->final_ok = ok ? 1 : 0;
+}
+
+}  // namespace
+
+hipError_t launch_pinf_find(const PinfArgs &a, hipStream_t s) {
+    const uint64_t n = a.end_byte - a.first_byte;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pinf_find, dim3((uint32_t)((n + kFindBytes - 1) / kFindBytes)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_pinf_block(const PinfArgs &a, uint32_t first, uint32_t count, hipStream_t s) {
+    hipLaunchKernelGGL(k_pinf_block, dim3(count), dim3(kLanes), 0, s, a, first, count);
+    return hipGetLastError();
+}
+hipError_t launch_pinf_chain(const PinfArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_pinf_chain, dim3(1), dim3(kChainThreads), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total, int cus, hipStream_t s) {
+    if (n_chain) hipLaunchKernelGGL(k_pinf_emit, dim3(n_chain), dim3(kLanes), 0, s, a);
+    if (a.mcap) hipLaunchKernelGGL(k_pinf_expand, dim3((a.mcap + 3) / 4), dim3(256), 0, s, a);
+    const uint32_t g = (uint32_t)((std::max<uint64_t>(1, (total + 255) / 256) + 7) / 8 * 8);
+    for (uint32_t r = 0; r < kPinfMaxRounds; ++r) hipLaunchKernelGGL(k_pinf_resolve, dim3(g), dim3(256), 0, s, a, r);
+    const uint32_t parts = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kPinfMaxParts, (total + 4095) / 4096));
+    hipLaunchKernelGGL(k_pinf_finish, dim3(parts), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pinf_check, dim3(1), dim3(64), 0, s, a, parts);
+    return hipGetLastError();
+}
+
+}  // namespace rdx

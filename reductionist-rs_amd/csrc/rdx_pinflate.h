@@ -1,0 +1,68 @@
+// Launch descriptor of the single-stream parallel inflate (k_pinflate.hip), shared by host and device.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rdx {
+
+constexpr uint32_t kPinfMaxCand = 4096;   // block-start candidates per stream (more: the stream falls back)
+#ifndef RDX_PINF_LANES
+#define RDX_PINF_LANES 256
+#endif
+constexpr uint32_t kPinfLanes = RDX_PINF_LANES;   // decode lanes per block (k_pinf_block / k_pinf_emit)
+constexpr uint32_t kPinfMaxRounds = 8;    // pointer-jumping launches (each chases up to 16 links per byte)
+constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
+
+enum : uint32_t { kPinfFallback = 0, kPinfOk = 1, kPinfMiss = 2 };
+
+// one candidate block start, decoded
+struct PinfBlk {
+    uint64_t end;      // bit after its end-of-block code (stored: after its data)
+    uint64_t bytes;    // output bytes
+    uint64_t body;     // first bit of the body (stored: of the data)
+    uint32_t status;   // 0 decoded, 1 error (on its own path)
+    uint32_t nlanes;   // lanes with verified starts (the last one ends the block)
+    uint32_t nlen, ndist;
+};
+
+struct PinfState {
+    uint32_t n_cand, overflow;        // candidates found (k_pinf_find, + the host's forced ones)
+    uint32_t n_chain, status;         // k_pinf_chain: blocks on the chain, kPinf*
+    uint64_t miss_bit;                // kPinfMiss: the block start no candidate covers
+    uint32_t miss_type, emit_err;     // its BTYPE; k_pinf_emit / k_pinf_finish errors
+    uint64_t total;                   // output bytes
+    uint64_t trailer_byte;            // the checksum trailer (aligned byte position)
+    uint32_t unresolved[kPinfMaxRounds];
+    uint32_t final_ok, n_match;       // k_pinf_check's verdict; long-match records of k_pinf_emit
+};
+
+struct PinfArgs {
+    const uint32_t *w;      // the stream as dwords from its 4-byte aligned base
+    uint64_t nw;            // dwords holding stream bytes
+    uint32_t lmask;         // valid bytes of the last dword
+    uint32_t format;        // RDX_COMPRESSION_GZIP / ZLIB
+    uint64_t first_byte;    // the stream's first byte in aligned coordinates (its base's skew)
+    uint64_t end_byte;      // first byte past it
+    uint64_t end_bits;      // 8 * end_byte
+    uint64_t *cand;         // [kPinfMaxCand] bit << 2 | type (0 stored: bit of LEN; 1 fixed; 2 dynamic)
+    PinfBlk *blk;           // [kPinfMaxCand]
+    uint64_t *lst;          // [kPinfMaxCand][kPinfLanes] lane starts
+    uint32_t *lnb;          // [kPinfMaxCand][kPinfLanes] lane output bytes
+    uint8_t *lens;          // [kPinfMaxCand][320] code lengths
+    uint32_t *chain;        // [kPinfMaxCand] candidate of each chain block
+    uint64_t *coff;         // [kPinfMaxCand] its output offset
+    PinfState *state;
+    uint32_t *src;          // [total] the source of every output byte
+    uint8_t *out;           // [total] (16-byte aligned)
+    uint64_t *partial;      // [kPinfMaxParts][3] checksum partials
+    uint4 *mlist;           // [mcap] long matches (o, len, dist): written by k_pinf_expand
+    uint32_t mcap;
+    uint64_t *prof;         // RDX_PINF_PROF: per-workgroup (start, end) of k_pinf_block, then k_pinf_emit; else null
+};
+
+hipError_t launch_pinf_find(const PinfArgs &a, hipStream_t s);
+hipError_t launch_pinf_block(const PinfArgs &a, uint32_t first, uint32_t count, hipStream_t s);
+hipError_t launch_pinf_chain(const PinfArgs &a, hipStream_t s);
+hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total, int cus, hipStream_t s);
+
+}  // namespace rdx

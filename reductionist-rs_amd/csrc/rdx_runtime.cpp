@@ -28,6 +28,7 @@
 #include "../../include/rdx.h"
 #include "rdx_cbor.hpp"
 #include "rdx_kernels.hpp"
+#include "rdx_pinflate.h"
 #include "rdx_plan.hpp"
 
 using namespace rdx;
@@ -79,6 +80,9 @@ struct Tuning {
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
     int direct_max = env_int("RDX_DIRECT_MAX", 1);                     // idle-queue fast path: callers launching at once
     int idle_passes = env_int("RDX_DISPATCH_IDLE_PASSES", 512);        // dispatcher: empty polls before it naps
+    int pinflate = env_int("RDX_PINFLATE", 1);                         // a lone gzip / zlib stream: k_pinflate
+    int pinflate_min = env_int("RDX_PINFLATE_MIN_BYTES", 1024);        // ... from this many compressed bytes
+    int pinflate_prof = env_int("RDX_PINF_PROF", 0);                   // tuning: per-workgroup times to stderr
 #if RDX_PROBES
     int epoch_start = env_int("RDX_EPOCH_START", 0);                   // tests: start workspaces' tags near the wrap
 #endif
@@ -139,6 +143,12 @@ struct rdx_workspace {
     // the coalescer's idle-queue fast path: this workspace's own page-locked result slots (a one-request
     // lane launched on the caller's thread; rdx_device.hpp put_host_slot)
     uint64_t *h_slot = nullptr;
+    // k_pinflate (one stream decoded by the whole device): its scratch arena, the byte sources, and the
+    // page-locked copy of its state
+    DevBuf<uint8_t> pinf;
+    DevBuf<uint32_t> psrc;
+    DevBuf<uint64_t> pprof;
+    PinfState *pinf_back = nullptr;
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
     hipEvent_t piece_ev[8] = {};
@@ -598,6 +608,124 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
 }
 
 thread_local uint32_t g_inflate_error = RDX_INFLATE_OK;
+thread_local uint32_t g_inflate_path = RDX_INFLATE_PATH_NONE;
+
+// ---- one gzip / zlib stream decoded by the whole device (k_pinflate.hip) ------------------------------
+// Returns RDX_OK with the stream's bytes in ws->raw (*raw_len of them), kNotDecoded when the sequential
+// decoder must run (an error anywhere, a chain it could not follow), or a device / memory error.
+const rdx_status kNotDecoded = static_cast<rdx_status>(254);
+
+rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_t *d_src, uint64_t len, hipStream_t s,
+                           uint64_t *raw_len) {
+    rdx_status st;
+    // arena: state | cand | blk | chain | coff | partial | lens | lnb | lst
+    constexpr uint64_t oState = 0, oCand = 256, oBlk = oCand + 8ull * kPinfMaxCand,
+                       oChain = oBlk + sizeof(PinfBlk) * kPinfMaxCand, oCoff = oChain + 4ull * kPinfMaxCand,
+                       oPart = oCoff + 8ull * kPinfMaxCand, oLens = oPart + 24ull * kPinfMaxParts,
+                       oLnb = oLens + 320ull * kPinfMaxCand, oLst = oLnb + 4ull * kPinfMaxCand * kPinfLanes,
+                       oEnd = oLst + 8ull * kPinfMaxCand * kPinfLanes;
+    static_assert(sizeof(PinfState) <= 256, "state slot");
+    if ((st = ensure(ws, ws->pinf, oEnd, s))) return st;
+    if (!ws->pinf_back) RDX_HIP(hipHostMalloc((void **)&ws->pinf_back, sizeof(PinfState), hipHostMallocDefault));
+    uint8_t *ar = ws->pinf.p;
+    PinfArgs a{};
+    const uint64_t skew = (uintptr_t)d_src & 3;
+    a.w = reinterpret_cast<const uint32_t *>(d_src - skew);
+    a.first_byte = skew;
+    a.end_byte = skew + len;
+    a.end_bits = 8 * a.end_byte;
+    a.nw = (a.end_byte + 3) / 4;
+    a.lmask = a.end_byte % 4 ? (1u << (8 * (a.end_byte % 4))) - 1 : 0xffffffffu;
+    a.format = compression;
+    a.state = reinterpret_cast<PinfState *>(ar + oState);
+    a.cand = reinterpret_cast<uint64_t *>(ar + oCand);
+    a.blk = reinterpret_cast<PinfBlk *>(ar + oBlk);
+    a.chain = reinterpret_cast<uint32_t *>(ar + oChain);
+    a.coff = reinterpret_cast<uint64_t *>(ar + oCoff);
+    a.partial = reinterpret_cast<uint64_t *>(ar + oPart);
+    a.lens = ar + oLens;
+    a.lnb = reinterpret_cast<uint32_t *>(ar + oLnb);
+    a.lst = reinterpret_cast<uint64_t *>(ar + oLst);
+    if (tuning().pinflate_prof) {
+        if ((st = ensure(ws, ws->pprof, 16ull * kPinfMaxCand, s))) return st;
+        RDX_HIP(hipMemsetAsync(ws->pprof.p, 0, 128ull * kPinfMaxCand, s));
+        a.prof = ws->pprof.p;
+    }
+    RDX_HIP(hipMemsetAsync(a.state, 0, sizeof(PinfState), s));
+    RDX_HIP(launch_pinf_find(a, s));
+    RDX_HIP(launch_pinf_block(a, 0, kPinfMaxCand, s));
+    PinfState &h = *ws->pinf_back;
+    for (uint32_t forced = 0;; ++forced) {
+        RDX_HIP(launch_pinf_chain(a, s));
+        RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipStreamSynchronize(s));
+        if (h.status != kPinfMiss) break;
+        // a block start no candidate covers (a fixed-Huffman block, or a header the finder's zlib-encoder
+        // rules reject): decode that one block and follow the chain again
+        const uint32_t n = h.n_cand;
+        if (forced >= 64 || n >= kPinfMaxCand || h.miss_type == 3) return kNotDecoded;
+        const uint64_t e = h.miss_bit;
+        const uint64_t key = h.miss_type == 0 ? (8 * ((e + 3 + 7) / 8)) << 2 : e << 2 | h.miss_type;
+        const uint32_t n1 = n + 1;
+        RDX_HIP(hipMemcpyAsync(a.cand + n, &key, sizeof key, hipMemcpyHostToDevice, s));
+        RDX_HIP(hipMemcpyAsync(&a.state->n_cand, &n1, sizeof n1, hipMemcpyHostToDevice, s));
+        RDX_HIP(launch_pinf_block(a, n, 1, s));
+        RDX_HIP(hipStreamSynchronize(s));   // the host values above are on the stack
+    }
+    if (h.status != kPinfOk) return kNotDecoded;
+    const uint64_t total = h.total;
+    if ((st = ensure(ws, ws->raw, std::max<uint64_t>((total + 15) / 16 * 16, 16), s))) return st;
+    // the sources, then the long-match records (at most total / 32 of them)
+    const uint64_t mcap = total / 32;
+    if ((st = ensure(ws, ws->psrc, std::max<uint64_t>(total + 4 * mcap + 4, 1), s))) return st;
+    a.src = ws->psrc.p;
+    a.mlist = reinterpret_cast<uint4 *>(ws->psrc.p + (total + 3) / 4 * 4);
+    a.mcap = (uint32_t)mcap;
+    a.out = ws->raw.p;
+    RDX_HIP(launch_pinf_rest(a, h.n_chain, total, ws->cus, s));
+    RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
+    RDX_HIP(hipStreamSynchronize(s));
+    if (a.prof) {   // tuning: the slowest workgroups of k_pinf_block / k_pinf_emit, phase by phase
+        std::vector<uint64_t> pr(16ull * kPinfMaxCand);
+        std::vector<uint64_t> keys(kPinfMaxCand);
+        std::vector<PinfBlk> blks(kPinfMaxCand);
+        std::vector<uint32_t> chain(kPinfMaxCand);
+        RDX_HIP(hipMemcpy(pr.data(), a.prof, pr.size() * 8, hipMemcpyDeviceToHost));
+        RDX_HIP(hipMemcpy(keys.data(), a.cand, keys.size() * 8, hipMemcpyDeviceToHost));
+        RDX_HIP(hipMemcpy(blks.data(), a.blk, blks.size() * sizeof(PinfBlk), hipMemcpyDeviceToHost));
+        RDX_HIP(hipMemcpy(chain.data(), a.chain, chain.size() * 4, hipMemcpyDeviceToHost));
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t n = k == 0 ? std::min(h.n_cand, kPinfMaxCand) : h.n_chain;
+            uint64_t lo = ~0ull, hi = 0, worst = 0;
+            uint32_t wi = 0;
+            std::vector<uint64_t> d;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint64_t *w = &pr[8 * (k * kPinfMaxCand + i)];
+                if (!w[0]) continue;
+                lo = std::min(lo, w[0]);
+                hi = std::max(hi, w[4]);
+                d.push_back(w[4] - w[0]);
+                if (w[4] - w[0] > worst) { worst = w[4] - w[0]; wi = i; }
+            }
+            std::sort(d.begin(), d.end());
+            const uint32_t c = k == 0 ? wi : chain[wi];
+            const uint64_t *w = &pr[8 * (k * kPinfMaxCand + wi)];
+            auto us = [&](uint64_t x) { return x > w[0] ? (x - w[0]) / 100.0 : -1.0; };
+            std::fprintf(stderr, "{\"pinf_prof\": \"%s\", \"wgs\": %zu, \"span_us\": %.1f, \"median_us\": %.1f, "
+                         "\"max_us\": %.1f, \"max_cand\": %u, \"type\": %u, \"bytes\": %llu, \"bits\": %llu, "
+                         "\"lanes\": %u, \"status\": %u, \"t_tables\": %.1f, \"t_pass0\": %.1f, \"t_agree\": %.1f, "
+                         "\"rounds\": %llu, \"walks\": %llu, \"exts\": %llu}\n", k ? "emit" : "block", d.size(),
+                         (hi - lo) / 100.0, d.empty() ? 0.0 : d[d.size() / 2] / 100.0, worst / 100.0, c,
+                         (unsigned)(keys[c] & 3), (unsigned long long)blks[c].bytes,
+                         (unsigned long long)(blks[c].end - (keys[c] >> 2)), blks[c].nlanes, blks[c].status, us(w[1]),
+                         us(w[2]), us(w[3]), (unsigned long long)(k ? 0 : w[5]), (unsigned long long)(k ? 0 : w[6]),
+                         (unsigned long long)(k ? 0 : w[7]));
+        }
+    }
+    if (!h.final_ok) return kNotDecoded;
+    *raw_len = total;
+    return RDX_OK;
+}
 
 // compression::decompress (compression.rs:18-27) of n device-resident streams into d_out (stream i at
 // d_out + i*cap), asynchronous on s.
@@ -674,7 +802,8 @@ rdx_status decompress_launch(rdx_workspace *ws, uint32_t compression, uint64_t n
 // RDX_INFLATE_OUTPUT_OVERFLOW, so a stream longer than the shape implies still decodes to its end and
 // meets validate_raw_size (app.rs:169-172) exactly like the reference.
 rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const uint8_t *d_src, uint64_t len,
-                              uint64_t size_hint, hipStream_t s, uint64_t *raw_len, const uint8_t *h_src = nullptr) {
+                              uint64_t size_hint, hipStream_t s, uint64_t *raw_len, const uint8_t *h_src = nullptr,
+                              bool any_size = false) {
     g_inflate_error = RDX_INFLATE_OK;
     const bool blosc2 = req.compression == RDX_COMPRESSION_BLOSC2;
     if (req.compression != RDX_COMPRESSION_GZIP && req.compression != RDX_COMPRESSION_ZLIB && !blosc2)
@@ -689,6 +818,17 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
     if (blosc2 && size_hint) cap = size_hint;   // the header's nbytes (read on the host)
     if (cap == 0) cap = 4 * len + 4096;
     rdx_status st;
+    g_inflate_path = RDX_INFLATE_PATH_SERIAL;
+    if (!blosc2 && tuning().pinflate && (any_size || len >= (uint64_t)std::max(0, tuning().pinflate_min))) {
+        // a lone stream: the whole device decodes it; anything it does not accept goes to k_inflate below
+        st = pinflate_stream(ws, req.compression, d_src, len, s, raw_len);
+        if (st == RDX_OK) {
+            g_inflate_path = RDX_INFLATE_PATH_PARALLEL;
+            return RDX_OK;
+        }
+        if (st != kNotDecoded) return st;
+        g_inflate_path = RDX_INFLATE_PATH_PARALLEL_FALLBACK;
+    }
     if ((st = ensure(ws, ws->zout_len, 1, s))) return st;
     if ((st = ensure(ws, ws->zerr, 1, s))) return st;
     if (!ws->zback) RDX_HIP(hipHostMalloc((void **)&ws->zback, 2 * sizeof(uint64_t), hipHostMallocDefault));
@@ -783,6 +923,10 @@ void destroy_workspace(rdx_workspace *ws) {
         if (e) (void)hipEventDestroy(e);
     if (ws->zback) (void)hipHostFree(ws->zback);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
+    if (ws->pinf_back) (void)hipHostFree(ws->pinf_back);
+    fr(ws->pinf.p);
+    fr(ws->psrc.p);
+    fr(ws->pprof.p);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
     if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
@@ -1029,6 +1173,8 @@ const char *rdx_inflate_error_string(uint32_t code) {
 }
 
 uint32_t rdx_inflate_last_error(void) { return g_inflate_error; }
+
+uint32_t rdx_inflate_last_path(void) { return g_inflate_path; }
 
 uint32_t rdx_last_unsupported_reason(void) { return last_unsupported(); }
 
@@ -2078,6 +2224,36 @@ rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, 
     return decompress_launch(ws, compression, n, reinterpret_cast<const uint8_t *const *>(h_in_ptrs), h_in_lens,
                              static_cast<uint8_t *>(d_out), out_capacity, d_out_lens, d_errors,
                              static_cast<hipStream_t>(stream));
+}
+
+rdx_status rdx_decompress_one_device(rdx_workspace *ws, uint32_t compression, const void *d_in, uint64_t len,
+                                     void *d_out, uint64_t out_cap, uint64_t *out_len, uint32_t *error,
+                                     void *stream) {
+    if (!ws || !out_len || !error || (!d_in && len) || (!d_out && out_cap) ||
+        (compression != RDX_COMPRESSION_GZIP && compression != RDX_COMPRESSION_ZLIB))
+        return RDX_E_INVALID_ARGUMENT;
+    RDX_HIP(hipSetDevice(ws->device));
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    rdx_request req{};
+    req.abi_version = RDX_ABI_VERSION;
+    req.compression = compression;
+    uint64_t n = 0;
+    *out_len = 0;
+    const rdx_status st = decompress_request(ws, req, static_cast<const uint8_t *>(d_in), len, 0, s, &n, nullptr, true);
+    if (st == RDX_E_DECOMPRESSION) {
+        *error = g_inflate_error;
+        return RDX_OK;
+    }
+    if (st) return st;
+    *out_len = n;
+    if (n > out_cap) {
+        *error = RDX_INFLATE_OUTPUT_OVERFLOW;
+        return RDX_OK;
+    }
+    if (n) RDX_HIP(hipMemcpyAsync(d_out, ws->raw.p, n, hipMemcpyDeviceToDevice, s));
+    RDX_HIP(hipStreamSynchronize(s));
+    *error = RDX_INFLATE_OK;
+    return RDX_OK;
 }
 
 rdx_status rdx_execute(rdx_context *ctx, const rdx_request *req, const void *chunk, uint64_t chunk_len, void *body,

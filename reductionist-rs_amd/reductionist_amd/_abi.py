@@ -185,6 +185,8 @@ def _declare(lib):
         "rdx_execute_batch_device": (C.c_int, [VP, req_p, U64, P(VP), U64, VP, VP, VP, VP, info_p]),
         "rdx_inflate_error_string": (C.c_char_p, [C.c_uint32]),
         "rdx_inflate_last_error": (C.c_uint32, []),
+        "rdx_inflate_last_path": (C.c_uint32, []),
+        "rdx_decompress_one_device": (C.c_int, [VP, C.c_uint32, VP, U64, VP, U64, P(U64), P(C.c_uint32), VP]),
         "rdx_last_unsupported_reason": (C.c_uint32, []),
         "rdx_decompress_batch_device": (C.c_int, [VP, C.c_uint32, U64, P(VP), P(U64), VP, U64, VP, VP, VP]),
         "rdx_blosc2_cbuffer_sizes": (C.c_int, [VP, U64, P(U64), P(U64), P(U64)]),
@@ -215,7 +217,8 @@ EXPORTED = ["rdx_abi_version", "rdx_status_string", "rdx_device_count", "rdx_con
             "rdx_inflate_last_error", "rdx_decompress_batch_device", "rdx_execute_multi_device",
             "rdx_execute_owned", "rdx_result_free", "rdx_cbor_bound", "rdx_cbor_encode", "rdx_cbor_encode_device",
             "rdx_execute_cbor", "rdx_blosc2_cbuffer_sizes", "rdx_last_unsupported_reason",
-            "rdx_context_configure", "rdx_context_stats", "rdx_execute_resident"]
+            "rdx_context_configure", "rdx_context_stats", "rdx_execute_resident", "rdx_inflate_last_path",
+            "rdx_decompress_one_device"]
 
 
 def lib():

@@ -184,6 +184,18 @@ class Workspace:
         check(self.lib.rdx_execute_multi_device(self.ws, n, arr, C.c_void_p(stream or 0), statuses, infos))
         return [int(x) for x in statuses[:n]], [infos[i] for i in range(n)]
 
+    def decompress_one_device(self, compression: str, d_in: int, length: int, d_out: int, out_capacity: int,
+                              stream: int | None = None):
+        """rdx_decompress_one_device: one device-resident gzip / zlib stream decoded by the whole device
+        (k_pinflate, or k_inflate for a stream it declines), synchronously.  Returns (rdx_inflate_error,
+        decompressed size, rdx_inflate_last_path)."""
+        n = C.c_uint64()
+        err = C.c_uint32()
+        check(self.lib.rdx_decompress_one_device(self.ws, _abi.COMPRESSION[compression], C.c_void_p(d_in), length,
+                                                 C.c_void_p(d_out), out_capacity, C.byref(n), C.byref(err),
+                                                 C.c_void_p(stream or 0)))
+        return int(err.value), int(n.value), int(self.lib.rdx_inflate_last_path())
+
     def decompress_batch_device(self, compression: str, d_streams: Sequence[int], lens: Sequence[int], d_out: int,
                                 out_capacity: int, d_out_lens: int, d_errors: int, stream: int | None) -> None:
         """compression::decompress (compression.rs:18-27) of device-resident gzip/zlib streams:
