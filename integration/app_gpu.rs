@@ -38,16 +38,23 @@ pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
     request_data: models::RequestData,
     data: Bytes,
 ) -> Result<models::Response, ActiveStorageError> {
-    // gzip / zlib: one request = one DEFLATE stream, and a stream is serial: a wavefront decodes a 4 MiB
-    // chunk in ~100-220 ms, a CPU core in ~4-7 ms.  A lone gzip/zlib request therefore
-    // keeps the reference's host decompression (compression.rs:18-27); those chunks are inflated on the
-    // device only in batches (rdx_decompress_batch_device).
+    // gzip / zlib: a lone request's DEFLATE stream is decoded by the whole device (k_pinflate, DESIGN.md
+    // §9.2: candidate block starts, blocks and the symbols inside them decoded in parallel, then the copies
+    // resolved) — faster than the reference's host decoder on one core for the chunks scientific data
+    // gives (profiles/r04_pinflate_probe.jsonl).  A stream whose request states it expands more than
+    // 16-fold (long matches, few blocks: the parallel decode has little to split) keeps the host path, as
+    // does any request when REDUCTIONIST_GPU_INFLATE=0.
     // blosc2: a chunk is hundreds of independent block streams that the device decodes in parallel
     // (k_blosc2), but a lone 4 MiB chunk still takes 1.6-1.7 ms there, and no record here
     // shows that beating the reference's host decoder for ONE request; so a lone blosc2 request is
     // decompressed on the host too unless the operator opts in (REDUCTIONIST_GPU_BLOSC2=1).  A codec the
     // device does not decode comes back as UnsupportedOperation and is decompressed here instead.
-    if request_data.compression == Some(models::Compression::Blosc2) && gpu_blosc2() {
+    let on_device = match request_data.compression {
+        Some(models::Compression::Blosc2) => gpu_blosc2(),
+        Some(_) => gpu_inflate(&request_data, data.len()),
+        None => false,
+    };
+    if on_device {
         match debug_span!("operation_gpu").in_scope(|| operations_gpu::execute_slice(&request_data, &data, T::OP)) {
             Err(ActiveStorageError::UnsupportedOperation { .. }) => {}
             other => return other,
@@ -60,6 +67,22 @@ pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
     // the chunk as downloaded — page-locked when the downloader filled a pinned_gpu::PinnedBuf — straight
     // to the engine: no Bytes -> Vec conversion (zero copies, app.rs:173-181's intent)
     debug_span!("operation_gpu").in_scope(|| operations_gpu::execute_slice(&request_data, &data, T::OP))
+}
+
+/// Lone gzip / zlib requests decoded on the device (see operation_gpu): on unless REDUCTIONIST_GPU_INFLATE=0,
+/// and not for a request whose shape says the chunk expands more than 16-fold.
+fn gpu_inflate(request_data: &models::RequestData, compressed_len: usize) -> bool {
+    static ON: std::sync::OnceLock<bool> = std::sync::OnceLock::new();
+    if !*ON.get_or_init(|| std::env::var("REDUCTIONIST_GPU_INFLATE").map(|v| v != "0").unwrap_or(true)) {
+        return false;
+    }
+    match &request_data.shape {
+        Some(shape) => {
+            let raw = shape.iter().product::<usize>().saturating_mul(request_data.dtype.size_of());
+            raw <= compressed_len.saturating_mul(16)
+        }
+        None => true,
+    }
 }
 
 /// Lone blosc2 requests decoded on the device (opt-in: REDUCTIONIST_GPU_BLOSC2=1; see operation_gpu).
@@ -93,10 +116,15 @@ pub async fn operation_handler_cbor<const OP: u32>(
     let mem_permits = state.resource_manager.memory(memory).await?;
     let data = state.chunk_store.get(&auth, &request_data, &state.resource_manager, mem_permits).await?;
     let run = move || -> Result<Bytes, ActiveStorageError> {
-        // a lone compressed chunk is decompressed on the host, as in operation_gpu (blosc2 goes to the
-        // device only with REDUCTIONIST_GPU_BLOSC2=1)
+        // a lone compressed chunk goes to the device as in operation_gpu (gzip / zlib unless the request
+        // says it expands more than 16-fold; blosc2 only with REDUCTIONIST_GPU_BLOSC2=1), else the host
+        let on_device = match request_data.compression {
+            Some(models::Compression::Blosc2) => gpu_blosc2(),
+            Some(_) => gpu_inflate(&request_data, data.len()),
+            None => true,
+        };
         let (request_data, data) = match request_data.compression {
-            Some(c) if c != models::Compression::Blosc2 || !gpu_blosc2() => {
+            Some(c) if !on_device => {
                 let d = compression::decompress(c, &data)?;
                 (host_decompressed(request_data), d)
             }

@@ -10,7 +10,7 @@
 //                   byte offset for a stored block (LEN = ~NLEN, zero bits before it): the candidates
 //                   (every such block start, plus rare false ones).
 //  2. k_pinf_block  one workgroup per candidate parses its header with the oracle's checks, builds the
-//                   decode tables in LDS and decodes the block body with 256 lanes at once: lane k starts
+//                   decode tables in LDS and decodes the block body with 1024 lanes at once: lane k starts
 //                   at an arbitrary bit of the body (Huffman decoding resynchronises within a few
 //                   symbols), stops at its first symbol boundary past its range, and is valid once its
 //                   start equals the exit of lane k-1; a mismatched lane re-decodes from that exit, in
@@ -25,11 +25,12 @@
 //                   writes every output byte as a 32-bit SOURCE: a literal (flag | byte) or the position
 //                   the byte copies (o - dist; inside an overlapping match, (j mod dist) into the bytes
 //                   before it).
-//  5. k_pinf_resolve  pointer jumping over the sources, in place (each pass chases up to 16 links per
-//                   byte; a link always points to a byte with the same final value), until every byte is
-//                   a literal.
-//  6. k_pinf_finish / k_pinf_check  the bytes, Adler-32 / CRC-32 over segments combined by weights /
-//                   GF(2) shifts, the trailer.
+//  5. k_pinf_tile   pointer jumping over the sources inside 32 KiB tiles of output in LDS (a link always
+//                   points to a byte with the same final value) until each byte is a literal or a link
+//                   into the previous tile; k_pinf_scan then walks the tiles in order, the previous
+//                   tile's bytes in LDS, and writes the bytes.
+//  6. k_pinf_finish / k_pinf_check  Adler-32 / CRC-32 over segments combined by weights / GF(2) shifts,
+//                   the trailer.
 //
 // The path only ever ACCEPTS a stream the sequential decoder accepts, with the same bytes: any error on
 // the chain, a chain that cannot be followed, an unresolved byte or a checksum mismatch reports "not
@@ -45,10 +46,10 @@ namespace {
 
 constexpr uint32_t kLanes = kPinfLanes;    // decode lanes (threads) per block
 #ifndef RDX_PINF_MINBITS
-#define RDX_PINF_MINBITS 512
+#define RDX_PINF_MINBITS 256
 #endif
 constexpr uint64_t kMinLaneBits = RDX_PINF_MINBITS;   // a lane's share of a block body, at least
-constexpr uint32_t kRoot = 10, kDRoot = 8; // LDS root tables: literal/length, distance
+constexpr uint32_t kRoot = 11, kDRoot = 9; // LDS root tables: literal/length, distance
 constexpr uint32_t kFlag = 0x80000000u;    // a source that is a literal byte
 constexpr uint32_t kRounds = 6;            // resync rounds before a sequential walk
 constexpr uint64_t kMaxSpan = 1ull << 21;  // bits a candidate may decode (a zlib block is < 1.6 M bits)
@@ -64,7 +65,8 @@ __constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 
 __constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
                                      193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
 __constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-__constant__ uint8_t c_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+typedef const __attribute__((address_space(3))) uint32_t *lds_u32p;   // an LDS pointer: ds_read, not flat
 
 // ---- the stream as dwords from its 4-byte aligned base (bit positions in those coordinates) ------------
 struct Stream {
@@ -72,7 +74,7 @@ struct Stream {
     uint64_t nw;        // dwords holding stream bytes
     uint32_t lmask;     // valid bytes of the last one
     // a window of the stream staged in LDS (dwords [l0, l0 + ln)), read instead of L2 where it covers
-    const uint32_t *lds;
+    lds_u32p lds;
     uint64_t l0;
     uint32_t ln;
     __device__ __forceinline__ uint32_t ldg(uint64_t i) const {
@@ -89,7 +91,7 @@ struct Stream {
     __device__ __forceinline__ void stage(uint32_t *buf, uint32_t cap, uint64_t i0, uint64_t i1) {
         const uint32_t n = (uint32_t)min<uint64_t>(cap, i1 > i0 ? i1 - i0 : 0);
         for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) buf[k] = ldg(i0 + k);
-        lds = buf;
+        lds = (lds_u32p)buf;
         l0 = i0;
         ln = n;
         __syncthreads();
@@ -142,10 +144,13 @@ struct Bits {
 };
 
 // ---- Huffman tables in LDS --------------------------------------------------------------------------
+// Per code: count[len] (count[0] = unused symbols), first[len] = the first canonical code of that length
+// and offs[len] = its first symbol's index in sym[] (puff's running `first` / `index`), the symbols in
+// canonical order, and a root table of 2^root entries (codes up to `root` bits in one lookup).
 struct Tabs {
     uint32_t lit[1u << kRoot];
     uint32_t dist[1u << kDRoot];
-    uint16_t lcount[16], dcount[16];
+    uint16_t lcount[16], dcount[16], lfirst[16], dfirst[16], loffs[16], doffs[16];
     uint16_t lsym[288], dsym[32];
     uint8_t lens[320];
 };
@@ -161,10 +166,10 @@ __device__ __forceinline__ uint32_t entry_of(uint32_t s, bool litlen) {
     return kTyBad;
 }
 
-// Canonical code of n lengths -> root table + count[] / sym[] (for codes longer than the root), built by
-// one wavefront (ballot ranks).  Returns puff's `left`: 0 complete, > 0 incomplete, < 0 over-subscribed.
-__device__ int build(const uint8_t *lens, uint32_t n, uint32_t *tab, uint32_t root, uint16_t *count, uint16_t *sym,
-                     bool litlen, uint32_t lane) {
+// Counts, first codes, offsets and canonical symbol order of n lengths, by one wavefront (ballot ranks).
+// Returns puff's `left`: 0 complete, > 0 incomplete, < 0 over-subscribed.
+__device__ int code_counts(const uint8_t *lens, uint32_t n, uint16_t *count, uint16_t *first, uint16_t *offs,
+                           uint16_t *sym, uint32_t lane) {
     uint32_t cnt[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) cnt[l] = 0;
@@ -176,26 +181,32 @@ __device__ int build(const uint8_t *lens, uint32_t n, uint32_t *tab, uint32_t ro
     }
     int left = 1;
     bool over = false;
-    uint32_t offs[16], next[16];
-    offs[0] = 0;
-    offs[1] = 0;
-    next[0] = 0;
-    uint32_t code = 0;
+    uint32_t of[16], fi[16];
+    of[0] = fi[0] = 0;
+    of[1] = fi[1] = 0;
 #pragma unroll
     for (int l = 1; l < 16; ++l) {
         left <<= 1;
         left -= (int)cnt[l];
         over |= left < 0;
-        if (l < 15) offs[l + 1] = offs[l] + cnt[l];
-        code = (code + (l == 1 ? 0 : cnt[l - 1])) << 1;
-        next[l] = code;
+        if (l < 15) {
+            of[l + 1] = of[l] + cnt[l];
+            fi[l + 1] = (fi[l] + cnt[l]) << 1;
+        }
     }
-    for (uint32_t i = lane; i < (1u << root); i += 64) tab[i] = 0;
-    if (lane < 16) count[lane] = (uint16_t)cnt[lane];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    if (lane < 16) {
+        uint32_t c = 0, f = 0, o = 0;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            c = lane == (uint32_t)l ? cnt[l] : c;
+            f = lane == (uint32_t)l ? fi[l] : f;
+            o = lane == (uint32_t)l ? of[l] : o;
+        }
+        count[lane] = (uint16_t)c;
+        first[lane] = (uint16_t)f;
+        offs[lane] = (uint16_t)o;
+    }
     if (over) return -1;
-    if (cnt[0] == n) return left;   // no codes at all
     uint32_t run[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) run[l] = 0;
@@ -203,46 +214,69 @@ __device__ int build(const uint8_t *lens, uint32_t n, uint32_t *tab, uint32_t ro
     for (uint32_t b0 = 0; b0 < n; b0 += 64) {
         const uint32_t s = b0 + lane;
         const uint32_t l = s < n ? lens[s] : 0;
-        uint32_t rank = 0, off = 0, nx = 0;
+        uint32_t rank = 0, off = 0;
 #pragma unroll
         for (int q = 1; q < 16; ++q) {
             const uint64_t m = __ballot(l == (uint32_t)q);
             if (l == (uint32_t)q) {
                 rank = run[q] + (uint32_t)__popcll(m & lt);
-                off = offs[q];
-                nx = next[q];
+                off = of[q];
             }
             run[q] += (uint32_t)__popcll(m);
         }
-        if (l) {
-            sym[off + rank] = (uint16_t)s;
-            if (l <= root) {
-                const uint32_t c = nx + rank;
-                const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
-                const uint32_t e = entry_of(s, litlen) | l << 16;
-                for (uint32_t k = r; k < (1u << root); k += 1u << l) tab[k] = e;
-            }
-        }
+        if (l) sym[off + rank] = (uint16_t)s;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     return left;
 }
 
-// A code longer than the root (or no code): the canonical bit-serial walk (puff's decode()) over the bits
-// in `bb`; returns the entry with its length set, or kTyBad.
-__device__ __noinline__ uint32_t slow_decode(uint64_t bb, const uint16_t *count, const uint16_t *sym, bool litlen) {
-    int code = 0, first = 0, index = 0;
+// The canonical decode of the bits `b` (LSB first) with codes of length lo..hi only: the entry (length in
+// bits 16-19), or 0 when no code of those lengths is a prefix of b.
+__device__ __forceinline__ uint32_t canon(uint32_t b, const uint16_t *count, const uint16_t *first, const uint16_t *offs,
+                                          const uint16_t *sym, bool litlen, int lo, int hi) {
+    uint32_t code = 0, e = 0;
+#pragma unroll
     for (int len = 1; len < 16; ++len) {
-        code |= (int)((bb >> (len - 1)) & 1);
-        const int c = count[len];
-        if (code - c < first) return entry_of(sym[index + (code - first)], litlen) | (uint32_t)len << 16;
-        index += c;
-        first += c;
-        first <<= 1;
-        code <<= 1;
+        code = code << 1 | ((b >> (len - 1)) & 1);
+        if (len >= lo && len <= hi && e == 0 && code < (uint32_t)first[len] + count[len])
+            e = entry_of(sym[offs[len] + code - first[len]], litlen) | (uint32_t)len << 16;
     }
-    return kTyBad | 1u << 16;
+    return e;
+}
+
+// Both codes of a block from T.lens, by every thread of the workgroup: counts by wave 0, then the root
+// tables filled in parallel, one entry per thread and step.  Returns (the same for all threads) whether
+// both codes are acceptable as oracle_inflate's construct() judges them: not over-subscribed, and
+// incomplete only with a single code.
+__device__ bool build_tabs(Tabs &T, uint32_t nl, uint32_t nd) {
+    __shared__ int s_left[2];
+    const uint32_t t = threadIdx.x;
+    if (t < 64) {
+        const int a = code_counts(T.lens, nl, T.lcount, T.lfirst, T.loffs, T.lsym, t);
+        const int b = code_counts(T.lens + nl, nd, T.dcount, T.dfirst, T.doffs, T.dsym, t);
+        if (t == 0) {
+            s_left[0] = a;
+            s_left[1] = b;
+        }
+    }
+    __syncthreads();
+    const int l0 = s_left[0], l1 = s_left[1];
+    const bool ok = !(l0 < 0 || (l0 > 0 && nl != (uint32_t)T.lcount[0] + T.lcount[1])) &&
+                    !(l1 < 0 || (l1 > 0 && nd != (uint32_t)T.dcount[0] + T.dcount[1]));
+    if (ok) {
+        for (uint32_t i = t; i < (1u << kRoot); i += blockDim.x)
+            T.lit[i] = canon(i, T.lcount, T.lfirst, T.loffs, T.lsym, true, 1, kRoot);
+        for (uint32_t i = t; i < (1u << kDRoot); i += blockDim.x)
+            T.dist[i] = canon(i, T.dcount, T.dfirst, T.doffs, T.dsym, false, 1, kDRoot);
+    }
+    __syncthreads();
+    return ok;
+}
+
+// A code longer than the root (or no code at all): the lengths root+1..15 from the same bits.
+__device__ __forceinline__ uint32_t slow_decode(uint64_t bb, const uint16_t *count, const uint16_t *first,
+                                                const uint16_t *offs, const uint16_t *sym, bool litlen, int root) {
+    const uint32_t e = canon((uint32_t)bb, count, first, offs, sym, litlen, root + 1, 15);
+    return e ? e : kTyBad | 1u << 16;
 }
 
 // A lane's sources, written four at a time: entries gather in registers for the aligned quad that holds
@@ -292,7 +326,8 @@ constexpr uint32_t kLongMatch = 32;   // matches at least this long are expanded
 // decoded.  EMIT: also write each byte's source at src[o0 + ...] (and check distances against o0).
 template <bool EMIT>
 __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t stop, uint64_t end_bits,
-                             uint64_t *exit, uint64_t *bytes, uint32_t *src, uint64_t o0, const PinfArgs *pa = nullptr) {
+                             uint64_t *exit, uint64_t *bytes, uint32_t *src, uint64_t o0, const PinfArgs *pa = nullptr,
+                             uint64_t limit = 0) {
     SrcOut out;
     if (EMIT) {
         out.p = src;
@@ -310,11 +345,17 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
         if (p >= stop) break;
         br.refill(S);
         uint32_t e = T.lit[(uint32_t)br.bb & ((1u << kRoot) - 1)];
-        if (((e >> 16) & 15) == 0) e = slow_decode(br.bb, T.lcount, T.lsym, true);
+        if (((e >> 16) & 15) == 0) e = slow_decode(br.bb, T.lcount, T.lfirst, T.loffs, T.lsym, true, kRoot);
         br.drop((e >> 16) & 15);
         const uint32_t ty = e & (3u << 24);
         if (ty == 0) {
-            if (EMIT) out.put(kFlag | (e & 0xff));
+            if (EMIT) {
+                if (o0 + nb >= limit) {   // more output than the block decode counted for this lane
+                    r = 2;
+                    break;
+                }
+                out.put(kFlag | (e & 0xff));
+            }
             ++nb;
             continue;
         }
@@ -331,7 +372,7 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
         br.drop(lx);
         br.refill(S);
         uint32_t d = T.dist[(uint32_t)br.bb & ((1u << kDRoot) - 1)];
-        if (((d >> 16) & 15) == 0) d = slow_decode(br.bb, T.dcount, T.dsym, false);
+        if (((d >> 16) & 15) == 0) d = slow_decode(br.bb, T.dcount, T.dfirst, T.doffs, T.dsym, false, kDRoot);
         if ((d & (3u << 24)) == kTyBad) {
             r = 2;
             break;
@@ -342,8 +383,8 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
         br.drop(dx);
         if (EMIT) {
             const uint64_t q = o0 + nb;
-            if (dist > q) {   // before the start of the output (RDX_INFLATE_DISTANCE)
-                r = 2;
+            if (dist > q || q + len > limit) {   // before the start of the output (RDX_INFLATE_DISTANCE), or
+                r = 2;                           // more output than the block decode counted for this lane
                 break;
             }
             const uint32_t base = (uint32_t)(q - dist);
@@ -432,7 +473,7 @@ __device__ __forceinline__ uint32_t cl_kraft(uint64_t cb) {
     return k;
 }
 
-// The code-length code (19 lengths of 3 bits in cb, field i = symbol c_order[i]) as registers: per-length
+// The code-length code (19 lengths of 3 bits in cb, field i = the i-th symbol of RFC 1951 3.2.7 order) as registers: per-length
 // counts and the symbols packed 5 bits each in (length, symbol) order; then the literal / length and
 // distance code lengths decoded with it, summed into Kraft sums as they come (STORE: also written to
 // lens[]).  The rules are oracle_inflate's: a complete code-length code, no repeat (16) first, no run past
@@ -472,9 +513,18 @@ __device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint
     uint32_t idx = 0, prev = 0;
     kl = kd = used_d = 0;
     eob = false;
+    // the bits through a 64-bit buffer refilled a dword at a time (one LDS read per two or three symbols)
+    uint64_t nxt = pos >> 5;
+    uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
+    uint32_t bc = 64 - (uint32_t)(pos & 31);
+    nxt += 2;
     while (idx < total) {
         if (pos > end_bits) return false;
-        const uint32_t w = S.at(pos);
+        if (bc < 32) {
+            bb |= (uint64_t)S.ld(nxt++) << bc;
+            bc += 32;
+        }
+        const uint32_t w = (uint32_t)bb;
         // canonical walk over lengths 1..7 (predicated; a complete code always decodes)
         int code = 0, first = 0, index = 0, si = -1, len = 0;
 #pragma unroll
@@ -491,23 +541,25 @@ __device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint
         }
         if (si < 0) return false;
         const uint32_t sym = (uint32_t)((si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31);
-        pos += len;
         const uint32_t x = w >> len;
-        uint32_t rep = 1, val = sym;
+        uint32_t rep = 1, val = sym, used = (uint32_t)len;
         if (sym == 16) {
             if (idx == 0) return false;
             val = prev;
             rep = 3 + (x & 3);
-            pos += 2;
+            used += 2;
         } else if (sym == 17) {
             val = 0;
             rep = 3 + (x & 7);
-            pos += 3;
+            used += 3;
         } else if (sym == 18) {
             val = 0;
             rep = 11 + (x & 127);
-            pos += 7;
+            used += 7;
         }
+        pos += used;
+        bb >>= used;
+        bc -= used;
         if (idx + rep > total) return false;
         if (STORE)
             for (uint32_t r = 0; r < rep; ++r) lens[idx + r] = (uint8_t)val;
@@ -536,17 +588,22 @@ __device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, 
 }
 
 // ---- 1. candidates ------------------------------------------------------------------------------------
-// A workgroup tests the bit offsets of kFindBytes bytes (4 per thread) and each of those bytes as the LEN of
-// a stored block.  The bytes and the longest header behind them (<= 4500 bits) are staged in LDS first and
-// read from there only (a surviving offset decodes its header symbol by symbol: each dependent read from L2
-// would cost the wave a round trip).  The 32 offsets of a thread are first screened without branches
-// (BTYPE, HLIT, HDIST, the code-length code's Kraft sum); only the rare survivors decode their headers.
-constexpr uint32_t kFindBytes = 1024, kFindLook = 640;
+// A workgroup tests the bit offsets of kFindBytes bytes and each of those bytes as the LEN of a stored
+// block.  The bytes and the longest header behind them (<= 4500 bits) are staged in LDS first and read from
+// there only (a surviving offset decodes its header symbol by symbol: each dependent read from L2 would
+// cost the lane a round trip).  Rounds of 1024 bytes, 4 per thread: the 32 offsets of a thread are screened
+// without branches (BTYPE, HLIT, HDIST, then the code-length code's Kraft sum), and the survivors (about
+// one offset in a thousand) go to a list in LDS; the list's headers are then decoded one per lane, so that
+// no lane waits on another's survivors.  No global atomics but the rare candidates' (one counter shared
+// by every workgroup serialises in L2: a per-wave atomic cost 150 us on a 3.5 MB stream, profiles/r04_*).
+constexpr uint32_t kFindBytes = 8192, kFindLook = 640;
 constexpr uint32_t kFindWin = (kFindBytes + kFindLook) / 4 + 4;
+constexpr uint32_t kFindList = 8192 + 256;   // a round adds at most 8192; decoded once it holds 256
 
 struct WinStream {   // bit reads from the staged window only (positions inside it by construction)
-    const uint32_t *lds;
+    lds_u32p lds;
     uint64_t l0;
+    __device__ __forceinline__ uint32_t ld(uint64_t i) const { return lds[min((uint32_t)(i - l0), kFindWin - 1)]; }
     __device__ __forceinline__ uint32_t at(uint64_t p) const {
         const uint32_t i = min((uint32_t)((p >> 5) - l0), kFindWin - 2);
         const uint64_t v = (uint64_t)lds[i] | (uint64_t)lds[i + 1] << 32;
@@ -556,13 +613,20 @@ struct WinStream {   // bit reads from the staged window only (positions inside 
 
 __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     __shared__ uint32_t win[kFindWin];
+    __shared__ uint32_t list[kFindList];   // survivors: bit offsets from 8 * q0
+    __shared__ uint32_t n_list;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    // RDX_PINF_PROF: (start, staged, last header pass, end, survivors) per workgroup, after k_pinf_emit's
+    uint64_t *const prof = a.prof && blockIdx.x < kPinfMaxCand ? a.prof + 16ull * kPinfMaxCand + 8ull * blockIdx.x : nullptr;
+    const uint64_t ts0 = prof ? wall_clock64() : 0;
     const Stream G = make_stream(a);
     const uint64_t q0 = a.first_byte + (uint64_t)blockIdx.x * kFindBytes;
     const uint64_t l0 = q0 >= 4 ? (q0 >> 2) - 1 : 0;
-    for (uint32_t k = threadIdx.x; k < kFindWin; k += 256) win[k] = G.ldg(l0 + k);
+    for (uint32_t k = t; k < kFindWin; k += 256) win[k] = G.ldg(l0 + k);
+    if (t == 0) n_list = 0;
     __syncthreads();
     WinStream S;
-    S.lds = win;
+    S.lds = (lds_u32p)win;
     S.l0 = l0;
     PinfState *st = a.state;
     auto push = [&](uint64_t key) {
@@ -570,45 +634,86 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
         if (i < kPinfMaxCand) a.cand[i] = key;
         else atomicOr(&st->overflow, 1u);
     };
-    // this thread's 4 bytes: q0 + 4t .. q0 + 4t + 3 (consecutive: their bits come from one 64-bit window)
-    const uint64_t qt = q0 + 4 * threadIdx.x;
-    // BTYPE = 2 and HLIT, HDIST <= 29 for all 32 offsets from one 64-bit window (no branches)
-    const uint64_t w64 = (uint64_t)S.at(8 * qt) | (uint64_t)S.at(8 * qt + 32) << 32;
-    uint32_t cheap = 0;
+    const uint64_t ts1 = prof ? wall_clock64() : 0;
+    uint64_t ts2 = 0;
+    uint32_t survivors = 0;   // (thread 0: this workgroup's, for the tuning counter)
+    for (uint32_t r = 0; r < kFindBytes / 1024; ++r) {
+        // this thread's 4 bytes: consecutive, so their 32 offsets' bits come from one 64-bit window
+        const uint64_t qt = q0 + 1024 * r + 4 * t;
+        const uint64_t w64 = (uint64_t)S.at(8 * qt) | (uint64_t)S.at(8 * qt + 32) << 32;
+        uint32_t cheap = 0;
 #pragma unroll
-    for (uint32_t b = 0; b < 32; ++b) {
-        const uint32_t h = (uint32_t)(w64 >> b);
-        const bool pass = ((h >> 1) & 3) == 2 && ((h >> 3) & 31) <= 29 && ((h >> 8) & 31) <= 29 && qt + b / 8 < a.end_byte;
-        cheap |= pass ? 1u << b : 0u;
+        for (uint32_t b = 0; b < 32; ++b) {
+            const uint32_t h = (uint32_t)(w64 >> b);
+            const bool pass = ((h >> 1) & 3) == 2 && ((h >> 3) & 31) <= 29 && ((h >> 8) & 31) <= 29 && qt + b / 8 < a.end_byte;
+            cheap |= pass ? 1u << b : 0u;
+        }
+        // the code-length code's Kraft sum (about a fifth of the offsets get here)
+        uint32_t mask = 0;
+        while (cheap) {
+            const uint32_t b = __builtin_ctz(cheap);
+            cheap &= cheap - 1;
+            const uint64_t p = 8 * qt + b;
+            const uint32_t h = (uint32_t)(w64 >> b);
+            const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
+                                ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
+            mask |= cl_kraft(cb) == 128 ? 1u << b : 0u;
+        }
+        // append: one LDS atomic per wave
+        const uint32_t cnt = __builtin_popcount(mask);
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= (uint32_t)d) incl += o;
+        }
+        const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+        uint32_t base = 0;
+        if (lane == 63 && tot) base = atomicAdd(&n_list, tot);
+        base = (uint32_t)__shfl((int)base, 63, 64);
+        uint32_t k = base + incl - cnt;
+        while (mask) {
+            const uint32_t b = __builtin_ctz(mask);
+            mask &= mask - 1;
+            list[k++] = (uint32_t)(8 * (qt - q0) + b);
+        }
+        // stored: LEN, NLEN at q, q+2; the two bits before q are zero (padding or BTYPE 00); the data fits
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint64_t q = qt + j;
+            if (q >= a.first_byte + 1 && q + 4 <= a.end_byte) {
+                const uint32_t v = S.at(8 * q - 8);   // byte q-1, LEN, NLEN (low 8 bits first)
+                const uint32_t len = (v >> 8) & 0xffff;
+                const uint32_t nlen = S.at(8 * q + 16) & 0xffff;
+                if (len == (~nlen & 0xffff) && ((v >> 6) & 3) == 0 && q + 4 + len <= a.end_byte) push((8 * q) << 2 | 0);
+            }
+        }
+        __syncthreads();
+        const uint32_t n = n_list;
+        if (n >= 256 || r + 1 == kFindBytes / 1024) {
+            // the survivors' full header test, one per lane
+            if (prof) ts2 = wall_clock64();
+            for (uint32_t i = t; i < n; i += 256) {
+                const uint64_t p = 8 * q0 + list[i];
+                const uint32_t h = S.at(p);
+                const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
+                                    ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
+                if (dyn_candidate_rest(S, p, a.end_bits, h, cb)) push(p << 2 | 2);
+            }
+            survivors += n;
+            __syncthreads();
+            if (t == 0) n_list = 0;
+            __syncthreads();
+        }
     }
-    // then the code-length code's Kraft sum (about a fifth of the offsets get here)
-    uint32_t mask = 0;
-    while (cheap) {
-        const uint32_t b = __builtin_ctz(cheap);
-        cheap &= cheap - 1;
-        const uint64_t p = 8 * qt + b;
-        const uint32_t h = (uint32_t)(w64 >> b);
-        const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
-                            ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
-        mask |= cl_kraft(cb) == 128 ? 1u << b : 0u;
-    }
-    while (mask) {
-        const uint32_t b = __builtin_ctz(mask);
-        mask &= mask - 1;
-        const uint64_t p = 8 * qt + b;
-        const uint32_t h = S.at(p);
-        const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
-                            ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
-        if (dyn_candidate_rest(S, p, a.end_bits, h, cb)) push(p << 2 | 2);
-    }
-    // stored: LEN, NLEN at q, q+2; the two bits before q are zero (padding or BTYPE 00); the data fits
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint64_t q = qt + k;
-        if (q >= a.first_byte + 1 && q + 4 <= a.end_byte) {
-            const uint32_t v = S.at(8 * q - 8);   // byte q-1, LEN, NLEN (low 8 bits first)
-            const uint32_t len = (v >> 8) & 0xffff;
-            const uint32_t nlen = S.at(8 * q + 16) & 0xffff;
-            if (len == (~nlen & 0xffff) && ((v >> 6) & 3) == 0 && q + 4 + len <= a.end_byte) push((8 * q) << 2 | 0);
+    if (t == 0 && survivors) atomicAdd(&st->n_surv, survivors);
+    if (prof) {
+        __syncthreads();
+        if (t == 0) {
+            prof[0] = ts0;
+            prof[1] = ts1;
+            prof[2] = ts2;
+            prof[3] = wall_clock64();
+            prof[4] = survivors;
         }
     }
 }
@@ -687,16 +792,9 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
         s_ndist = nd;
     }
     __syncthreads();
-    if (t < 64 && s_ok) {
-        const uint32_t nl = s_nlen, nd = s_ndist;
-        int r = build(T.lens, nl, T.lit, kRoot, T.lcount, T.lsym, true, t);
-        bool ok = !(r < 0 || (r > 0 && nl != (uint32_t)T.lcount[0] + T.lcount[1]));
-        r = build(T.lens + nl, nd, T.dist, kDRoot, T.dcount, T.dsym, false, t);
-        ok = ok && !(r < 0 || (r > 0 && nd != (uint32_t)T.dcount[0] + T.dcount[1]));
-        if (t == 0) s_ok = ok ? 1 : 0;
-    }
-    __syncthreads();
-    if (!s_ok) {
+    const bool hdr_ok = s_ok != 0;
+    const bool tabs_ok = hdr_ok && build_tabs(T, s_nlen, s_ndist);
+    if (!tabs_ok) {
         if (t == 0) B.status = 1;
         return;
     }
@@ -1018,10 +1116,7 @@ __device__ void emit_body(const PinfArgs &a) {
     S.stage(win, kWinDwords, l0 >> 5, (B.end >> 5) + 2);
     for (uint32_t i = t; i < 320; i += kLanes) T.lens[i] = a.lens[(uint64_t)c * 320 + i];
     __syncthreads();
-    if (t < 64) {
-        build(T.lens, B.nlen, T.lit, kRoot, T.lcount, T.lsym, true, t);
-        build(T.lens + B.nlen, B.ndist, T.dist, kDRoot, T.dcount, T.dsym, false, t);
-    }
+    build_tabs(T, B.nlen, B.ndist);
     uint64_t *const prof = a.prof ? a.prof + 8ull * (kPinfMaxCand + blockIdx.x) : nullptr;
     const uint32_t nb = t < L ? a.lnb[(uint64_t)c * kLanes + t] : 0;
     // exclusive prefix of the lanes' bytes
@@ -1040,7 +1135,7 @@ __device__ void emit_body(const PinfArgs &a) {
     br.seek(S, a.lst[(uint64_t)c * kLanes + t]);
     const uint64_t stop = t + 1 < L ? a.lst[(uint64_t)c * kLanes + t + 1] : ~0ull;
     uint64_t x, got;
-    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a);
+    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + nb);
     const uint32_t want = t + 1 < L ? 0u : 1u;
     if (r != want || got != nb) atomicOr(&a.state->emit_err, 1u);
 }
@@ -1065,6 +1160,10 @@ __global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
     const uint4 m = a.mlist[r];
     const uint32_t o = m.x, len = m.y, dist = m.z;
     uint32_t *src = a.src;
+    if ((uint64_t)o + len > a.state->total || dist > o || dist == 0) {   // (k_pinf_emit checked it: never)
+        if (lane == 0) atomicOr(&a.state->emit_err, 8u);
+        return;
+    }
     if (dist >= len) {
         for (uint32_t j = lane; j < len; j += 64) src[o + j] = o + j - dist;
     } else {   // overlapping: (j mod dist) into the dist bytes before the match (a float quotient, corrected)
@@ -1078,29 +1177,141 @@ __global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
     }
 }
 
-// ---- 5. pointer jumping ----------------------------------------------------------------------------------
-// One byte per thread; each launch chases up to 8 links per byte and stores where it got to (every link
-// leads to a byte with the same final value, so racing with other threads' stores is harmless).
-__global__ __launch_bounds__(256) void k_pinf_resolve(PinfArgs a, uint32_t round) {
+// ---- 5. sources -> bytes -------------------------------------------------------------------------------
+// Tiles of 32 KiB of output, the DEFLATE window: a link from a tile leads into the same tile or the one
+// before it.  k_pinf_tile (one workgroup per tile, its sources in 128 KiB of LDS) follows every link that
+// stays in the tile, at LDS latency, until each byte is a literal or a link into the previous tile, and
+// writes the tile back as 16-bit entries (a literal byte, or an offset into the previous tile); a tile of
+// literals only writes its bytes.  k_pinf_scan (one workgroup) then walks the tiles in order with the
+// previous tile's bytes in LDS: each entry is its byte or one LDS read.  Links always point back (a copy
+// source precedes its byte); one that does not, or a link further back than the window, is an
+// inconsistency (stale sources after a failed emit): the check rejects the stream.
+constexpr uint32_t kTile = 32768, kTileThreads = 1024;
+
+__global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
+    __shared__ uint32_t tl[kTile];
     PinfState *st = a.state;
-    if (round > 0 && st->unresolved[round - 1] == 0) return;
-    uint32_t *src = a.src;
     const uint64_t N = st->total;
-    // workgroups are dealt to the 8 XCDs round-robin; give each XCD one contiguous eighth of the bytes, so
-    // the links it chases (<= 32 KiB back) stay in its own L2
-    const uint32_t per = (gridDim.x + 7) / 8;
-    const uint32_t tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    const uint64_t o = (uint64_t)tile * 256 + threadIdx.x;
-    bool any = false;
-    if (o < N) {
-        uint32_t v = src[o];
-        if (!(v & kFlag)) {
-            for (uint32_t h = 0; h < 8 && !(v & kFlag); ++h) v = src[v];
-            src[o] = v;
-            any = !(v & kFlag);
+    const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
+    if (T0 >= N) return;
+    const uint32_t n = (uint32_t)min<uint64_t>(kTile, N - T0), t = threadIdx.x;
+    uint32_t *src = a.src + T0;   // (16-byte aligned: the buffer is, and T0 is a multiple of 32 KiB)
+    for (uint32_t i = 4 * t; i < n; i += 4 * kTileThreads) {
+        if (i + 4 <= n) {
+            const uint4 v = gld<uint4>(src + i);
+            tl[i] = v.x;
+            tl[i + 1] = v.y;
+            tl[i + 2] = v.z;
+            tl[i + 3] = v.w;
+        } else {
+            for (uint32_t k = i; k < n; ++k) tl[k] = src[k];
         }
     }
-    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(&st->unresolved[round], 1u);
+    __syncthreads();
+    bool err = false, more = true;
+    for (uint32_t it = 0; it < 48 && more; ++it) {   // (chains halve per pass: 15 passes cover a tile)
+        bool m = false;
+        for (uint32_t i = t; i < n; i += kTileThreads) {
+            const uint32_t v = tl[i];
+            if ((v & kFlag) || v < T0) continue;   // a literal, or a link out of the tile
+            if (v >= T0 + i) {
+                err = true;
+                tl[i] = kFlag;
+                continue;
+            }
+            const uint32_t w = tl[v - T0];
+            tl[i] = w;
+            m |= !(w & kFlag) && w >= T0;
+        }
+        more = __syncthreads_or(m);
+    }
+    err |= more;
+    bool lit = true;
+    for (uint32_t i = t; i < n; i += kTileThreads) lit &= (tl[i] & kFlag) != 0;
+    const bool all_lit = __syncthreads_and(lit);
+    if (all_lit) {   // the bytes themselves (out is 16-byte aligned)
+        for (uint32_t i = 4 * t; i < n; i += 4 * kTileThreads) {
+            if (i + 4 <= n) {
+                gst<uint32_t>(a.out + T0 + i, (tl[i] & 0xff) | (tl[i + 1] & 0xff) << 8 | (tl[i + 2] & 0xff) << 16 | tl[i + 3] << 24);
+            } else {
+                for (uint32_t k = i; k < n; ++k) a.out[T0 + k] = (uint8_t)tl[k];
+            }
+        }
+    } else {         // 16-bit entries over the tile's own (already read) sources
+        uint16_t *rel = reinterpret_cast<uint16_t *>(src);
+        const uint64_t base = T0 - kTile;   // the previous tile (T0 > 0 here: tile 0 has no links out)
+        auto enc = [&](uint32_t v) -> uint32_t {
+            if (v & kFlag) return 0x8000u | (v & 0xff);
+            if (T0 == 0 || v < base || v >= T0) {
+                err = true;
+                return 0x8000u;
+            }
+            return (uint32_t)(v - base);
+        };
+        for (uint32_t i = 8 * t; i < n; i += 8 * kTileThreads) {
+            if (i + 8 <= n) {
+                gst<uint4>(rel + i, make_uint4(enc(tl[i]) | enc(tl[i + 1]) << 16, enc(tl[i + 2]) | enc(tl[i + 3]) << 16,
+                                               enc(tl[i + 4]) | enc(tl[i + 5]) << 16, enc(tl[i + 6]) | enc(tl[i + 7]) << 16));
+            } else {
+                for (uint32_t k = i; k < n; ++k) rel[k] = (uint16_t)enc(tl[k]);
+            }
+        }
+    }
+    if (t == 0) a.tflag[blockIdx.x] = all_lit ? 1u : 0u;
+    if (__syncthreads_or(err) && t == 0) atomicOr(&st->emit_err, 4u);
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_pinf_scan(PinfArgs a) {
+    __shared__ uint8_t win[2][kTile];
+    const uint64_t N = a.state->total;
+    const uint32_t tiles = (uint32_t)((N + kTile - 1) / kTile), full = (uint32_t)(N / kTile), t = threadIdx.x;
+    // a full tile's loads are issued one tile ahead (the walk is one workgroup: latency is its bound):
+    // entries of a tile with links, or the bytes of a literal tile that the next tile reads
+    uint4 nx[4] = {};
+    auto issue = [&](uint32_t k) {
+        const uint64_t T0 = (uint64_t)k * kTile;
+        if (!a.tflag[k]) {
+            const uint16_t *rel = reinterpret_cast<const uint16_t *>(a.src + T0);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) nx[j] = gld<uint4>(reinterpret_cast<const uint4 *>(rel + 8 * (t + kTileThreads * j)));
+        } else if (k + 1 < tiles && !a.tflag[k + 1]) {
+#pragma unroll
+            for (uint32_t j = 0; j < 2; ++j) nx[j] = gld<uint4>(reinterpret_cast<const uint4 *>(a.out + T0 + 16 * (t + kTileThreads * j)));
+        }
+    };
+    if (full) issue(0);
+    for (uint32_t k = 0; k < tiles; ++k) {
+        const uint64_t T0 = (uint64_t)k * kTile;
+        const uint32_t n = (uint32_t)min<uint64_t>(kTile, N - T0);
+        uint8_t *cur = win[k & 1];
+        const uint8_t *prev = win[(k & 1) ^ 1];
+        auto dec = [&](uint32_t r) -> uint32_t { return r & 0x8000u ? r & 0xff : prev[r & 0x7fff]; };
+        const bool lit = a.tflag[k] != 0;
+        if (k < full) {
+            uint4 v[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) v[j] = nx[j];
+            if (k + 1 < full) issue(k + 1);
+            if (lit) {
+                if (k + 1 < tiles && !a.tflag[k + 1])
+#pragma unroll
+                    for (uint32_t j = 0; j < 2; ++j) *reinterpret_cast<uint4 *>(cur + 16 * (t + kTileThreads * j)) = v[j];
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t i = 8 * (t + kTileThreads * j);
+                    const uint32_t lo = dec(v[j].x & 0xffff) | dec(v[j].x >> 16) << 8 | dec(v[j].y & 0xffff) << 16 | dec(v[j].y >> 16) << 24;
+                    const uint32_t hi = dec(v[j].z & 0xffff) | dec(v[j].z >> 16) << 8 | dec(v[j].w & 0xffff) << 16 | dec(v[j].w >> 16) << 24;
+                    *reinterpret_cast<uint2 *>(cur + i) = make_uint2(lo, hi);
+                    gst<uint64_t>(a.out + T0 + i, (uint64_t)hi << 32 | lo);
+                }
+            }
+        } else if (!lit) {   // the last, partial tile (nothing reads it after)
+            const uint16_t *rel = reinterpret_cast<const uint16_t *>(a.src + T0);
+            for (uint32_t j = t; j < n; j += kTileThreads) a.out[T0 + j] = (uint8_t)dec(rel[j]);
+        }
+        __syncthreads();
+    }
 }
 
 // ---- 6. bytes + checksums -----------------------------------------------------------------------------------
@@ -1152,23 +1363,18 @@ __global__ __launch_bounds__(256) void k_pinf_finish(PinfArgs a) {
     const uint64_t b0 = min(N, s0 + t * sl), b1 = min(N, s0 + (t + 1) * sl);
     uint64_t sa = 0, sw = 0;
     uint32_t c = 0xffffffffu;
-    bool bad = false;
     for (uint64_t o = b0; o < b1; o += 4) {
-        uint32_t word = 0;
         const uint32_t k = (uint32_t)min<uint64_t>(4, b1 - o);
+        uint32_t word = 0;
+        if (k == 4) word = gld<uint32_t>(reinterpret_cast<const uint32_t *>(a.out + o));   // (out: 16-byte aligned)
+        else for (uint32_t i = 0; i < k; ++i) word |= (uint32_t)a.out[o + i] << (8 * i);
         for (uint32_t i = 0; i < k; ++i) {
-            const uint32_t v = a.src[o + i];
-            bad |= !(v & kFlag);
-            const uint32_t by = v & 0xff;
-            word |= by << (8 * i);
+            const uint32_t by = (word >> (8 * i)) & 0xff;
             if (gz) c = crc_tab[(c ^ by) & 0xff] ^ (c >> 8);
             sa += by;
             sw += (b1 - (o + i)) * by;   // weight: bytes of the slice from this one to its end
         }
-        if (k == 4) gst<uint32_t>(a.out + o, word);   // out is 16-byte aligned, o a multiple of 4
-        else for (uint32_t i = 0; i < k; ++i) a.out[o + i] = (uint8_t)(word >> (8 * i));
     }
-    if (__ballot(bad) && (t & 63) == 0) atomicOr(&st->emit_err, 2u);
     // fold to the whole stream: Adler s2 gains (bytes after the slice) x s1; CRC shifts by those bytes
     const uint64_t after = N - b1;
     uint64_t p1 = sa % kAdler, p2 = (sw % kAdler + (after % kAdler) * p1) % kAdler;
@@ -1214,7 +1420,6 @@ __global__ __launch_bounds__(64) void k_pinf_check(PinfArgs a, uint32_t parts) {
     if (t) return;
     const uint64_t N = st->total, tb = st->trailer_byte;
     bool ok = st->emit_err == 0;
-    for (uint32_t r = 0; r < kPinfMaxRounds; ++r) ok = ok && (r + 1 < kPinfMaxRounds || st->unresolved[r] == 0);
     if (a.format == RDX_COMPRESSION_ZLIB) {
         // Adler-32: s1 starts at 1, so s2 gains N more
         const uint32_t A1 = (uint32_t)((1 + s1) % kAdler), A2 = (uint32_t)((s2 + N) % kAdler);
@@ -1248,8 +1453,10 @@ hipError_t launch_pinf_chain(const PinfArgs &a, hipStream_t s) {
 hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total, int cus, hipStream_t s) {
     if (n_chain) hipLaunchKernelGGL(k_pinf_emit, dim3(n_chain), dim3(kLanes), 0, s, a);
     if (a.mcap) hipLaunchKernelGGL(k_pinf_expand, dim3((a.mcap + 3) / 4), dim3(256), 0, s, a);
-    const uint32_t g = (uint32_t)((std::max<uint64_t>(1, (total + 255) / 256) + 7) / 8 * 8);
-    for (uint32_t r = 0; r < kPinfMaxRounds; ++r) hipLaunchKernelGGL(k_pinf_resolve, dim3(g), dim3(256), 0, s, a, r);
+    if (total) {
+        hipLaunchKernelGGL(k_pinf_tile, dim3((uint32_t)((total + kTile - 1) / kTile)), dim3(kTileThreads), 0, s, a);
+        hipLaunchKernelGGL(k_pinf_scan, dim3(1), dim3(kTileThreads), 0, s, a);
+    }
     const uint32_t parts = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kPinfMaxParts, (total + 4095) / 4096));
     hipLaunchKernelGGL(k_pinf_finish, dim3(parts), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pinf_check, dim3(1), dim3(64), 0, s, a, parts);

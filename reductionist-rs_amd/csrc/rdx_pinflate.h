@@ -7,10 +7,9 @@ namespace rdx {
 
 constexpr uint32_t kPinfMaxCand = 4096;   // block-start candidates per stream (more: the stream falls back)
 #ifndef RDX_PINF_LANES
-#define RDX_PINF_LANES 256
+#define RDX_PINF_LANES 1024
 #endif
 constexpr uint32_t kPinfLanes = RDX_PINF_LANES;   // decode lanes per block (k_pinf_block / k_pinf_emit)
-constexpr uint32_t kPinfMaxRounds = 8;    // pointer-jumping launches (each chases up to 16 links per byte)
 constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
 
 enum : uint32_t { kPinfFallback = 0, kPinfOk = 1, kPinfMiss = 2 };
@@ -32,8 +31,8 @@ struct PinfState {
     uint32_t miss_type, emit_err;     // its BTYPE; k_pinf_emit / k_pinf_finish errors
     uint64_t total;                   // output bytes
     uint64_t trailer_byte;            // the checksum trailer (aligned byte position)
-    uint32_t unresolved[kPinfMaxRounds];
     uint32_t final_ok, n_match;       // k_pinf_check's verdict; long-match records of k_pinf_emit
+    uint32_t n_surv, pad;             // offsets k_pinf_find's screen passed to the full header test
 };
 
 struct PinfArgs {
@@ -57,6 +56,7 @@ struct PinfArgs {
     uint64_t *partial;      // [kPinfMaxParts][3] checksum partials
     uint4 *mlist;           // [mcap] long matches (o, len, dist): written by k_pinf_expand
     uint32_t mcap;
+    uint32_t *tflag;        // [ceil(total / 32 KiB)] k_pinf_tile: the tile is literals only
     uint64_t *prof;         // RDX_PINF_PROF: per-workgroup (start, end) of k_pinf_block, then k_pinf_emit; else null
 };
 

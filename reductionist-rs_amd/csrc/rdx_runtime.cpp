@@ -647,8 +647,8 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
     a.lnb = reinterpret_cast<uint32_t *>(ar + oLnb);
     a.lst = reinterpret_cast<uint64_t *>(ar + oLst);
     if (tuning().pinflate_prof) {
-        if ((st = ensure(ws, ws->pprof, 16ull * kPinfMaxCand, s))) return st;
-        RDX_HIP(hipMemsetAsync(ws->pprof.p, 0, 128ull * kPinfMaxCand, s));
+        if ((st = ensure(ws, ws->pprof, 24ull * kPinfMaxCand, s))) return st;
+        RDX_HIP(hipMemsetAsync(ws->pprof.p, 0, 192ull * kPinfMaxCand, s));
         a.prof = ws->pprof.p;
     }
     RDX_HIP(hipMemsetAsync(a.state, 0, sizeof(PinfState), s));
@@ -672,21 +672,27 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
         RDX_HIP(launch_pinf_block(a, n, 1, s));
         RDX_HIP(hipStreamSynchronize(s));   // the host values above are on the stack
     }
-    if (h.status != kPinfOk) return kNotDecoded;
+    if (h.status != kPinfOk) {
+        if (tuning().pinflate_prof)
+            std::fprintf(stderr, "{\"pinf_declined\": {\"chain_status\": %u, \"n_chain\": %u, \"n_cand\": %u, "
+                         "\"overflow\": %u}}\n", h.status, h.n_chain, h.n_cand, h.overflow);
+        return kNotDecoded;
+    }
     const uint64_t total = h.total;
     if ((st = ensure(ws, ws->raw, std::max<uint64_t>((total + 15) / 16 * 16, 16), s))) return st;
-    // the sources, then the long-match records (at most total / 32 of them)
-    const uint64_t mcap = total / 32;
-    if ((st = ensure(ws, ws->psrc, std::max<uint64_t>(total + 4 * mcap + 4, 1), s))) return st;
+    // the sources, the long-match records (at most total / 32 of them), the tiles' flags
+    const uint64_t mcap = total / 32, msta = (total + 3) / 4 * 4, tiles = (total + 32767) / 32768;
+    if ((st = ensure(ws, ws->psrc, std::max<uint64_t>(msta + 4 * mcap + tiles, 1), s))) return st;
     a.src = ws->psrc.p;
-    a.mlist = reinterpret_cast<uint4 *>(ws->psrc.p + (total + 3) / 4 * 4);
+    a.mlist = reinterpret_cast<uint4 *>(ws->psrc.p + msta);
     a.mcap = (uint32_t)mcap;
+    a.tflag = ws->psrc.p + msta + 4 * mcap;
     a.out = ws->raw.p;
     RDX_HIP(launch_pinf_rest(a, h.n_chain, total, ws->cus, s));
     RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
     RDX_HIP(hipStreamSynchronize(s));
     if (a.prof) {   // tuning: the slowest workgroups of k_pinf_block / k_pinf_emit, phase by phase
-        std::vector<uint64_t> pr(16ull * kPinfMaxCand);
+        std::vector<uint64_t> pr(24ull * kPinfMaxCand);
         std::vector<uint64_t> keys(kPinfMaxCand);
         std::vector<PinfBlk> blks(kPinfMaxCand);
         std::vector<uint32_t> chain(kPinfMaxCand);
@@ -722,7 +728,34 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
                          (unsigned long long)(k ? 0 : w[7]));
         }
     }
-    if (!h.final_ok) return kNotDecoded;
+    if (a.prof) {   // k_pinf_find: the slowest workgroup's phases
+        std::vector<uint64_t> pr(8ull * kPinfMaxCand);
+        RDX_HIP(hipMemcpy(pr.data(), a.prof + 16ull * kPinfMaxCand, pr.size() * 8, hipMemcpyDeviceToHost));
+        uint64_t lo = ~0ull, hi = 0, worst = 0, surv = 0;
+        uint32_t wi = 0, n = 0;
+        for (uint32_t i = 0; i < kPinfMaxCand; ++i) {
+            const uint64_t *w = &pr[8ull * i];
+            if (!w[0]) continue;
+            ++n;
+            surv += w[4];
+            lo = std::min(lo, w[0]);
+            hi = std::max(hi, w[3]);
+            if (w[3] - w[0] > worst) { worst = w[3] - w[0]; wi = i; }
+        }
+        const uint64_t *w = &pr[8ull * wi];
+        auto us = [&](uint64_t x) { return x > w[0] ? (x - w[0]) / 100.0 : -1.0; };
+        std::fprintf(stderr, "{\"pinf_prof\": \"find\", \"wgs\": %u, \"span_us\": %.1f, \"max_us\": %.1f, "
+                     "\"survivors\": %llu, \"max_wg\": %u, \"t_staged\": %.1f, \"t_headers\": %.1f, "
+                     "\"wg_survivors\": %llu}\n", n, (hi - lo) / 100.0, worst / 100.0, (unsigned long long)surv, wi,
+                     us(w[1]), us(w[2]), (unsigned long long)w[4]);
+    }
+    if (!h.final_ok) {
+        if (tuning().pinflate_prof)   // tuning / diagnosis: why the parallel path declined
+            std::fprintf(stderr, "{\"pinf_declined\": {\"emit_err\": %u, \"n_chain\": %u, \"total\": %llu, "
+                         "\"n_cand\": %u, \"n_match\": %u}}\n", h.emit_err, h.n_chain, (unsigned long long)total,
+                         h.n_cand, h.n_match);
+        return kNotDecoded;
+    }
     *raw_len = total;
     return RDX_OK;
 }

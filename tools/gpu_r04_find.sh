@@ -15,4 +15,3 @@ PY
 for f in c0 c3; do
   echo "== $f"; timeout -k 10 60 tools/probe_pinf_find /tmp/$f.zlib | tee -a $OUT/find_$f.jsonl || exit 1
 done
-SKIP_TESTS=1 bash tools/gpu_r04_pinf.sh
