@@ -90,6 +90,16 @@ __device__ __forceinline__ void consume_group(Red<T, OP> &r, const T (&x)[N], co
     }
 }
 
+// f64 sums without a missing predicate: groups of a lane's consecutive elements are added pairwise and the
+// group's sum enters the compensated (Neumaier) accumulator once.  Integer-valued data stays exact; the
+// order of additions already differs from the reference's sequential sum (lanes, then a tree), so no new
+// class of deviation: a NaN or an inf anywhere gives the same NaN / inf.
+#ifndef RDX_F64_GROUP_SUM
+#define RDX_F64_GROUP_SUM 1
+#endif
+template <typename T, int OP, int MK>
+constexpr bool kGroupSum = RDX_F64_GROUP_SUM && OP == OP_SUM && std::is_same_v<T, double> && MK == MK_NONE;
+
 // One tile step for one lane: the 16-byte granules this lane owns in tile `t`.
 //   fused   : element granule [e, e+16) with e = t*4096 + lane*16, one 16 B load per plane
 //   plain   : 4 granules of 16 B at byte offsets t*16384 + m*4096 + lane*16
@@ -123,6 +133,26 @@ __device__ __forceinline__ void load_tile(Tile<T, FUSED> &tl, const uint8_t *bas
             const uint64_t o = (uint64_t)m * kBlock * 16 + threadIdx.x * 16;
             if (FULL || o + 16 <= lim) tl.p[m] = gld_stream<uint4>(b + o);
         }
+    }
+}
+
+// UNR full tiles' loads; RDX_PLANE_MAJOR: byte-shuffled 8-byte elements issue plane by plane across the
+// tiles (planes 0-3 of every tile, then 4-7) instead of tile by tile
+#ifndef RDX_PLANE_MAJOR
+#define RDX_PLANE_MAJOR 0
+#endif
+template <typename T, bool FUSED, int UNR>
+__device__ __forceinline__ void load_tiles(Tile<T, FUSED> (&x)[UNR], const uint8_t *base, uint64_t plane,
+                                           const uint64_t (&t0)[UNR], uint64_t vb) {
+    if constexpr (RDX_PLANE_MAJOR && FUSED && sizeof(T) == 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+                x[u].p[k] = gld_stream<uint4>(base + (uint64_t)k * plane + t0[u] + threadIdx.x * 16);
+    } else {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, plane, t0[u], vb);
     }
 }
 
@@ -167,7 +197,14 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
                 T xs[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) xs[m] = from_u<T>((U)(((uint64_t)hi[m] << 32) | lo[m]));
-                consume_group<T, OP, MK, 4>(r, xs, a, e + j * 4);
+                if constexpr (kGroupSum<T, OP, MK>) {
+                    // the 4 elements summed pairwise, then one compensated add (a quarter of the
+                    // per-element Neumaier steps)
+                    Red<T, OP>::neumaier(r.s, r.c, ((double)xs[0] + (double)xs[1]) + ((double)xs[2] + (double)xs[3]));
+                    r.cnt += 4;
+                } else {
+                    consume_group<T, OP, MK, 4>(r, xs, a, e + j * 4);
+                }
             }
         }
     } else {
@@ -201,7 +238,12 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
                 T xs[2];
 #pragma unroll
                 for (int q = 0; q < 2; ++q) xs[q] = from_u<T>((U)(bswap ? bswap_u(w[q]) : w[q]));
-                consume_group<T, OP, MK, 2>(r, xs, a, e);
+                if constexpr (kGroupSum<T, OP, MK>) {
+                    Red<T, OP>::neumaier(r.s, r.c, (double)xs[0] + (double)xs[1]);
+                    r.cnt += 2;
+                } else {
+                    consume_group<T, OP, MK, 2>(r, xs, a, e);
+                }
             }
         }
     }
@@ -281,13 +323,21 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
     if constexpr (kPipelined<T, OP, FUSED>) {
     if (k + UNR <= nk) {
         Tile<T, FUSED> x[UNR], y[UNR];
+        auto tiles_at = [&](uint64_t k0_, uint64_t (&t)[UNR]) {
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + u), vb);
+            for (int u = 0; u < UNR; ++u) t[u] = tile(k0_ + u);
+        };
+        {
+            uint64_t t[UNR];
+            tiles_at(k, t);
+            load_tiles<T, FUSED, UNR>(x, base, a.src.plane, t, vb);
+        }
         while (true) {
             const bool m1 = k + 2 * UNR <= nk;
             if (m1) {
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(y[u], base, a.src.plane, tile(k + UNR + u), vb);
+                uint64_t t[UNR];
+                tiles_at(k + UNR, t);
+                load_tiles<T, FUSED, UNR>(y, base, a.src.plane, t, vb);
             }
 #pragma unroll
             for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
@@ -295,8 +345,9 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
             if (!m1) break;
             const bool m2 = k + 2 * UNR <= nk;
             if (m2) {
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + UNR + u), vb);
+                uint64_t t[UNR];
+                tiles_at(k + UNR, t);
+                load_tiles<T, FUSED, UNR>(x, base, a.src.plane, t, vb);
             }
 #pragma unroll
             for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, y[u], a, tile(k + u), vb, selA, selB);
