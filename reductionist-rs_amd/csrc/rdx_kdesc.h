@@ -192,10 +192,10 @@ struct KCbor {
     uint64_t b_off;             // offset of segment B (after the body)
     uint64_t raw_len;           // bytes of the count_as_bytes payload between D and F (copied by the host)
     uint64_t *out_len;          // device: total encoded length
-    uint64_t *records;          // one tagged granule per tile (look-back)
+    uint64_t *records;          // one word per tile: k_cbor_agg's encoded length, k_cbor_scan's offset
     const uint8_t *body;        // the response body (device), copied in-kernel when copy_body
     uint64_t body_len;
-    uint32_t epoch, n_tiles, vec;
+    uint32_t n_tiles, vec;
     uint32_t copy_body, copy_raw;   // in-kernel copies (alignment permitting), else hipMemcpyAsync
     uint32_t a_len, b_len, d_len, f_len;
     uint8_t fixed[kCborFixedMax];   // A then B

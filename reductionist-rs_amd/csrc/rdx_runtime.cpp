@@ -148,6 +148,7 @@ struct rdx_workspace {
     DevBuf<uint8_t> pinf;
     DevBuf<uint32_t> psrc;
     DevBuf<uint64_t> pprof;
+    DevBuf<uint64_t> cbor_rec;   // k_cbor_agg / k_cbor_scan: per-tile lengths, then offsets
     PinfState *pinf_back = nullptr;
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
@@ -960,6 +961,7 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->pinf.p);
     fr(ws->psrc.p);
     fr(ws->pprof.p);
+    fr(ws->cbor_rec.p);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
     if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
@@ -1013,15 +1015,13 @@ rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const v
     m.copy_raw = L.count_raw && al(d_counts, 16) && al(out + m.c_off + L.d.size(), 4);
     const uint64_t copy_bytes = (m.copy_body ? L.body_len : 0) + (m.copy_raw ? m.raw_len : 0);
     const uint64_t copy_blocks = std::min<uint64_t>((copy_bytes + 65535) / 65536, (uint64_t)ws->cus * 8);
-    // one workgroup per tile (tiles in workgroup order); the copies share the grid.  Resident workgroups
-    // looping over tiles with the next tile prefetched, and a workgroup-wide look-back window, both
-    // measured slower (225 us vs 173 us for 32 Mi counts)
+    // one encoding workgroup per tile; the copies share the grid.  (Resident workgroups looping over the
+    // tiles with the next one prefetched: 142 vs 136 us for 32 Mi counts, profiles/r04_cbor_variants.jsonl)
     const uint32_t blocks = (uint32_t)std::max<uint64_t>({1, tiles, copy_blocks});
     rdx_status st;
     if (m.n_tiles) {
-        if ((st = ensure(ws, ws->partials, m.n_tiles, s, true))) return st;
-        if ((st = next_epoch(ws, s, m.epoch))) return st;
-        m.records = ws->partials.p;
+        if ((st = ensure(ws, ws->cbor_rec, m.n_tiles, s))) return st;   // (not the tagged hand-off records)
+        m.records = ws->cbor_rec.p;
     }
     if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
     if (L.body_len && !m.copy_body)
