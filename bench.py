@@ -931,7 +931,10 @@ def leg_native_concurrent(cx):
                 (independent launches);
       resident: rdx_execute_resident on the context's pool — concurrent small all-axes requests are
                 coalesced by the pool's dispatcher into shared launches (same-plan groups / k_multi), each
-                caller's result written to page-locked host memory by the fold."""
+                caller's result written to page-locked host memory by the fold; an idle entry runs the
+                request on the caller's own thread (the direct fast path, direct_requests);
+      owned:    rdx_execute_owned of a 1 MiB page-locked host chunk (s1: the plugin's own call; host chunks
+                of 1 MiB or less coalesce by default)."""
     exe = ROOT / "reductionist-rs_amd" / "rdx_conc_bench"
     if not exe.exists():
         return {"skipped": f"{exe} not built"}
@@ -942,6 +945,7 @@ def leg_native_concurrent(cx):
                                      ("c1", 1, 2000, "device"), ("c1", pool, 2000, "device"),
                                      ("c1", 1, 2000, "resident"), ("c1", pool, 2000, "resident"),
                                      ("c1", 4 * pool, 1000, "resident"),
+                                     ("s1", 1, 2000, "owned"), ("s1", pool, 2000, "owned"),
                                      ("c2", 1, 300, "device"), ("c2", 4, 300, "device")):
         out.append(conc_bench(cfg, threads, reqs, path))
     return out
