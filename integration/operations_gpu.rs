@@ -43,6 +43,11 @@ pub fn context() -> *mut RdxContext {
     ctx()
 }
 
+/// Whether `init` has created the engine (download_gpu: page-locked download buffers only then).
+pub fn initialized() -> bool {
+    CTX.get().is_some()
+}
+
 /// `Gpu<OP>` — OP: 0 count, 1 max, 2 min, 3 select, 4 sum (rdx_op).
 pub struct Gpu<const OP: u32>;
 pub type GpuCount = Gpu<0>;

@@ -9,15 +9,8 @@
 //! same one copy per body part, and `rdx_execute*` DMAs it to HBM directly (the engine detects pinned
 //! chunks; selects from pinned chunks into pinned results are pipelined).
 //!
-//! In s3_client.rs:221 (and chunk_downloader_http.rs:143), with the GPU engine enabled:
-//!
-//! ```ignore
-//! let mut buf = crate::pinned_gpu::PinnedBuf::with_capacity(content_length)?;
-//! while let Some(bytes) = response.body.try_next().instrument(tracing::Span::current()).await? {
-//!     buf.extend_from_slice(&bytes)?;
-//! }
-//! Ok(buf.into_bytes())
-//! ```
+//! The downloaders fill it through `download_gpu.rs` (the patch to s3_client.rs:215-233 and
+//! chunk_downloader_http.rs:137-146), with the GPU engine enabled;
 //! and `app_gpu::operation_gpu` hands the resulting `Bytes` to the engine as a slice
 //! (`operations_gpu::execute_slice`), never converting it to a `Vec`.
 

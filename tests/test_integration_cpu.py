@@ -183,3 +183,11 @@ def test_pinned_download_path():
     ops = (ROOT / "integration" / "operations_gpu.rs").read_text()
     assert "pub fn execute_slice(rd: &models::RequestData, data: &[u8], op: u32)" in ops
     assert "execute_slice(rd, &data, OP)" in ops            # the Operation trait goes through it too
+    # the downloaders' patch: both bodies into a PinnedBuf, part by part, only with the engine created
+    dl = (ROOT / "integration" / "download_gpu.rs").read_text()
+    code = "\n".join(line for line in dl.splitlines() if not line.strip().startswith("//"))
+    assert "s3_client.rs:215-233" in dl and "chunk_downloader_http.rs:137-146" in dl
+    assert code.count("PinnedBuf::with_capacity(content_length)?") == 2
+    assert code.count("buf.extend_from_slice(&part)?;") == 2 and code.count("Ok(buf.into_bytes())") == 2
+    assert "crate::operations_gpu::initialized()" in code and "pub fn initialized() -> bool" in ops
+    assert ".bytes().await" not in code                     # no whole-body intermediate copy
