@@ -462,17 +462,6 @@ __device__ bool dyn_candidate(const SRC &S, uint64_t p, uint64_t end_bits) {
     return dyn_candidate_rest(S, p, end_bits, h, cb);
 }
 
-// The header test's Kraft sum of the code-length code (the 3-bit fields of cb): 128 = complete.
-__device__ __forceinline__ uint32_t cl_kraft(uint64_t cb) {
-    uint32_t k = 0;
-#pragma unroll
-    for (int i = 0; i < 19; ++i) {
-        const uint32_t l = (uint32_t)(cb >> (3 * i)) & 7;
-        k += l ? 128u >> l : 0u;
-    }
-    return k;
-}
-
 // The code-length code (19 lengths of 3 bits in cb, field i = the i-th symbol of RFC 1951 3.2.7 order) as registers: per-length
 // counts and the symbols packed 5 bits each in (length, symbol) order; then the literal / length and
 // distance code lengths decoded with it, summed into Kraft sums as they come (STORE: also written to
@@ -577,14 +566,88 @@ __device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint
     return pos <= end_bits;
 }
 
+// The finder's whole-header test (the rules of decode_lengths, check only), written for one survivor per
+// lane of a wave: the code-length code as packed registers — per-length region starts S_l and symbol
+// offsets O_l in the space of the 7 peeked bits read MSB first (canonical codes of one length are one
+// contiguous region, lengths in increasing order), the symbols 5 bits each in canonical order — so a
+// symbol is one bit reversal, six compares and two packed lookups; every step is branch-free (one
+// exec mask for the lanes still decoding), where the per-length walk with early returns compiled to
+// ~170 instructions of exec-mask branches per symbol.
 template <class SRC>
 __device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb) {
+    constexpr int kField[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};   // symbol -> field
     const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
+    uint64_t cnt = 0;   // byte l: codes of length l
+#pragma unroll
+    for (int i = 0; i < 19; ++i) cnt += 1ull << (8 * ((cb >> (3 * i)) & 7));
+    int left = 1;
+    uint64_t Sp = 0, Op = 0;   // byte l: S_l, O_l
+    uint32_t st = 0, of = 0;
+#pragma unroll
+    for (int l = 1; l < 8; ++l) {
+        const uint32_t c = (uint32_t)(cnt >> (8 * l)) & 0xff;
+        left = (left << 1) - (int)c;
+        Sp |= (uint64_t)st << (8 * l);
+        Op |= (uint64_t)of << (8 * l);
+        st += c << (7 - l);
+        of += c;
+    }
+    if (left != 0) return false;   // over-subscribed or incomplete (construct() != 0)
+    uint64_t pk0 = 0, pk1 = 0, run = 0;
+#pragma unroll
+    for (int sy = 0; sy < 19; ++sy) {
+        const uint32_t l = (uint32_t)(cb >> (3 * kField[sy])) & 7;
+        const uint32_t r = (uint32_t)((Op + run) >> (8 * l)) & 0xff;   // (bytes <= 38: no carries)
+        run += l ? 1ull << (8 * l) : 0;
+        pk0 |= l && r < 12 ? (uint64_t)sy << (5 * r) : 0;
+        pk1 |= l && r >= 12 ? (uint64_t)sy << (5 * (r - 12)) : 0;
+    }
+    const uint64_t E = Sp >> 16;   // byte l-1: S_{l+1}, the end of length l's region (l = 1..6)
+    const uint32_t total = nl + nd;
     uint64_t pos = p + 17 + 3 * nc;
-    uint32_t kl, kd, used_d;
-    bool eob;
-    if (!decode_lengths<false>(S, pos, end_bits, cb, nl, nd, nullptr, kl, kd, used_d, eob)) return false;
-    return eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
+    uint64_t nxt = pos >> 5;
+    uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
+    uint32_t bc = 64 - (uint32_t)(pos & 31);
+    nxt += 2;
+    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0;
+    bool eob = false, bad = false, live = true;
+    while (__builtin_amdgcn_ballot_w64(live)) {
+        if (live) {
+            const uint32_t w = S.ld(nxt);
+            const bool need = bc < 32;
+            bb |= need ? (uint64_t)w << (bc & 63) : 0;
+            bc += need ? 32 : 0;
+            nxt += need ? 1 : 0;
+            const uint32_t j = __builtin_bitreverse32((uint32_t)bb) >> 25;
+            uint32_t len = 1;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) len += ((uint32_t)(E >> (8 * l)) & 0xff) <= j ? 1u : 0u;
+            const uint32_t Sl = (uint32_t)(Sp >> (8 * len)) & 0xff, Ol = (uint32_t)(Op >> (8 * len)) & 0xff;
+            const uint32_t si = Ol + ((j - Sl) >> (7 - len));
+            const uint32_t sym = (uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31;
+            const uint32_t x = (uint32_t)(bb >> len);
+            const bool s16 = sym == 16, s17 = sym == 17, s18 = sym == 18;
+            const uint32_t rep = s16 ? 3 + (x & 3) : s17 ? 3 + (x & 7) : s18 ? 11 + (x & 127) : 1;
+            const uint32_t used = len + (s16 ? 2 : s17 ? 3 : s18 ? 7 : 0);
+            const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
+            bad |= (s16 && idx == 0) || idx + rep > total;
+            const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
+            eob |= idx <= 256 && 256 < idx + nlit && val != 0;
+            const uint32_t sh = 15 - val;
+            kl += val ? nlit << sh : 0u;
+            kd += val ? ndst << sh : 0u;
+            used_d += val ? ndst : 0u;
+            bad |= kl > (1u << 15) || kd > (1u << 15);
+            pos += used;
+            bb >>= used;
+            bc -= used;
+            idx += rep;
+            prev = val;
+            bad |= pos > end_bits;
+            live = !bad && idx < total;
+        }
+    }
+    return !bad && eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
 }
 
 // ---- 1. candidates ------------------------------------------------------------------------------------
@@ -615,6 +678,7 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     __shared__ uint32_t win[kFindWin];
     __shared__ uint32_t list[kFindList];   // survivors: bit offsets from 8 * q0
     __shared__ uint32_t n_list;
+    __shared__ uint16_t kraft4[4096];      // Kraft sum (x128) of four 3-bit code-length fields
     const uint32_t t = threadIdx.x, lane = t & 63;
     // RDX_PINF_PROF: (start, staged, last header pass, end, survivors) per workgroup, after k_pinf_emit's
     uint64_t *const prof = a.prof && blockIdx.x < kPinfMaxCand ? a.prof + 16ull * kPinfMaxCand + 8ull * blockIdx.x : nullptr;
@@ -623,6 +687,15 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     const uint64_t q0 = a.first_byte + (uint64_t)blockIdx.x * kFindBytes;
     const uint64_t l0 = q0 >= 4 ? (q0 >> 2) - 1 : 0;
     for (uint32_t k = t; k < kFindWin; k += 256) win[k] = G.ldg(l0 + k);
+    for (uint32_t e = t; e < 4096; e += 256) {
+        uint32_t k = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t l = (e >> (3 * i)) & 7;
+            k += l ? 128u >> l : 0u;
+        }
+        kraft4[e] = (uint16_t)k;
+    }
     if (t == 0) n_list = 0;
     __syncthreads();
     WinStream S;
@@ -657,7 +730,9 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
             const uint32_t h = (uint32_t)(w64 >> b);
             const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
                                 ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
-            mask |= cl_kraft(cb) == 128 ? 1u << b : 0u;
+            const uint32_t kr = kraft4[cb & 0xfff] + kraft4[(cb >> 12) & 0xfff] + kraft4[(cb >> 24) & 0xfff] +
+                                kraft4[(cb >> 36) & 0xfff] + kraft4[(cb >> 48) & 0xfff];
+            mask |= kr == 128 ? 1u << b : 0u;
         }
         // append: one LDS atomic per wave
         const uint32_t cnt = __builtin_popcount(mask);
