@@ -413,41 +413,6 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
     return r;
 }
 
-template <bool STORE, class SRC>
-__device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint64_t end_bits, uint64_t cb, uint32_t nl,
-                                               uint32_t nd, uint8_t *lens, uint32_t &kl, uint32_t &kd, uint32_t &used_d,
-                                               bool &eob);
-
-// Parse a block header at bit `p` (its BFINAL bit) the way oracle_inflate does; thread 0 only.  type 1:
-// fixed lengths, 2: dynamic (code lengths into T.lens).  Returns false on any error; *body = first bit of
-// the body, *nlen / *ndist the code counts.
-__device__ bool parse_header(const Stream &S, uint64_t p, uint32_t type, uint64_t end_bits, Tabs &T, uint64_t *body,
-                             uint32_t *nlen, uint32_t *ndist) {
-    uint64_t pos = p + 3;
-    if (type == 1) {
-        for (uint32_t s = 0; s < 288; ++s) T.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-        for (uint32_t s = 0; s < 30; ++s) T.lens[288 + s] = 5;
-        *nlen = 288;
-        *ndist = 30;
-        *body = pos;
-        return pos <= end_bits;
-    }
-    const uint32_t h = S.at(pos);
-    const uint32_t nl = (h & 31) + 257, nd = ((h >> 5) & 31) + 1, nc = ((h >> 10) & 15) + 4;
-    pos += 14;
-    if (nl > 286 || nd > 30) return false;
-    const uint64_t cb = ((uint64_t)S.at(pos) | (uint64_t)S.at(pos + 32) << 32) & ((1ull << (3 * nc)) - 1);
-    pos += 3 * nc;
-    uint32_t kl, kd, used_d;
-    bool eob;
-    // (the codes' completeness is judged by build(), as construct() does in the oracle)
-    if (!decode_lengths<true>(S, pos, end_bits, cb, nl, nd, T.lens, kl, kd, used_d, eob) || !eob) return false;
-    *nlen = nl;
-    *ndist = nd;
-    *body = pos;
-    return true;
-}
-
 // The finder's strict dynamic-header test at bit p (a zlib encoder's header: complete codes), in
 // registers only (one thread per bit offset; no per-lane arrays, so no scratch): the code-length code as
 // per-length counts and its symbols packed 5 bits each in (len, symbol) order; the literal / length and
@@ -462,121 +427,21 @@ __device__ bool dyn_candidate(const SRC &S, uint64_t p, uint64_t end_bits) {
     return dyn_candidate_rest(S, p, end_bits, h, cb);
 }
 
-// The code-length code (19 lengths of 3 bits in cb, field i = the i-th symbol of RFC 1951 3.2.7 order) as registers: per-length
-// counts and the symbols packed 5 bits each in (length, symbol) order; then the literal / length and
-// distance code lengths decoded with it, summed into Kraft sums as they come (STORE: also written to
-// lens[]).  The rules are oracle_inflate's: a complete code-length code, no repeat (16) first, no run past
-// HLIT + HDIST.  Returns false on the first violation or an over-subscribed literal / distance code.
-template <bool STORE, class SRC>
-__device__ __forceinline__ bool decode_lengths(const SRC &S, uint64_t &pos, uint64_t end_bits, uint64_t cb, uint32_t nl,
-                                               uint32_t nd, uint8_t *lens, uint32_t &kl, uint32_t &kd, uint32_t &used_d,
-                                               bool &eob) {
-    uint32_t cnt[8];
-#pragma unroll
-    for (int l = 0; l < 8; ++l) cnt[l] = 0;
-#pragma unroll
-    for (int i = 0; i < 19; ++i) {
-        const uint32_t l = (uint32_t)(cb >> (3 * i)) & 7;
-#pragma unroll
-        for (int q = 1; q < 8; ++q) cnt[q] += l == (uint32_t)q ? 1u : 0u;
-    }
-    int left = 1;
-#pragma unroll
-    for (int l = 1; l < 8; ++l) left = (left << 1) - (int)cnt[l];
-    if (left != 0) return false;   // over-subscribed or incomplete (construct() != 0)
-    constexpr int kInv[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
-    uint64_t pk0 = 0, pk1 = 0;
-    uint32_t k = 0;
-#pragma unroll
-    for (int l = 1; l < 8; ++l) {
-#pragma unroll
-        for (int sy = 0; sy < 19; ++sy) {
-            const bool hit = ((uint32_t)(cb >> (3 * kInv[sy])) & 7) == (uint32_t)l;
-            const uint64_t v = hit ? (uint64_t)sy : 0;
-            pk0 |= k < 12 ? v << (5 * k) : 0;
-            pk1 |= k >= 12 ? v << (5 * (k - 12)) : 0;
-            k += hit ? 1 : 0;
-        }
-    }
-    const uint32_t total = nl + nd;
-    uint32_t idx = 0, prev = 0;
-    kl = kd = used_d = 0;
-    eob = false;
-    // the bits through a 64-bit buffer refilled a dword at a time (one LDS read per two or three symbols)
-    uint64_t nxt = pos >> 5;
-    uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
-    uint32_t bc = 64 - (uint32_t)(pos & 31);
-    nxt += 2;
-    while (idx < total) {
-        if (pos > end_bits) return false;
-        if (bc < 32) {
-            bb |= (uint64_t)S.ld(nxt++) << bc;
-            bc += 32;
-        }
-        const uint32_t w = (uint32_t)bb;
-        // canonical walk over lengths 1..7 (predicated; a complete code always decodes)
-        int code = 0, first = 0, index = 0, si = -1, len = 0;
-#pragma unroll
-        for (int l = 1; l < 8; ++l) {
-            code |= (int)((w >> (l - 1)) & 1);
-            const int c = (int)cnt[l];
-            if (si < 0 && code - c < first) {
-                si = index + (code - first);
-                len = l;
-            }
-            index += c;
-            first = (first + c) << 1;
-            code <<= 1;
-        }
-        if (si < 0) return false;
-        const uint32_t sym = (uint32_t)((si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31);
-        const uint32_t x = w >> len;
-        uint32_t rep = 1, val = sym, used = (uint32_t)len;
-        if (sym == 16) {
-            if (idx == 0) return false;
-            val = prev;
-            rep = 3 + (x & 3);
-            used += 2;
-        } else if (sym == 17) {
-            val = 0;
-            rep = 3 + (x & 7);
-            used += 3;
-        } else if (sym == 18) {
-            val = 0;
-            rep = 11 + (x & 127);
-            used += 7;
-        }
-        pos += used;
-        bb >>= used;
-        bc -= used;
-        if (idx + rep > total) return false;
-        if (STORE)
-            for (uint32_t r = 0; r < rep; ++r) lens[idx + r] = (uint8_t)val;
-        const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
-        if (idx <= 256 && 256 < idx + nlit) eob = val != 0;
-        if (val) {
-            kl += nlit << (15 - val);
-            kd += ndst << (15 - val);
-            used_d += ndst;
-            if (kl > (1u << 15) || kd > (1u << 15)) return false;
-        }
-        prev = val;
-        idx += rep;
-    }
-    return pos <= end_bits;
-}
-
-// The finder's whole-header test (the rules of decode_lengths, check only), written for one survivor per
-// lane of a wave: the code-length code as packed registers — per-length region starts S_l and symbol
+// A dynamic header's code lengths (STORE: into lens[]) with oracle_inflate's rules — a complete
+// code-length code, no repeat (16) first, no run past HLIT + HDIST, no over-subscribed literal / length or
+// distance code — and their Kraft sums (kl, kd: x 2^15), the distance codes used, whether the end-of-block
+// code has a length.  Written for one header per lane of a wave (the finder's survivors; thread 0 of
+// k_pinf_block's parse): the code-length code as packed registers — per-length region starts S_l and symbol
 // offsets O_l in the space of the 7 peeked bits read MSB first (canonical codes of one length are one
 // contiguous region, lengths in increasing order), the symbols 5 bits each in canonical order — so a
 // symbol is one bit reversal, six compares and two packed lookups; every step is branch-free (one
 // exec mask for the lanes still decoding), where the per-length walk with early returns compiled to
 // ~170 instructions of exec-mask branches per symbol.
-template <class SRC>
-__device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb) {
+template <bool STORE, class SRC>
+__device__ __forceinline__ bool header_lengths(const SRC &S, uint64_t &pos, uint64_t end_bits, uint64_t cb, uint32_t nl,
+                                               uint32_t nd, uint8_t *lens, uint32_t &kl, uint32_t &kd, uint32_t &used_d,
+                                               bool &eob) {
     constexpr int kField[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};   // symbol -> field
-    const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
     uint64_t cnt = 0;   // byte l: codes of length l
 #pragma unroll
     for (int i = 0; i < 19; ++i) cnt += 1ull << (8 * ((cb >> (3 * i)) & 7));
@@ -604,20 +469,22 @@ __device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, 
     }
     const uint64_t E = Sp >> 16;   // byte l-1: S_{l+1}, the end of length l's region (l = 1..6)
     const uint32_t total = nl + nd;
-    uint64_t pos = p + 17 + 3 * nc;
     uint64_t nxt = pos >> 5;
     uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
     uint32_t bc = 64 - (uint32_t)(pos & 31);
     nxt += 2;
-    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0;
-    bool eob = false, bad = false, live = true;
+    uint32_t idx = 0, prev = 0;
+    kl = kd = used_d = 0;
+    eob = false;
+    bool bad = false, live = true;
+    uint32_t w = S.ld(nxt);   // the next dword, loaded one refill ahead (off the symbol's dependency chain)
     while (__builtin_amdgcn_ballot_w64(live)) {
         if (live) {
-            const uint32_t w = S.ld(nxt);
             const bool need = bc < 32;
             bb |= need ? (uint64_t)w << (bc & 63) : 0;
             bc += need ? 32 : 0;
             nxt += need ? 1 : 0;
+            if (need) w = S.ld(nxt);
             const uint32_t j = __builtin_bitreverse32((uint32_t)bb) >> 25;
             uint32_t len = 1;
 #pragma unroll
@@ -631,6 +498,8 @@ __device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, 
             const uint32_t used = len + (s16 ? 2 : s17 ? 3 : s18 ? 7 : 0);
             const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
             bad |= (s16 && idx == 0) || idx + rep > total;
+            if (STORE && !bad && val)   // (lens[] is zeroed by the caller: runs of zeros write nothing)
+                for (uint32_t r = 0; r < rep; ++r) lens[idx + r] = (uint8_t)val;
             const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
             eob |= idx <= 256 && 256 < idx + nlit && val != 0;
             const uint32_t sh = 15 - val;
@@ -647,7 +516,141 @@ __device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, 
             live = !bad && idx < total;
         }
     }
-    return !bad && eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
+    return !bad;
+}
+
+// The same for k_pinf_block's parse, by the 64 lanes of one wave together (the wave is alone on the block's
+// critical path: one lane decoding ~300 symbols took 70-90 us, every step waiting on the previous one's
+// latency).  Lane k decodes the symbol that would start at bit base + k (all 64 candidates at once); the
+// chain of actual symbols is then followed with uniform lane reads (scalar work, ~14 symbols per 64-bit
+// window), and a nonzero run is stored by its lanes in parallel.  Same rules and results as
+// header_lengths<true>; every lane returns the same values.
+__device__ bool header_lengths_wave(const Stream &S, uint64_t &pos_io, uint64_t end_bits, uint64_t cb, uint32_t nl,
+                                    uint32_t nd, uint8_t *lens, uint32_t &kl_o, uint32_t &kd_o, uint32_t &used_d_o,
+                                    bool &eob_o) {
+    constexpr int kField[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 19; ++i) cnt += 1ull << (8 * ((cb >> (3 * i)) & 7));
+    int left = 1;
+    uint64_t Sp = 0, Op = 0;
+    uint32_t st = 0, of = 0;
+#pragma unroll
+    for (int l = 1; l < 8; ++l) {
+        const uint32_t c = (uint32_t)(cnt >> (8 * l)) & 0xff;
+        left = (left << 1) - (int)c;
+        Sp |= (uint64_t)st << (8 * l);
+        Op |= (uint64_t)of << (8 * l);
+        st += c << (7 - l);
+        of += c;
+    }
+    if (left != 0) return false;
+    uint64_t pk0 = 0, pk1 = 0, run = 0;
+#pragma unroll
+    for (int sy = 0; sy < 19; ++sy) {
+        const uint32_t l = (uint32_t)(cb >> (3 * kField[sy])) & 7;
+        const uint32_t r = (uint32_t)((Op + run) >> (8 * l)) & 0xff;
+        run += l ? 1ull << (8 * l) : 0;
+        pk0 |= l && r < 12 ? (uint64_t)sy << (5 * r) : 0;
+        pk1 |= l && r >= 12 ? (uint64_t)sy << (5 * (r - 12)) : 0;
+    }
+    const uint64_t E = Sp >> 16;
+    const uint32_t total = nl + nd;
+    uint64_t base = pos_io, pos = pos_io;
+    uint32_t off = 64;   // (forces the first window)
+    uint32_t symv = 0, usedv = 0, repv = 0;
+    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0;
+    bool eob = false, bad = false;
+    while (!bad && idx < total) {
+        if (off >= 64) {   // this window: lane k decodes the symbol at bit base + k
+            base = pos;
+            off = 0;
+            const uint32_t v = S.at(base + lane);
+            const uint32_t j = __builtin_bitreverse32(v) >> 25;
+            uint32_t len = 1;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) len += ((uint32_t)(E >> (8 * l)) & 0xff) <= j ? 1u : 0u;
+            const uint32_t Sl = (uint32_t)(Sp >> (8 * len)) & 0xff, Ol = (uint32_t)(Op >> (8 * len)) & 0xff;
+            const uint32_t si = Ol + ((j - Sl) >> (7 - len));
+            symv = (uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31;
+            const uint32_t x = v >> len;
+            repv = symv == 16 ? 3 + (x & 3) : symv == 17 ? 3 + (x & 7) : symv == 18 ? 11 + (x & 127) : 1;
+            usedv = len + (symv == 16 ? 2 : symv == 17 ? 3 : symv == 18 ? 7 : 0);
+        }
+        const uint32_t sym = (uint32_t)__builtin_amdgcn_readlane((int)symv, (int)off);
+        const uint32_t rep = (uint32_t)__builtin_amdgcn_readlane((int)repv, (int)off);
+        const uint32_t used = (uint32_t)__builtin_amdgcn_readlane((int)usedv, (int)off);
+        const uint32_t val = sym == 16 ? prev : sym >= 17 ? 0 : sym;
+        if ((sym == 16 && idx == 0) || idx + rep > total) {
+            bad = true;
+            break;
+        }
+        if (val && lane < rep) lens[idx + lane] = (uint8_t)val;   // (zeroed by the caller)
+        const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
+        if (idx <= 256 && 256 < idx + nlit) eob = val != 0;
+        if (val) {
+            kl += nlit << (15 - val);
+            kd += ndst << (15 - val);
+            used_d += ndst;
+            if (kl > (1u << 15) || kd > (1u << 15)) {
+                bad = true;
+                break;
+            }
+        }
+        pos += used;
+        off += used;
+        idx += rep;
+        prev = val;
+        if (pos > end_bits) bad = true;
+    }
+    pos_io = pos;
+    kl_o = kl;
+    kd_o = kd;
+    used_d_o = used_d;
+    eob_o = eob;
+    return !bad;
+}
+
+// A block header at bit p (its BFINAL bit) parsed the way oracle_inflate does, by the 64 lanes of wave 0
+// (k_pinf_block).  type 1: fixed lengths, 2: dynamic (code lengths into T.lens).  Returns false on any
+// error; *body = first bit of the body, *nlen / *ndist the code counts; the same results in every lane.
+__device__ bool parse_header_wave(const Stream &S, uint64_t p, uint32_t type, uint64_t end_bits, Tabs &T, uint64_t *body,
+                                  uint32_t *nlen, uint32_t *ndist) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t pos = p + 3;
+    if (type == 1) {
+        for (uint32_t s = lane; s < 320; s += 64) T.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : s < 318 ? 5 : 0;
+        *nlen = 288;
+        *ndist = 30;
+        *body = pos;
+        return pos <= end_bits;
+    }
+    const uint32_t h = S.at(pos);
+    const uint32_t nl = (h & 31) + 257, nd = ((h >> 5) & 31) + 1, nc = ((h >> 10) & 15) + 4;
+    pos += 14;
+    if (nl > 286 || nd > 30) return false;
+    for (uint32_t i = lane; i < 320; i += 64) T.lens[i] = 0;
+    const uint64_t cb = ((uint64_t)S.at(pos) | (uint64_t)S.at(pos + 32) << 32) & ((1ull << (3 * nc)) - 1);
+    pos += 3 * nc;
+    uint32_t kl, kd, used_d;
+    bool eob;
+    // (the codes' completeness is judged by build(), as construct() does in the oracle)
+    if (!header_lengths_wave(S, pos, end_bits, cb, nl, nd, T.lens, kl, kd, used_d, eob) || !eob) return false;
+    *nlen = nl;
+    *ndist = nd;
+    *body = pos;
+    return true;
+}
+
+template <class SRC>
+__device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb) {
+    const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
+    uint64_t pos = p + 17 + 3 * nc;
+    uint32_t kl, kd, used_d;
+    bool eob;
+    if (!header_lengths<false>(S, pos, end_bits, cb, nl, nd, nullptr, kl, kd, used_d, eob)) return false;
+    return eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
 }
 
 // ---- 1. candidates ------------------------------------------------------------------------------------
@@ -831,6 +834,7 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
     static_assert(kLanes % 64 == 0 && kLanes <= 1024, "lanes per block");
     __shared__ uint32_t s_nb[kLanes];
     __shared__ uint8_t s_ed[kLanes];
+    __shared__ uint32_t s_wm[kLanes / 64];
     __shared__ uint64_t s_body;
     __shared__ uint32_t s_ok, s_nlen, s_ndist, s_first;
     __shared__ uint32_t win[kWinDwords];
@@ -858,15 +862,19 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
     }
     // the header and (where it fits) the body from LDS: the window starts at the header's dword
     S.stage(win, kWinDwords, bit >> 5, a.nw);
-    if (t == 0) {
+    if (t < 64) {
         uint64_t body = 0;
         uint32_t nl = 0, nd = 0;
-        s_ok = parse_header(S, bit, type, a.end_bits, T, &body, &nl, &nd) ? 1 : 0;
-        s_body = body;
-        s_nlen = nl;
-        s_ndist = nd;
+        const bool ok = parse_header_wave(S, bit, type, a.end_bits, T, &body, &nl, &nd);
+        if (t == 0) {
+            s_ok = ok ? 1 : 0;
+            s_body = body;
+            s_nlen = nl;
+            s_ndist = nd;
+        }
     }
     __syncthreads();
+    PINF_STAMP(6, wall_clock64());   // staged and parsed
     const bool hdr_ok = s_ok != 0;
     const bool tabs_ok = hdr_ok && build_tabs(T, s_nlen, s_ndist);
     if (!tabs_ok) {
@@ -898,22 +906,32 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
         __syncthreads();
         PINF_STAMP(2, wall_clock64());
         for (;;) {
-            // resync rounds: lane k re-decodes from lane k-1's exit when its start differs
+            // resync rounds: lane k re-decodes from lane k-1's exit when its start differs.  Lanes up to
+            // the first break of the chain from lane 0 are verified; the rounds end once a verified lane
+            // has ended the block (lanes past it decode bits after the block and do not matter) or every
+            // lane is verified
             bool done = false;
             for (uint32_t round = 0; round < kRounds; ++round) {
+                const bool brk = t >= 1 && t < L && (s_ed[t - 1] != 0 || s_st[t] != s_x[t - 1]);
+                const uint64_t bw = __ballot(brk);
+                if ((t & 63) == 0) s_wm[t >> 6] = bw ? (t & ~63u) + (uint32_t)__builtin_ctzll(bw) : L;
+                __syncthreads();
+                uint32_t m = L;
+                for (uint32_t w = 0; w < kLanes / 64; ++w) m = s_wm[w] < m ? s_wm[w] : m;
+                if (m >= L || s_ed[m - 1] != 0) {
+                    done = true;
+                    break;
+                }
                 uint64_t px = 0;
                 bool redo = false;
-                if (t >= 1 && t < L) {
+                if (t >= m && t < L) {
                     px = s_x[t - 1];
                     redo = s_ed[t - 1] == 0 && s_st[t] != px;
                 }
                 __syncthreads();
                 if (redo) run(t, px);
                 ++rounds;
-                if (!__syncthreads_or(redo)) {
-                    done = true;
-                    break;
-                }
+                __syncthreads();
             }
             if (done) break;
             // the data keeps the parses apart: the first mismatched lane walks on sequentially
@@ -937,15 +955,16 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
         __syncthreads();
         const uint32_t j = s_first;
         PINF_STAMP(3, wall_clock64());
-        if (j == L) {   // no end of block before E: extend the body to the next candidate
+        if (j == L) {   // no end of block before E (a false candidate inside the body): extend the body
+            // to the next candidate, and at least to a whole pass of lanes (the lanes' time does not grow
+            // with the span up to kLanes x kMinLaneBits; each extension costs a pass)
             if (E >= a.end_bits) break;
-            E = next_cand(a, n, E, s_red);
+            E = max(next_cand(a, n, E, s_red), min(body + (uint64_t)kLanes * kMinLaneBits, a.end_bits));
             ++exts;
             continue;
         }
         PINF_STAMP(5, rounds);
-        PINF_STAMP(6, walks);
-        PINF_STAMP(7, exts);
+        PINF_STAMP(7, exts | walks << 32);
         if (t == 0) {
             uint64_t bytes = 0;
             for (uint32_t k = 0; k <= j; ++k) bytes += s_nb[k];

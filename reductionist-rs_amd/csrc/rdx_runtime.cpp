@@ -721,12 +721,12 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
             std::fprintf(stderr, "{\"pinf_prof\": \"%s\", \"wgs\": %zu, \"span_us\": %.1f, \"median_us\": %.1f, "
                          "\"max_us\": %.1f, \"max_cand\": %u, \"type\": %u, \"bytes\": %llu, \"bits\": %llu, "
                          "\"lanes\": %u, \"status\": %u, \"t_tables\": %.1f, \"t_pass0\": %.1f, \"t_agree\": %.1f, "
-                         "\"rounds\": %llu, \"walks\": %llu, \"exts\": %llu}\n", k ? "emit" : "block", d.size(),
+                         "\"rounds\": %llu, \"t_parsed\": %.1f, \"exts\": %llu, \"walks\": %llu}\n", k ? "emit" : "block", d.size(),
                          (hi - lo) / 100.0, d.empty() ? 0.0 : d[d.size() / 2] / 100.0, worst / 100.0, c,
                          (unsigned)(keys[c] & 3), (unsigned long long)blks[c].bytes,
                          (unsigned long long)(blks[c].end - (keys[c] >> 2)), blks[c].nlanes, blks[c].status, us(w[1]),
-                         us(w[2]), us(w[3]), (unsigned long long)(k ? 0 : w[5]), (unsigned long long)(k ? 0 : w[6]),
-                         (unsigned long long)(k ? 0 : w[7]));
+                         us(w[2]), us(w[3]), (unsigned long long)(k ? 0 : w[5]), k ? -1.0 : us(w[6]),
+                         (unsigned long long)(k ? 0 : w[7] & 0xffffffffu), (unsigned long long)(k ? 0 : w[7] >> 32));
         }
     }
     if (a.prof) {   // k_pinf_find: the slowest workgroup's phases
