@@ -24,6 +24,7 @@ CASES = {
     "k_axis_rows": ("axis1_rows", 64 << 20, 4096 * 4 + 4096 * 8),
     "k_multi": ("mixed_multi", 10 * ((4 << 20) + C3_NSEL * 8), 0),
     "k_cbor": ("cbor_counts", 8 * (512 * 256 * 256), 512 * 256 * 256),
+    "k_cbor_agg": ("cbor_agg", 8 * (512 * 256 * 256), 0),   # (round 4: the tile lengths' pass re-reads the counts)
 }
 
 
