@@ -52,6 +52,10 @@ constexpr uint64_t kMinLaneBits = RDX_PINF_MINBITS;   // a lane's share of a blo
 constexpr uint32_t kRoot = 11, kDRoot = 9; // LDS root tables: literal/length, distance
 constexpr uint32_t kFlag = 0x80000000u;    // a source that is a literal byte
 constexpr uint32_t kRounds = 6;            // resync rounds before a sequential walk
+#ifndef RDX_PINF_WARMBITS
+#define RDX_PINF_WARMBITS 128
+#endif
+constexpr uint64_t kWarmBits = RDX_PINF_WARMBITS;   // bits a lane decodes before its range in pass 0
 constexpr uint64_t kMaxSpan = 1ull << 21;  // bits a candidate may decode (a zlib block is < 1.6 M bits)
 constexpr uint32_t kWinDwords = 8192;      // LDS window of the stream per block workgroup (32 KiB)
 
@@ -902,7 +906,19 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
             s_nb[k] = (uint32_t)nb;
             s_ed[k] = (uint8_t)r;
         };
-        if (t < L) run(t, lo(t));
+        // pass 0: lane k > 0 first decodes kWarmBits before its range and starts at its first symbol
+        // boundary at or past lo(k) — by then its parse has almost always resynchronised with the true one,
+        // so few lanes need resync rounds (each round costs a whole pass)
+        if (t < L) {
+            uint64_t from = lo(t);
+            if (t > 0 && from - body > kWarmBits) {
+                Bits br;
+                br.seek(S, from - kWarmBits);
+                uint64_t x, nb;
+                if (run_lane<false>(T, S, br, from, a.end_bits, &x, &nb, nullptr, 0) == 0) from = x;
+            }
+            run(t, from);
+        }
         __syncthreads();
         PINF_STAMP(2, wall_clock64());
         for (;;) {
