@@ -28,6 +28,7 @@
 #include "../../include/rdx.h"
 #include "rdx_cbor.hpp"
 #include "rdx_kernels.hpp"
+#include "rdx_jobsync.hpp"
 #include "rdx_pinflate.h"
 #include "rdx_plan.hpp"
 
@@ -196,13 +197,11 @@ struct Job {
     void *h_body = nullptr;        // host destinations
     int64_t *h_counts = nullptr;
     rdx_status st = RDX_OK;
-    // futex word: kJobPending -> (the caller gives up spinning) kJobSleeping -> kJobDone.  Whoever completes
-    // the job writes `st` and the outputs, then exchanges kJobDone in; after that exchange it touches no
-    // field of the Job (the caller may already have returned and its stack frame be reused): a wake-up
-    // passes only the word's address to the kernel.
-    std::atomic<uint32_t> state{0};
+    // futex word (rdx_jobsync.hpp): whoever completes the job writes `st` and the outputs, then exchanges
+    // kJobDone in; after that exchange it touches no field of the Job (the caller may already have returned
+    // and its stack frame be reused): a wake-up passes only the word's address to the kernel.
+    std::atomic<uint32_t> state{kJobPending};
 };
-constexpr uint32_t kJobPending = 0, kJobSleeping = 1, kJobDone = 2;
 
 // One entry of the context's device pool.
 struct PoolEntry {
@@ -1748,32 +1747,15 @@ rdx_status launch_lane(Lane &L) {
     return RDX_OK;
 }
 
-// Completion: the result is in the caller's buffers; release it, and wake it only if it is asleep.  One
-// atomic word: the exchange both publishes the result and tells whether the caller went to sleep, and it
-// is the last access to the Job (the futex wake-up names the address; it reads no memory there).
+// Completion: the result is in the caller's buffers; release it, and wake it only if it is asleep
+// (rdx_jobsync.hpp: the exchange is the last access to the Job).
 void finish_job(Job &j, rdx_status st) {
     j.st = st;
-    uint32_t *const word = reinterpret_cast<uint32_t *>(&j.state);
-    if (j.state.exchange(kJobDone, std::memory_order_acq_rel) == kJobSleeping)
-        syscall(SYS_futex, word, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    job_finish(j.state);
 }
 
-// The caller's wait: spin (no system call: a result arrives within tens of microseconds of its launch),
-// then announce the sleep with a CAS pending -> sleeping and sleep on the futex (RDX_WAIT_SPIN iterations
-// of the spin; 0 = sleep at once).  A failed CAS means the job is done.
-void wait_job(Job &j) {
-    const int spin = tuning().wait_spin;
-    for (int i = 0; i < spin; ++i) {
-        if (j.state.load(std::memory_order_acquire) == kJobDone) return;
-        __builtin_ia32_pause();
-    }
-    uint32_t expect = kJobPending;
-    if (!j.state.compare_exchange_strong(expect, kJobSleeping, std::memory_order_acq_rel)) return;
-    while (j.state.load(std::memory_order_acquire) != kJobDone) {
-        const timespec ts{0, 1000000};   // re-check every millisecond whatever happens
-        syscall(SYS_futex, reinterpret_cast<uint32_t *>(&j.state), FUTEX_WAIT_PRIVATE, kJobSleeping, &ts, nullptr, 0);
-    }
-}
+// The caller's wait: spin RDX_WAIT_SPIN pause iterations (0 = sleep at once), then sleep on the futex.
+void wait_job(Job &j) { job_wait(j.state, tuning().wait_spin); }
 
 // Poll a launched lane's slots: every request whose three granules carry the launch's tag is decoded into
 // its caller's buffers and released.  `kernel_done`: the launch has ended (its event), so a slot still
