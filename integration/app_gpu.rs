@@ -39,15 +39,15 @@ pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
     data: Bytes,
 ) -> Result<models::Response, ActiveStorageError> {
     // gzip / zlib: a lone request's DEFLATE stream is decoded by the whole device (k_pinflate, DESIGN.md
-    // §9.2: candidate block starts, blocks and the symbols inside them decoded in parallel, then the copies
-    // resolved) — faster than the reference's host decoder on one core for the chunks scientific data
-    // gives (profiles/r04_pinflate_probe.jsonl).  A stream whose request states it expands more than
-    // 16-fold (long matches, few blocks: the parallel decode has little to split) keeps the host path, as
-    // does any request when REDUCTIONIST_GPU_INFLATE=0.
+    // §9.1: candidate block starts, blocks and the symbols inside them decoded in parallel, then the copies
+    // resolved): a 4 MiB zlib-1 chunk in 0.71 ms against 3.6 ms for zlib on one host core, integer-valued
+    // chunks 0.9 ms against 6-10 ms (profiles/r04_pinflate_probe.jsonl, r04_bench.json).  A stream whose
+    // request states it expands more than 16-fold (long matches, few blocks: 7.8 ms on the device against
+    // 1.6 ms on the host) keeps the host path, as does any request when REDUCTIONIST_GPU_INFLATE=0.
     // blosc2: a chunk is hundreds of independent block streams that the device decodes in parallel
-    // (k_blosc2), but a lone 4 MiB chunk still takes 1.6-1.7 ms there, and no record here
-    // shows that beating the reference's host decoder for ONE request; so a lone blosc2 request is
-    // decompressed on the host too unless the operator opts in (REDUCTIONIST_GPU_BLOSC2=1).  A codec the
+    // (k_blosc2), but a lone 4 MiB chunk takes 1.6 ms (LZ4) / 3.3 ms (zstd) there against
+    // 0.75 / 1.5 ms for liblz4 / libzstd on one host thread; so a lone blosc2 request
+    // is decompressed on the host unless the operator opts in (REDUCTIONIST_GPU_BLOSC2=1).  A codec the
     // device does not decode comes back as UnsupportedOperation and is decompressed here instead.
     let on_device = match request_data.compression {
         Some(models::Compression::Blosc2) => gpu_blosc2(),
