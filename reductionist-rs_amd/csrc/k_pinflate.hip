@@ -1297,6 +1297,10 @@ __global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
 // source precedes its byte); one that does not, or a link further back than the window, is an
 // inconsistency (stale sources after a failed emit): the check rejects the stream.
 constexpr uint32_t kTile = 32768, kTileThreads = 1024;
+#ifndef RDX_PINF_TILE_HOPS
+#define RDX_PINF_TILE_HOPS 4
+#endif
+constexpr uint32_t kTileHops = RDX_PINF_TILE_HOPS;
 
 __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
     __shared__ uint32_t tl[kTile];
@@ -1329,7 +1333,13 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
                 tl[i] = kFlag;
                 continue;
             }
-            const uint32_t w = tl[v - T0];
+            // up to kTileHops links per pass (each read may already see other entries' progress)
+            uint32_t w = tl[v - T0];
+#pragma unroll
+            for (uint32_t h = 1; h < kTileHops; ++h) {
+                if ((w & kFlag) || w < T0) break;
+                w = tl[w - T0];
+            }
             tl[i] = w;
             m |= !(w & kFlag) && w >= T0;
         }
