@@ -323,7 +323,7 @@ struct SrcOut {
         o0 = o;
     }
 };
-constexpr uint32_t kLongMatch = 32;   // matches at least this long are expanded by k_pinf_expand
+constexpr uint32_t kLongMatch = kPinfLongMatch;   // matches at least this long are expanded by k_pinf_expand
 
 // One lane: decode symbols from the reader's position until the first symbol boundary at or past `stop`
 // (0), the end-of-block code (1, *exit after it) or an error (2).  *bytes = output bytes of the symbols

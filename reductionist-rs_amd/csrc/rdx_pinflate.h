@@ -11,6 +11,10 @@ constexpr uint32_t kPinfMaxCand = 4096;   // block-start candidates per stream (
 #endif
 constexpr uint32_t kPinfLanes = RDX_PINF_LANES;   // decode lanes per block (k_pinf_block / k_pinf_emit)
 constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
+#ifndef RDX_PINF_LONG_MATCH
+#define RDX_PINF_LONG_MATCH 32
+#endif
+constexpr uint32_t kPinfLongMatch = RDX_PINF_LONG_MATCH;   // matches this long are expanded by k_pinf_expand
 
 enum : uint32_t { kPinfFallback = 0, kPinfOk = 1, kPinfMiss = 2 };
 

@@ -680,8 +680,8 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
     }
     const uint64_t total = h.total;
     if ((st = ensure(ws, ws->raw, std::max<uint64_t>((total + 15) / 16 * 16, 16), s))) return st;
-    // the sources, the long-match records (at most total / 32 of them), the tiles' flags
-    const uint64_t mcap = total / 32, msta = (total + 3) / 4 * 4, tiles = (total + 32767) / 32768;
+    // the sources, the long-match records (at most total / kPinfLongMatch of them), the tiles' flags
+    const uint64_t mcap = total / kPinfLongMatch, msta = (total + 3) / 4 * 4, tiles = (total + 32767) / 32768;
     if ((st = ensure(ws, ws->psrc, std::max<uint64_t>(msta + 4 * mcap + tiles, 1), s))) return st;
     a.src = ws->psrc.p;
     a.mlist = reinterpret_cast<uint4 *>(ws->psrc.p + msta);
