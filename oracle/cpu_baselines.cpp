@@ -94,6 +94,16 @@ extern "C" {
 // 1 when liblz4.so.1 can be loaded here
 int cpu_lz4lib_available(void) { return load_lz4() ? 1 : 0; }
 
+// One chunk into out (raw_len bytes + 64 of slack): what the timed pool decodes per job, for the tests to
+// check the baseline's output against the golden chunks.  Returns 0 when decoded, else an error.
+int cpu_blosc2_lz4lib_one(const uint8_t *chunk, uint64_t len, uint8_t *out, uint64_t raw_len, int mode) {
+    const lz4_fn lz4 = load_lz4();
+    if (!lz4) return -1;
+    std::vector<uint8_t> tmp(raw_len + 64);
+    uint64_t bytes = 0;
+    return decode_chunk(lz4, chunk, len, out, tmp.data(), mode, &bytes);
+}
+
 // Decode jobs 0..n_jobs-1 (job i = chunk i % distinct) on `threads` threads; *seconds = wall time of the
 // pool (threads started before the clock), *lz4_bytes = bytes produced by LZ4_decompress_safe.
 // Returns the number of chunks that failed (0 expected).
