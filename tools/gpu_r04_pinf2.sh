@@ -1,5 +1,5 @@
 # GPU box (round 4): pinflate tests, then the lone-stream probe + per-workgroup profile for the product
-# library and the 1024-lane variant (librdx_l1024.so), then the find-kernel probe.
+# library and each variant library named in RDX_VARIANTS, then the find-kernel probe.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 rc=$?
 tail -3 $OUT/pytest_pinf.txt
 [ $rc -eq 0 ] || { tail -40 $OUT/pytest_pinf.txt; exit $rc; }
-for lib in librdx librdx_l1024; do
+for lib in librdx ${RDX_VARIANTS:-}; do
   [ -f reductionist-rs_amd/$lib.so ] || continue
   echo "== $lib"
   RDX_LIB_PATH=$PWD/reductionist-rs_amd/$lib.so timeout -k 10 300 python -u tools/probe_pinflate.py 10 > $OUT/probe_$lib.jsonl 2>$OUT/probe_$lib.err || { tail -20 $OUT/probe_$lib.err; exit 1; }
