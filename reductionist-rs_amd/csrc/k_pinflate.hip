@@ -1349,31 +1349,33 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
     bool lit = true;
     for (uint32_t i = t; i < n; i += kTileThreads) lit &= (tl[i] & kFlag) != 0;
     const bool all_lit = __syncthreads_and(lit);
-    if (all_lit) {   // the bytes themselves (out is 16-byte aligned)
+    if (all_lit) {   // the bytes themselves (out is 16-byte aligned), and the literals over the sources for
+                     // k_pinf_xhop, whose links into this tile then resolve with one read
         for (uint32_t i = 4 * t; i < n; i += 4 * kTileThreads) {
             if (i + 4 <= n) {
                 gst<uint32_t>(a.out + T0 + i, (tl[i] & 0xff) | (tl[i + 1] & 0xff) << 8 | (tl[i + 2] & 0xff) << 16 | tl[i + 3] << 24);
+                gst<uint4>(reinterpret_cast<uint4 *>(src + i), make_uint4(tl[i], tl[i + 1], tl[i + 2], tl[i + 3]));
             } else {
-                for (uint32_t k = i; k < n; ++k) a.out[T0 + k] = (uint8_t)tl[k];
+                for (uint32_t k = i; k < n; ++k) {
+                    a.out[T0 + k] = (uint8_t)tl[k];
+                    src[k] = tl[k];
+                }
             }
         }
-    } else {         // 16-bit entries over the tile's own (already read) sources
-        uint16_t *rel = reinterpret_cast<uint16_t *>(src);
-        const uint64_t base = T0 - kTile;   // the previous tile (T0 > 0 here: tile 0 has no links out)
-        auto enc = [&](uint32_t v) -> uint32_t {
-            if (v & kFlag) return 0x8000u | (v & 0xff);
-            if (T0 == 0 || v < base || v >= T0) {
+    } else {         // the entries themselves, back over the tile's sources: literals, or links into the previous tile
+        const uint64_t base = T0 - kTile;   // (T0 > 0 here: tile 0 has no links out)
+        auto chk = [&](uint32_t v) -> uint32_t {
+            if (!(v & kFlag) && (T0 == 0 || v < base || v >= T0)) {
                 err = true;
-                return 0x8000u;
+                return kFlag;
             }
-            return (uint32_t)(v - base);
+            return v;
         };
-        for (uint32_t i = 8 * t; i < n; i += 8 * kTileThreads) {
-            if (i + 8 <= n) {
-                gst<uint4>(rel + i, make_uint4(enc(tl[i]) | enc(tl[i + 1]) << 16, enc(tl[i + 2]) | enc(tl[i + 3]) << 16,
-                                               enc(tl[i + 4]) | enc(tl[i + 5]) << 16, enc(tl[i + 6]) | enc(tl[i + 7]) << 16));
+        for (uint32_t i = 4 * t; i < n; i += 4 * kTileThreads) {
+            if (i + 4 <= n) {
+                gst<uint4>(reinterpret_cast<uint4 *>(src + i), make_uint4(chk(tl[i]), chk(tl[i + 1]), chk(tl[i + 2]), chk(tl[i + 3])));
             } else {
-                for (uint32_t k = i; k < n; ++k) rel[k] = (uint16_t)enc(tl[k]);
+                for (uint32_t k = i; k < n; ++k) src[k] = chk(tl[k]);
             }
         }
     }
@@ -1381,57 +1383,70 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
     if (__syncthreads_or(err) && t == 0) atomicOr(&st->emit_err, 4u);
 }
 
-__global__ __launch_bounds__(kTileThreads) void k_pinf_scan(PinfArgs a) {
-    __shared__ uint8_t win[2][kTile];
-    const uint64_t N = a.state->total;
-    const uint32_t tiles = (uint32_t)((N + kTile - 1) / kTile), full = (uint32_t)(N / kTile), t = threadIdx.x;
-    // a full tile's loads are issued one tile ahead (the walk is one workgroup: latency is its bound):
-    // entries of a tile with links, or the bytes of a literal tile that the next tile reads
-    uint4 nx[4] = {};
-    auto issue = [&](uint32_t k) {
-        const uint64_t T0 = (uint64_t)k * kTile;
-        if (!a.tflag[k]) {
-            const uint16_t *rel = reinterpret_cast<const uint16_t *>(a.src + T0);
+// Cross-tile links, resolved in parallel by pointer jumping over every tile with links at once: round r
+// replaces each link by its target's own entry (a literal tile's entries are its literals), so a chain of h
+// tiles needs ceil(log2 h) + 1 rounds and every tile advances in every round; a round whose predecessor
+// left nothing unresolved returns at once.  Entries are read and written in place while other threads
+// advance them: any value read is an ancestor on the same chain, so the rounds only converge faster.
+constexpr uint32_t kXThreads = 256, kXPer = 8, kXPerTile = kTile / (kXThreads * kXPer);
+
+__global__ __launch_bounds__(kXThreads) void k_pinf_xhop(PinfArgs a, uint32_t r) {
+    PinfState *st = a.state;
+    if (r && !st->xmore[r - 1]) return;
+    const uint64_t N = st->total;
+    const uint32_t tile = blockIdx.x / kXPerTile;
+    if (a.tflag[tile]) return;
+    // entry j of a thread is base + t + 256 j: each load instruction reads 64 consecutive entries, and
+    // their targets (the consecutive sources of a match) are consecutive too
+    const uint64_t base = (uint64_t)tile * kTile + (blockIdx.x % kXPerTile) * (kXThreads * kXPer) + threadIdx.x;
+    bool more = false;
+    uint32_t v[kXPer], w[kXPer];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) nx[j] = gld<uint4>(reinterpret_cast<const uint4 *>(rel + 8 * (t + kTileThreads * j)));
-        } else if (k + 1 < tiles && !a.tflag[k + 1]) {
-#pragma unroll
-            for (uint32_t j = 0; j < 2; ++j) nx[j] = gld<uint4>(reinterpret_cast<const uint4 *>(a.out + T0 + 16 * (t + kTileThreads * j)));
-        }
-    };
-    if (full) issue(0);
-    for (uint32_t k = 0; k < tiles; ++k) {
-        const uint64_t T0 = (uint64_t)k * kTile;
-        const uint32_t n = (uint32_t)min<uint64_t>(kTile, N - T0);
-        uint8_t *cur = win[k & 1];
-        const uint8_t *prev = win[(k & 1) ^ 1];
-        auto dec = [&](uint32_t r) -> uint32_t { return r & 0x8000u ? r & 0xff : prev[r & 0x7fff]; };
-        const bool lit = a.tflag[k] != 0;
-        if (k < full) {
-            uint4 v[4];
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) v[j] = nx[j];
-            if (k + 1 < full) issue(k + 1);
-            if (lit) {
-                if (k + 1 < tiles && !a.tflag[k + 1])
-#pragma unroll
-                    for (uint32_t j = 0; j < 2; ++j) *reinterpret_cast<uint4 *>(cur + 16 * (t + kTileThreads * j)) = v[j];
-            } else {
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) {
-                    const uint32_t i = 8 * (t + kTileThreads * j);
-                    const uint32_t lo = dec(v[j].x & 0xffff) | dec(v[j].x >> 16) << 8 | dec(v[j].y & 0xffff) << 16 | dec(v[j].y >> 16) << 24;
-                    const uint32_t hi = dec(v[j].z & 0xffff) | dec(v[j].z >> 16) << 8 | dec(v[j].w & 0xffff) << 16 | dec(v[j].w >> 16) << 24;
-                    *reinterpret_cast<uint2 *>(cur + i) = make_uint2(lo, hi);
-                    gst<uint64_t>(a.out + T0 + i, (uint64_t)hi << 32 | lo);
-                }
-            }
-        } else if (!lit) {   // the last, partial tile (nothing reads it after)
-            const uint16_t *rel = reinterpret_cast<const uint16_t *>(a.src + T0);
-            for (uint32_t j = t; j < n; j += kTileThreads) a.out[T0 + j] = (uint8_t)dec(rel[j]);
-        }
-        __syncthreads();
+    for (uint32_t j = 0; j < kXPer; ++j) {
+        const uint64_t i = base + kXThreads * j;
+        v[j] = i < N ? gld<uint32_t>(a.src + i) : kFlag;
     }
+    // the targets' entries as independent loads (a literal reads its own slot; past the end, the first)
+#pragma unroll
+    for (uint32_t j = 0; j < kXPer; ++j) {
+        const uint64_t i = base + kXThreads * j;
+        w[j] = gld<uint32_t>(a.src + ((v[j] & kFlag) ? (i < N ? i : 0) : v[j]));
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kXPer; ++j) {
+        const uint64_t i = base + kXThreads * j;
+        if (!(v[j] & kFlag)) {
+            more |= !(w[j] & kFlag);
+            a.src[i] = w[j];
+        }
+    }
+    // one plain store per workgroup that left a link (same-address atomics from every wave serialise in
+    // L2 and cost a full round's time); every store writes the same 1
+    if (__syncthreads_or(more) && threadIdx.x == 0 && !__builtin_nontemporal_load(&st->xmore[r])) st->xmore[r] = 1u;
+}
+
+// the bytes of every tile with links (an entry still a link after the rounds is an inconsistency)
+__global__ __launch_bounds__(kXThreads) void k_pinf_xout(PinfArgs a) {
+    PinfState *st = a.state;
+    const uint64_t N = st->total;
+    const uint32_t tile = blockIdx.x / kXPerTile;
+    if (a.tflag[tile]) return;
+    const uint64_t i0 = (uint64_t)tile * kTile + (blockIdx.x % kXPerTile) * (kXThreads * kXPer) + kXPer * threadIdx.x;
+    bool err = false;
+    if (i0 + kXPer <= N) {
+        const uint4 p = gld<uint4>(reinterpret_cast<const uint4 *>(a.src + i0)), q = gld<uint4>(reinterpret_cast<const uint4 *>(a.src + i0 + 4));
+        err = !((p.x & p.y & p.z & p.w & q.x & q.y & q.z & q.w) & kFlag);
+        const uint32_t lo = (p.x & 0xff) | (p.y & 0xff) << 8 | (p.z & 0xff) << 16 | (p.w & 0xff) << 24;
+        const uint32_t hi = (q.x & 0xff) | (q.y & 0xff) << 8 | (q.z & 0xff) << 16 | (q.w & 0xff) << 24;
+        gst<uint64_t>(reinterpret_cast<uint64_t *>(a.out + i0), (uint64_t)hi << 32 | lo);
+    } else {
+        for (uint64_t i = i0; i < N; ++i) {
+            const uint32_t v = a.src[i];
+            err |= !(v & kFlag);
+            a.out[i] = (uint8_t)v;
+        }
+    }
+    if (__ballot(err) && (threadIdx.x & 63) == 0) atomicOr(&st->emit_err, 4u);
 }
 
 // ---- 6. bytes + checksums -----------------------------------------------------------------------------------
@@ -1575,7 +1590,12 @@ hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total,
     if (a.mcap) hipLaunchKernelGGL(k_pinf_expand, dim3((a.mcap + 3) / 4), dim3(256), 0, s, a);
     if (total) {
         hipLaunchKernelGGL(k_pinf_tile, dim3((uint32_t)((total + kTile - 1) / kTile)), dim3(kTileThreads), 0, s, a);
-        hipLaunchKernelGGL(k_pinf_scan, dim3(1), dim3(kTileThreads), 0, s, a);
+        const uint32_t tiles = (uint32_t)((total + kTile - 1) / kTile);
+        uint32_t rounds = 2;   // ceil(log2(tiles)) + 1 >= the rounds a chain of tiles - 1 hops needs
+        while ((1ull << (rounds - 1)) < tiles) ++rounds;
+        for (uint32_t r = 0; r < rounds && tiles > 1; ++r)
+            hipLaunchKernelGGL(k_pinf_xhop, dim3(tiles * kXPerTile), dim3(kXThreads), 0, s, a, r);
+        if (tiles > 1) hipLaunchKernelGGL(k_pinf_xout, dim3(tiles * kXPerTile), dim3(kXThreads), 0, s, a);
     }
     const uint32_t parts = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kPinfMaxParts, (total + 4095) / 4096));
     hipLaunchKernelGGL(k_pinf_finish, dim3(parts), dim3(256), 0, s, a);

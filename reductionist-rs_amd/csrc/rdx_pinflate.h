@@ -37,6 +37,7 @@ struct PinfState {
     uint64_t trailer_byte;            // the checksum trailer (aligned byte position)
     uint32_t final_ok, n_match;       // k_pinf_check's verdict; long-match records of k_pinf_emit
     uint32_t n_surv, pad;             // offsets k_pinf_find's screen passed to the full header test
+    uint32_t xmore[32];               // k_pinf_xhop round r left links unresolved
 };
 
 struct PinfArgs {
