@@ -1388,7 +1388,14 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
 // tiles needs ceil(log2 h) + 1 rounds and every tile advances in every round; a round whose predecessor
 // left nothing unresolved returns at once.  Entries are read and written in place while other threads
 // advance them: any value read is an ancestor on the same chain, so the rounds only converge faster.
-constexpr uint32_t kXThreads = 256, kXPer = 8, kXPerTile = kTile / (kXThreads * kXPer);
+#ifndef RDX_PINF_XHOPS
+#define RDX_PINF_XHOPS 2
+#endif
+#ifndef RDX_PINF_XPER
+#define RDX_PINF_XPER 8
+#endif
+constexpr uint32_t kXThreads = 256, kXPer = RDX_PINF_XPER, kXPerTile = kTile / (kXThreads * kXPer);
+constexpr uint32_t kXHops = RDX_PINF_XHOPS;   // links followed per entry and round
 
 __global__ __launch_bounds__(kXThreads) void k_pinf_xhop(PinfArgs a, uint32_t r) {
     PinfState *st = a.state;
@@ -1411,6 +1418,12 @@ __global__ __launch_bounds__(kXThreads) void k_pinf_xhop(PinfArgs a, uint32_t r)
     for (uint32_t j = 0; j < kXPer; ++j) {
         const uint64_t i = base + kXThreads * j;
         w[j] = gld<uint32_t>(a.src + ((v[j] & kFlag) ? (i < N ? i : 0) : v[j]));
+    }
+#pragma unroll
+    for (uint32_t h = 1; h < kXHops; ++h) {
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j)
+            if (!(v[j] & kFlag) && !(w[j] & kFlag)) w[j] = gld<uint32_t>(a.src + w[j]);
     }
 #pragma unroll
     for (uint32_t j = 0; j < kXPer; ++j) {
@@ -1591,8 +1604,10 @@ hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total,
     if (total) {
         hipLaunchKernelGGL(k_pinf_tile, dim3((uint32_t)((total + kTile - 1) / kTile)), dim3(kTileThreads), 0, s, a);
         const uint32_t tiles = (uint32_t)((total + kTile - 1) / kTile);
-        uint32_t rounds = 2;   // ceil(log2(tiles)) + 1 >= the rounds a chain of tiles - 1 hops needs
-        while ((1ull << (rounds - 1)) < tiles) ++rounds;
+        // a round multiplies the tiles every unresolved link has covered by kXHops + 1, and a chain spans
+        // at most tiles - 1: one round more than that needs
+        uint32_t rounds = 1;
+        for (uint64_t cov = 1; cov < tiles; cov *= kXHops + 1) ++rounds;
         for (uint32_t r = 0; r < rounds && tiles > 1; ++r)
             hipLaunchKernelGGL(k_pinf_xhop, dim3(tiles * kXPerTile), dim3(kXThreads), 0, s, a, r);
         if (tiles > 1) hipLaunchKernelGGL(k_pinf_xout, dim3(tiles * kXPerTile), dim3(kXThreads), 0, s, a);
