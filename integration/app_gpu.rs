@@ -40,8 +40,8 @@ pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
 ) -> Result<models::Response, ActiveStorageError> {
     // gzip / zlib: a lone request's DEFLATE stream is decoded by the whole device (k_pinflate, DESIGN.md
     // §9.1: candidate block starts, blocks and the symbols inside them decoded in parallel, then the copies
-    // resolved): a 4 MiB zlib-1 chunk in 0.67 ms against 3.5 ms for zlib on one host core, integer-valued
-    // chunks 0.9 ms against 6-10 ms (profiles/r04_pinflate_probe.jsonl, r04_bench.json).  A stream whose
+    // resolved): a 4 MiB zlib-1 chunk in 0.59 ms against 3.6 ms for zlib on one host core, integer-valued
+    // chunks 0.6 ms against 6-10 ms (profiles/r04_pinflate_probe_xhop.jsonl, r04_bench.json).  A stream whose
     // request states it expands more than 16-fold (long matches, few blocks: 7.8 ms on the device against
     // 1.6 ms on the host) keeps the host path, as does any request when REDUCTIONIST_GPU_INFLATE=0.
     // blosc2: a chunk is hundreds of independent block streams that the device decodes in parallel
