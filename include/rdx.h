@@ -25,7 +25,9 @@
 extern "C" {
 #endif
 
-#define RDX_ABI_VERSION 1u
+/* 2: rdx_device_stats grew to 80 bytes (round 4) and rdx_context_config.inflate_fallback (round 5).  A host
+ * checks rdx_abi_version() == RDX_ABI_VERSION once at load time before passing any struct. */
+#define RDX_ABI_VERSION 2u
 /* Maximum rank of a request shape (the reference accepts any rank via ndarray IxDyn; 32 matches
  * numpy's NPY_MAXDIMS and is far above any chunk layout seen in practice). */
 #define RDX_MAX_NDIM 32u
@@ -77,9 +79,9 @@ typedef enum rdx_inflate_error {
                                         user-defined codecs or filters, delta): status RDX_E_UNSUPPORTED */
 } rdx_inflate_error;
 
-/* Why this thread's last RDX_E_UNSUPPORTED was returned (rdx_last_unsupported_reason).  Only BLOSC2_CODEC
- * concerns the chunk's encoding (decompress it on the host and call again); every other reason is a request
- * the reference serves that this engine does not plan (run the reference's CPU path for it). */
+/* Why this thread's last RDX_E_UNSUPPORTED was returned (rdx_last_unsupported_reason).  BLOSC2_CODEC and
+ * INFLATE_DECLINED concern the chunk's encoding (decompress it on the host and call again); every other reason
+ * is a request the reference serves that this engine does not plan (run the reference's CPU path for it). */
 typedef enum rdx_unsupported_reason {
     RDX_UNSUPPORTED_NONE = 0,
     RDX_UNSUPPORTED_BLOSC2_CODEC = 1, /* RDX_BLOSC2_UNSUPPORTED: dictionaries, delta, user codecs, zstd checksums */
@@ -87,7 +89,12 @@ typedef enum rdx_unsupported_reason {
     RDX_UNSUPPORTED_VIEW_SIZE = 3,    /* a view of 2^32 or more elements, or a dim of 2^32 or more            */
     RDX_UNSUPPORTED_VIEW_DIMS = 4,    /* more than 16 dims left after canonicalisation                       */
     RDX_UNSUPPORTED_MISSING_LIST = 5, /* a missing_values list of 2^32 or more entries                       */
-    RDX_UNSUPPORTED_CBOR_SIZE = 6     /* a CBOR count vector of 2^43 or more entries                          */
+    RDX_UNSUPPORTED_CBOR_SIZE = 6,    /* a CBOR count vector of 2^43 or more entries                          */
+    RDX_UNSUPPORTED_INFLATE_DECLINED = 7 /* a lone gzip / zlib stream (> 4 KiB) the parallel decoder (k_pinflate)
+                                        did not accept — a block chain it does not follow (e.g. many fixed-
+                                        Huffman blocks) or a corrupt stream: decompress it on the host (the
+                                        reference's decoder gives its bytes or its error) and call again
+                                        uncompressed.  Only with inflate_fallback = 0 (the default).        */
 } rdx_unsupported_reason;
 
 /* ---- request enums (src/models.rs) ------------------------------------------------------------ */
@@ -203,7 +210,11 @@ typedef struct rdx_context_config {
     uint32_t max_workspaces;        /* per pool entry (0: 16); requests beyond it wait for a free one           */
     uint32_t coalesce;              /* 1 (default): coalesce small all-axes requests into k_multi launches; 0: off */
     uint32_t coalesce_lanes;        /* coalesced launches in flight per pool entry (0: 3)                      */
-    uint32_t reserved;
+    uint32_t inflate_fallback;      /* a lone gzip / zlib stream k_pinflate declines: 0 (default) -> RDX_E_UNSUPPORTED
+                                       (RDX_UNSUPPORTED_INFLATE_DECLINED; streams up to 4 KiB still decode on the
+                                       device), 1 -> the sequential k_inflate decodes it on the device (its bytes
+                                       or its error; 100-220 ms per 4 MiB).  Workspaces keep the value they were
+                                       created with.                                                          */
     uint64_t coalesce_max_bytes;    /* rdx_execute_resident chunks up to this many bytes coalesce (0: 64 MiB)  */
     uint64_t coalesce_host_max_bytes; /* rdx_execute / _owned host chunks up to this many (0: 1 MiB)           */
 } rdx_context_config;
@@ -248,13 +259,15 @@ const char *rdx_inflate_error_string(uint32_t code);
 uint32_t rdx_inflate_last_error(void);
 /* How this thread's last compressed request was decompressed: a lone gzip / zlib stream is decoded by the
  * whole device (k_pinflate: block starts found, blocks and the symbols inside them decoded in parallel);
- * a stream that path does not accept (errors, a block chain it cannot follow) is decoded again by the
+ * a stream that path does not accept (errors, a block chain it cannot follow) goes back to the caller
+ * (DECLINED: RDX_E_UNSUPPORTED) or, with inflate_fallback / up to 4 KiB, is decoded again by the
  * sequential k_inflate, whose result and error are the reference's. */
 typedef enum rdx_inflate_path {
     RDX_INFLATE_PATH_NONE = 0,
     RDX_INFLATE_PATH_SERIAL = 1,            /* k_inflate (one wavefront per stream) / k_blosc2             */
     RDX_INFLATE_PATH_PARALLEL = 2,          /* k_pinflate                                                   */
-    RDX_INFLATE_PATH_PARALLEL_FALLBACK = 3  /* k_pinflate declined, then k_inflate                          */
+    RDX_INFLATE_PATH_PARALLEL_FALLBACK = 3, /* k_pinflate declined, then k_inflate                          */
+    RDX_INFLATE_PATH_DECLINED = 4           /* k_pinflate declined: RDX_E_UNSUPPORTED, INFLATE_DECLINED       */
 } rdx_inflate_path;
 uint32_t rdx_inflate_last_path(void);
 /* The rdx_unsupported_reason of this thread's last RDX_E_UNSUPPORTED. */
@@ -386,8 +399,9 @@ rdx_status rdx_decompress_batch_device(rdx_workspace *ws, uint32_t compression, 
                                        uint64_t *d_out_lens, uint32_t *d_errors, void *stream);
 
 /* One device-resident gzip / zlib stream (d_in, len bytes), decoded by the whole device — the lone
- * compressed request of compression.rs:60-82 (k_pinflate; a stream it does not accept is decoded by
- * k_inflate, whose result and error are the reference's) — SYNCHRONOUSLY on `stream`.  *out_len (host) =
+ * compressed request of compression.rs:60-82 (k_pinflate; a stream it does not accept returns
+ * RDX_E_UNSUPPORTED / RDX_UNSUPPORTED_INFLATE_DECLINED, or with the workspace's inflate_fallback is decoded
+ * by k_inflate, whose result and error are the reference's) — SYNCHRONOUSLY on `stream`.  *out_len (host) =
  * the decompressed size; *error (host) = rdx_inflate_error: RDX_INFLATE_OUTPUT_OVERFLOW when that size
  * exceeds out_cap (nothing written), else the bytes are in d_out.  rdx_inflate_last_path() tells which
  * decoder produced them. */

@@ -41,14 +41,18 @@ pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
     // gzip / zlib: a lone request's DEFLATE stream is decoded by the whole device (k_pinflate, DESIGN.md
     // §9.1: candidate block starts, blocks and the symbols inside them decoded in parallel, then the copies
     // resolved): a 4 MiB zlib-1 chunk in 0.59 ms against 3.6 ms for zlib on one host core, integer-valued
-    // chunks 0.6 ms against 6-10 ms (profiles/r04_pinflate_probe_xhop.jsonl, r04_bench.json).  A stream whose
-    // request states it expands more than 16-fold (long matches, few blocks: 7.8 ms on the device against
-    // 1.6 ms on the host) keeps the host path, as does any request when REDUCTIONIST_GPU_INFLATE=0.
+    // chunks 0.6 ms against 6-10 ms (profiles/r04_pinflate_probe_xhop.jsonl, r04_bench.json).  A stream the
+    // device declines (a block chain it does not follow, e.g. many fixed-Huffman blocks, or a corrupt
+    // stream) comes back as UnsupportedOperation after the parallel attempt and is decompressed here, by the
+    // reference's own decoder (its bytes or its error).  A stream whose request states it expands more than
+    // 16-fold keeps the host path, as does any request when REDUCTIONIST_GPU_INFLATE=0.
     // blosc2: a chunk is hundreds of independent block streams that the device decodes in parallel
     // (k_blosc2), but a lone 4 MiB chunk takes 1.6 ms (LZ4) / 3.3 ms (zstd) there against
     // 0.75 / 1.5 ms for liblz4 / libzstd on one host thread; so a lone blosc2 request
     // is decompressed on the host unless the operator opts in (REDUCTIONIST_GPU_BLOSC2=1).  A codec the
     // device does not decode comes back as UnsupportedOperation and is decompressed here instead.
+    // (The engine's context is created with inflate_fallback = 0: a declined stream never runs the
+    // one-wavefront k_inflate, 100-220 ms per 4 MiB.)
     let on_device = match request_data.compression {
         Some(models::Compression::Blosc2) => gpu_blosc2(),
         Some(_) => gpu_inflate(&request_data, data.len()),

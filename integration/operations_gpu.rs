@@ -100,11 +100,14 @@ pub fn execute_slice(rd: &models::RequestData, data: &[u8], op: u32) -> Result<m
     ))
 }
 
-/// RDX_E_UNSUPPORTED for a reason other than the chunk's blosc2 codec: a request the reference serves
-/// that the engine does not plan (rank above 32, views of 2^32 or more elements; include/rdx.h
-/// rdx_unsupported_reason).  It runs on the reference's own CPU path instead of failing.
+/// RDX_E_UNSUPPORTED for a reason other than the chunk's encoding (a blosc2 codec the device does not
+/// decode, a gzip / zlib stream k_pinflate declined — both come back to `app_gpu::operation_gpu` as
+/// UnsupportedOperation and are decompressed on the host): a request the reference serves that the engine
+/// does not plan (rank above 32, views of 2^32 or more elements; include/rdx.h rdx_unsupported_reason).  It
+/// runs on the reference's own CPU path instead of failing.
 fn planned_on_cpu(st: i32) -> bool {
-    st == status::E_UNSUPPORTED && unsafe { rdx_last_unsupported_reason() } != unsupported::BLOSC2_CODEC
+    st == status::E_UNSUPPORTED
+        && !matches!(unsafe { rdx_last_unsupported_reason() }, unsupported::BLOSC2_CODEC | unsupported::INFLATE_DECLINED)
 }
 
 /// The reference's synchronous path for this route, unchanged: `operation::<T>` (app.rs:163-183: the
@@ -362,10 +365,11 @@ pub fn check(st: i32, compression: Option<Compression>, dtype: DType) -> Result<
         E_SHUFFLE_LENGTH => panic!("assertion `left == right` failed"),
         // operations.rs:181-183,355-357: NaN in a min/max comparison panics in the reference; parity
         E_NAN_UNORDERED => panic!("unexpected undefined order error for min"),
-        // a blosc2 codec / filter the device does not decode (dictionaries, delta, checksummed zstd frames):
-        // app_gpu::operation_gpu catches this variant and decompresses on the host instead.  The other
+        // a blosc2 codec / filter the device does not decode (dictionaries, delta, checksummed zstd frames) or
+        // a gzip / zlib stream k_pinflate declined: app_gpu::operation_gpu catches this variant and
+        // decompresses on the host instead (the reference's decoder: its bytes or its error).  The other
         // reasons never get here: Gpu<OP> serves them on the reference CPU path (planned_on_cpu).
-        E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "blosc2 codec on the GPU".into() }),
+        E_UNSUPPORTED => Err(ActiveStorageError::UnsupportedOperation { operation: "chunk codec on the GPU".into() }),
         // compression.rs:60-82 -> DecompressionFlate2 / DecompressionZune, 400 (error.rs:247-249)
         E_DECOMPRESSION => {
             let code = unsafe { rdx_inflate_last_error() };

@@ -23,9 +23,10 @@
 //!   rdx_decompress_batch_device       compression.rs:18-27 `decompress` for a batch of device streams
 //!   rdx_inflate_last_error / _string  the detail of RDX_E_DECOMPRESSION (error.rs:33-41)
 //!   rdx_decompress_one_device         compression.rs:60-82 for ONE device stream, decoded by the whole device
-//!   rdx_inflate_last_path             which decoder ran (k_pinflate, or k_inflate after it declined)
-//!   rdx_last_unsupported_reason       the cause of RDX_E_UNSUPPORTED: a blosc2 codec (host decompression)
-//!                                     or a request only the reference CPU path plans (operations.rs)
+//!   rdx_inflate_last_path             which decoder ran (k_pinflate; declined; or k_inflate)
+//!   rdx_last_unsupported_reason       the cause of RDX_E_UNSUPPORTED: a blosc2 codec or a gzip / zlib stream
+//!                                     k_pinflate declined (host decompression), or a request only the
+//!                                     reference CPU path plans (operations.rs)
 //!   rdx_execute_cbor                  app.rs:163-183 + app.rs:33-40: the response leaves the engine as
 //!                                     its CBOR body
 //!   rdx_cbor_bound / _encode / _encode_device
@@ -37,7 +38,7 @@
 use core::mem::{offset_of, size_of};
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const RDX_ABI_VERSION: u32 = 1;
+pub const RDX_ABI_VERSION: u32 = 2;
 pub const RDX_MAX_NDIM: usize = 32;
 /// rdx_cbor_* flags: RequestData.option_shape_as_bytes / option_count_as_bytes (models.rs:173-175)
 pub const RDX_CBOR_SHAPE_AS_BYTES: u32 = 1;
@@ -78,6 +79,7 @@ pub mod unsupported {
     pub const VIEW_DIMS: u32 = 4;
     pub const MISSING_LIST: u32 = 5;
     pub const CBOR_SIZE: u32 = 6;
+    pub const INFLATE_DECLINED: u32 = 7; // a lone gzip / zlib stream k_pinflate did not accept: host decompression
 }
 
 #[repr(C)]
@@ -166,7 +168,7 @@ pub struct RdxContextConfig {
     pub max_workspaces: u32,
     pub coalesce: u32,
     pub coalesce_lanes: u32,
-    pub reserved: u32,
+    pub inflate_fallback: u32, // 0: declined lone gzip / zlib streams -> E_UNSUPPORTED (INFLATE_DECLINED)
     pub coalesce_max_bytes: u64,
     pub coalesce_host_max_bytes: u64,
 }

@@ -198,9 +198,9 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 #pragma unroll
                 for (int m = 0; m < 4; ++m) xs[m] = from_u<T>((U)(((uint64_t)hi[m] << 32) | lo[m]));
                 if constexpr (kGroupSum<T, OP, MK>) {
-                    // the 4 elements summed pairwise, then one compensated add (a quarter of the
-                    // per-element Neumaier steps)
-                    Red<T, OP>::neumaier(r.s, r.c, ((double)xs[0] + (double)xs[1]) + ((double)xs[2] + (double)xs[3]));
+                    // the 4 elements summed pairwise with their rounding errors kept, then one
+                    // compensated add (a quarter of the per-element Neumaier steps, the same accuracy)
+                    Red<T, OP>::add4(r.s, r.c, (double)xs[0], (double)xs[1], (double)xs[2], (double)xs[3]);
                     r.cnt += 4;
                 } else {
                     consume_group<T, OP, MK, 4>(r, xs, a, e + j * 4);
@@ -239,7 +239,7 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 #pragma unroll
                 for (int q = 0; q < 2; ++q) xs[q] = from_u<T>((U)(bswap ? bswap_u(w[q]) : w[q]));
                 if constexpr (kGroupSum<T, OP, MK>) {
-                    Red<T, OP>::neumaier(r.s, r.c, (double)xs[0] + (double)xs[1]);
+                    Red<T, OP>::add2(r.s, r.c, (double)xs[0], (double)xs[1]);
                     r.cnt += 2;
                 } else {
                     consume_group<T, OP, MK, 2>(r, xs, a, e);

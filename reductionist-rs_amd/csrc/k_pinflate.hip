@@ -27,8 +27,8 @@
 //                   before it).
 //  5. k_pinf_tile   pointer jumping over the sources inside 32 KiB tiles of output in LDS (a link always
 //                   points to a byte with the same final value) until each byte is a literal or a link
-//                   into the previous tile; k_pinf_scan then walks the tiles in order, the previous
-//                   tile's bytes in LDS, and writes the bytes.
+//                   into the previous tile; k_pinf_xhop then resolves the links between tiles by pointer
+//                   jumping over every tile with links at once, and k_pinf_xout writes their bytes.
 //  6. k_pinf_finish / k_pinf_check  Adler-32 / CRC-32 over segments combined by weights / GF(2) shifts,
 //                   the trailer.
 //
@@ -1263,26 +1263,31 @@ __global__ __launch_bounds__(kLanes) void k_pinf_emit(PinfArgs a) {
 }
 
 // ---- 4b. long matches: one wavefront per match record ------------------------------------------------
+// (the grid is capped — launch_pinf_rest — and each wavefront loops over the records: near the 2^31-byte
+// limit one wavefront per record would exceed a launch's 2^32 work-items)
+constexpr uint32_t kExpandMaxBlocks = 65536;
+
 __global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
     const uint32_t n = min(a.state->n_match, a.mcap);
-    const uint32_t r = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x & 63;
-    if (r >= n) return;
-    const uint4 m = a.mlist[r];
-    const uint32_t o = m.x, len = m.y, dist = m.z;
+    const uint32_t lane = threadIdx.x & 63;
     uint32_t *src = a.src;
-    if ((uint64_t)o + len > a.state->total || dist > o || dist == 0) {   // (k_pinf_emit checked it: never)
-        if (lane == 0) atomicOr(&a.state->emit_err, 8u);
-        return;
-    }
-    if (dist >= len) {
-        for (uint32_t j = lane; j < len; j += 64) src[o + j] = o + j - dist;
-    } else {   // overlapping: (j mod dist) into the dist bytes before the match (a float quotient, corrected)
-        const float rd = __builtin_amdgcn_rcpf((float)dist);
-        for (uint32_t j = lane; j < len; j += 64) {
-            const uint32_t q = (uint32_t)((float)j * rd);
-            int32_t rem = (int32_t)(j - q * dist);
-            rem = rem < 0 ? rem + (int32_t)dist : (rem >= (int32_t)dist ? rem - (int32_t)dist : rem);
-            src[o + j] = o - dist + (uint32_t)rem;
+    for (uint32_t r = blockIdx.x * 4 + threadIdx.x / 64; r < n; r += gridDim.x * 4) {
+        const uint4 m = a.mlist[r];
+        const uint32_t o = m.x, len = m.y, dist = m.z;
+        if ((uint64_t)o + len > a.state->total || dist > o || dist == 0) {   // (k_pinf_emit checked it: never)
+            if (lane == 0) atomicOr(&a.state->emit_err, 8u);
+            continue;
+        }
+        if (dist >= len) {
+            for (uint32_t j = lane; j < len; j += 64) src[o + j] = o + j - dist;
+        } else {   // overlapping: (j mod dist) into the dist bytes before the match (a float quotient, corrected)
+            const float rd = __builtin_amdgcn_rcpf((float)dist);
+            for (uint32_t j = lane; j < len; j += 64) {
+                const uint32_t q = (uint32_t)((float)j * rd);
+                int32_t rem = (int32_t)(j - q * dist);
+                rem = rem < 0 ? rem + (int32_t)dist : (rem >= (int32_t)dist ? rem - (int32_t)dist : rem);
+                src[o + j] = o - dist + (uint32_t)rem;
+            }
         }
     }
 }
@@ -1291,11 +1296,10 @@ __global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
 // Tiles of 32 KiB of output, the DEFLATE window: a link from a tile leads into the same tile or the one
 // before it.  k_pinf_tile (one workgroup per tile, its sources in 128 KiB of LDS) follows every link that
 // stays in the tile, at LDS latency, until each byte is a literal or a link into the previous tile, and
-// writes the tile back as 16-bit entries (a literal byte, or an offset into the previous tile); a tile of
-// literals only writes its bytes.  k_pinf_scan (one workgroup) then walks the tiles in order with the
-// previous tile's bytes in LDS: each entry is its byte or one LDS read.  Links always point back (a copy
-// source precedes its byte); one that does not, or a link further back than the window, is an
-// inconsistency (stale sources after a failed emit): the check rejects the stream.
+// writes the tile back over its sources (a literal, or a link into the previous tile); a tile of literals
+// also writes its bytes.  k_pinf_xhop / k_pinf_xout (below) resolve the links between tiles.  Links always
+// point back (a copy source precedes its byte); one that does not, or a link further back than the window,
+// is an inconsistency (stale sources after a failed emit): the check rejects the stream.
 constexpr uint32_t kTile = 32768, kTileThreads = 1024;
 #ifndef RDX_PINF_TILE_HOPS
 #define RDX_PINF_TILE_HOPS 4
@@ -1386,8 +1390,11 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
 // Cross-tile links, resolved in parallel by pointer jumping over every tile with links at once: round r
 // replaces each link by its target's own entry (a literal tile's entries are its literals), so a chain of h
 // tiles needs ceil(log2 h) + 1 rounds and every tile advances in every round; a round whose predecessor
-// left nothing unresolved returns at once.  Entries are read and written in place while other threads
-// advance them: any value read is an ancestor on the same chain, so the rounds only converge faster.
+// left nothing unresolved returns at once.  Entries are read and written in place while other workgroups
+// advance them: every such access is a relaxed agent-scope atomic (single-copy atomic 32-bit entries, no
+// data race in the HIP memory model), and any value read is an ancestor on the same chain — an older entry
+// or one another workgroup already advanced — so the rounds only converge faster.  No ordering between
+// entries is needed: each entry is self-contained (a literal, or a position whose entry is still valid).
 #ifndef RDX_PINF_XHOPS
 #define RDX_PINF_XHOPS 2
 #endif
@@ -1396,6 +1403,10 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
 #endif
 constexpr uint32_t kXThreads = 256, kXPer = RDX_PINF_XPER, kXPerTile = kTile / (kXThreads * kXPer);
 constexpr uint32_t kXHops = RDX_PINF_XHOPS;   // links followed per entry and round
+
+__device__ __forceinline__ uint32_t xld(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __global__ __launch_bounds__(kXThreads) void k_pinf_xhop(PinfArgs a, uint32_t r) {
     PinfState *st = a.state;
@@ -1411,31 +1422,33 @@ __global__ __launch_bounds__(kXThreads) void k_pinf_xhop(PinfArgs a, uint32_t r)
 #pragma unroll
     for (uint32_t j = 0; j < kXPer; ++j) {
         const uint64_t i = base + kXThreads * j;
-        v[j] = i < N ? gld<uint32_t>(a.src + i) : kFlag;
+        v[j] = i < N ? xld(a.src + i) : kFlag;
     }
     // the targets' entries as independent loads (a literal reads its own slot; past the end, the first)
 #pragma unroll
     for (uint32_t j = 0; j < kXPer; ++j) {
         const uint64_t i = base + kXThreads * j;
-        w[j] = gld<uint32_t>(a.src + ((v[j] & kFlag) ? (i < N ? i : 0) : v[j]));
+        w[j] = xld(a.src + ((v[j] & kFlag) ? (i < N ? i : 0) : v[j]));
     }
 #pragma unroll
     for (uint32_t h = 1; h < kXHops; ++h) {
 #pragma unroll
         for (uint32_t j = 0; j < kXPer; ++j)
-            if (!(v[j] & kFlag) && !(w[j] & kFlag)) w[j] = gld<uint32_t>(a.src + w[j]);
+            if (!(v[j] & kFlag) && !(w[j] & kFlag)) w[j] = xld(a.src + w[j]);
     }
 #pragma unroll
     for (uint32_t j = 0; j < kXPer; ++j) {
         const uint64_t i = base + kXThreads * j;
         if (!(v[j] & kFlag)) {
             more |= !(w[j] & kFlag);
-            a.src[i] = w[j];
+            __hip_atomic_store(a.src + i, w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // one plain store per workgroup that left a link (same-address atomics from every wave serialise in
     // L2 and cost a full round's time); every store writes the same 1
-    if (__syncthreads_or(more) && threadIdx.x == 0 && !__builtin_nontemporal_load(&st->xmore[r])) st->xmore[r] = 1u;
+    if (__syncthreads_or(more) && threadIdx.x == 0 &&
+        !__hip_atomic_load(&st->xmore[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(&st->xmore[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the bytes of every tile with links (an entry still a link after the rounds is an inconsistency)
@@ -1465,7 +1478,10 @@ __global__ __launch_bounds__(kXThreads) void k_pinf_xout(PinfArgs a) {
 // ---- 6. bytes + checksums -----------------------------------------------------------------------------------
 constexpr uint32_t kAdler = 65521;
 
-__device__ uint32_t multmodp(uint32_t a, uint32_t b) {   // a(x) b(x) mod P (reflected), as zlib
+// GF(2) polynomial arithmetic modulo the CRC-32 polynomial, restated from zlib's crc32.c (multmodp /
+// x2nmodp; zlib 1.2.12+, (C) Jean-loup Gailly and Mark Adler, zlib license): a third-party algorithm, not
+// the reference's code.
+__device__ uint32_t multmodp(uint32_t a, uint32_t b) {   // a(x) b(x) mod P (reflected)
     uint32_t m = 1u << 31, p = 0;
     for (;;) {
         if (a & m) {
@@ -1600,7 +1616,8 @@ hipError_t launch_pinf_chain(const PinfArgs &a, hipStream_t s) {
 }
 hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total, int cus, hipStream_t s) {
     if (n_chain) hipLaunchKernelGGL(k_pinf_emit, dim3(n_chain), dim3(kLanes), 0, s, a);
-    if (a.mcap) hipLaunchKernelGGL(k_pinf_expand, dim3((a.mcap + 3) / 4), dim3(256), 0, s, a);
+    if (a.mcap)
+        hipLaunchKernelGGL(k_pinf_expand, dim3(std::min<uint32_t>(kExpandMaxBlocks, (a.mcap + 3) / 4)), dim3(256), 0, s, a);
     if (total) {
         hipLaunchKernelGGL(k_pinf_tile, dim3((uint32_t)((total + kTile - 1) / kTile)), dim3(kTileThreads), 0, s, a);
         const uint32_t tiles = (uint32_t)((total + kTile - 1) / kTile);

@@ -260,6 +260,26 @@ struct Red {
         else c_ += (x - t) + s_;
         s_ = t;
     }
+    // Knuth's TwoSum: a + b = s + e exactly (branch-free, 6 flops)
+    __device__ __forceinline__ static double two_sum(double a, double b, double &e) {
+        const double s_ = a + b, bb = s_ - a;
+        e = (a - (s_ - bb)) + (b - bb);
+        return s_;
+    }
+    // A group of elements added pairwise with every rounding error kept (TwoSum), then one compensated
+    // add: the same result class as a Neumaier step per element (e.g. [1e16, 1, -1e16, 1] sums to 2,
+    // exactly), a quarter of the dependent steps.
+    __device__ __forceinline__ static void add4(double &s_, double &c_, double x0, double x1, double x2, double x3) {
+        double e0, e1, e2;
+        const double p = two_sum(x0, x1, e0), q = two_sum(x2, x3, e1);
+        neumaier(s_, c_, two_sum(p, q, e2));
+        c_ += (e0 + e1) + e2;
+    }
+    __device__ __forceinline__ static void add2(double &s_, double &c_, double x0, double x1) {
+        double e0;
+        neumaier(s_, c_, two_sum(x0, x1, e0));
+        c_ += e0;
+    }
 
     // value only (count handled by caller for batched adds)
     template <class RankFn>

@@ -3,6 +3,7 @@
 // point fails with RDX_E_NO_DEVICE / RDX_E_DEVICE.
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
+#include <sys/prctl.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 #include <ctime>
@@ -80,10 +81,14 @@ struct Tuning {
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
     int direct_max = env_int("RDX_DIRECT_MAX", 1);                     // idle-queue fast path: callers launching at once
-    int idle_passes = env_int("RDX_DISPATCH_IDLE_PASSES", 512);        // dispatcher: empty polls before it naps
+    int idle_us = env_int("RDX_DISPATCH_IDLE_US", 30);                 // dispatcher: polling without progress before it naps
+    int nap_us = env_int("RDX_DISPATCH_NAP_US", 20);                   // ... and the nap between polls after that
+    int host_spin_us = env_int("RDX_HOST_SPIN_US", -1);                // caller's spin before it sleeps (-1: by request size)
     int pinflate = env_int("RDX_PINFLATE", 1);                         // a lone gzip / zlib stream: k_pinflate
     int pinflate_min = env_int("RDX_PINFLATE_MIN_BYTES", 1024);        // ... from this many compressed bytes
     int pinflate_prof = env_int("RDX_PINF_PROF", 0);                   // tuning: per-workgroup times to stderr
+    int pinflate_forced = env_int("RDX_PINF_MAX_FORCED", 8);           // host-forced block starts before it declines
+    int inflate_serial_max = env_int("RDX_INFLATE_SERIAL_MAX", 4096);  // declined streams up to this many bytes: k_inflate
 #if RDX_PROBES
     int epoch_start = env_int("RDX_EPOCH_START", 0);                   // tests: start workspaces' tags near the wrap
 #endif
@@ -105,6 +110,7 @@ struct DevBuf {
 struct rdx_workspace {
     int device = 0;
     int cus = 256;
+    bool inflate_fallback = false;     // rdx_context_config.inflate_fallback of the context that made it
     hipStream_t own_stream = nullptr;  // host path
     DevBuf<uint64_t> partials;   // hand-off records (tagged granules, rdx_device.hpp publish / collect)
     DevBuf<uint32_t> tickets;
@@ -154,6 +160,9 @@ struct rdx_workspace {
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
     hipEvent_t piece_ev[8] = {};
+    // a host chunk's H2D copy (a coalesced launch waits for it on the device), and the end of this
+    // workspace's work for a caller that sleeps instead of spinning (wait_event)
+    hipEvent_t copy_ev = nullptr, done_ev = nullptr;
 };
 
 namespace {
@@ -190,6 +199,7 @@ struct Job {
     KAllContig contig{};
     KAllStrided strided{};
     const uint8_t *chunk = nullptr;        // device
+    hipEvent_t dep = nullptr;              // the chunk's H2D copy (host chunks): the launch waits for it on the device
     // the heterogeneous form (k_multi), when the request fits it
     bool multi_ok = false;
     KMultiReq q{};                 // chunk / view / op; outputs are bound to the lane's slots at launch
@@ -200,6 +210,14 @@ struct Job {
     // futex word (rdx_jobsync.hpp): whoever completes the job writes `st` and the outputs, then exchanges
     // kJobDone in; after that exchange it touches no field of the Job (the caller may already have returned
     // and its stack frame be reused): a wake-up passes only the word's address to the kernel.
+    std::atomic<uint32_t> state{kJobPending};
+};
+
+// A caller that waits for an event of its own stream without spinning: the entry's dispatcher thread
+// polls the event with its lanes and wakes it (wait_event; the same one-word hand-off as a Job).
+struct Waiter {
+    hipEvent_t ev = nullptr;
+    rdx_status st = RDX_OK;
     std::atomic<uint32_t> state{kJobPending};
 };
 
@@ -214,6 +232,7 @@ struct PoolEntry {
     // the coalescer: callers append to `jobs`; one dispatcher thread per entry launches and completes them
     std::condition_variable job_cv;              // the idle dispatcher waits here for work
     std::deque<Job *> jobs;
+    std::vector<Waiter *> watch;                 // waiters handed to the dispatcher
     std::thread dispatcher;
     bool dispatcher_idle = false, stop = false;
     std::vector<Lane *> lanes;                   // dispatcher-owned
@@ -614,6 +633,7 @@ thread_local uint32_t g_inflate_path = RDX_INFLATE_PATH_NONE;
 // Returns RDX_OK with the stream's bytes in ws->raw (*raw_len of them), kNotDecoded when the sequential
 // decoder must run (an error anywhere, a chain it could not follow), or a device / memory error.
 const rdx_status kNotDecoded = static_cast<rdx_status>(254);
+constexpr uint64_t kPinfKeepSources = 256ull << 20;   // source entries kept between streams (1 GiB)
 
 rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_t *d_src, uint64_t len, hipStream_t s,
                            uint64_t *raw_len) {
@@ -663,7 +683,10 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
         // a block start no candidate covers (a fixed-Huffman block, or a header the finder's zlib-encoder
         // rules reject): decode that one block and follow the chain again
         const uint32_t n = h.n_cand;
-        if (forced >= 64 || n >= kPinfMaxCand || h.miss_type == 3) return kNotDecoded;
+        // (a stream of many fixed-Huffman blocks, Z_FIXED, would take a host round trip per block: it is
+        // declined after a few, so a decline costs little more than the finder and the block decode)
+        if (forced >= (uint32_t)std::max(0, tuning().pinflate_forced) || n >= kPinfMaxCand || h.miss_type == 3)
+            return kNotDecoded;
         const uint64_t e = h.miss_bit;
         const uint64_t key = h.miss_type == 0 ? (8 * ((e + 3 + 7) / 8)) << 2 : e << 2 | h.miss_type;
         const uint32_t n1 = n + 1;
@@ -679,10 +702,15 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
         return kNotDecoded;
     }
     const uint64_t total = h.total;
-    if ((st = ensure(ws, ws->raw, std::max<uint64_t>((total + 15) / 16 * 16, 16), s))) return st;
-    // the sources, the long-match records (at most total / kPinfLongMatch of them), the tiles' flags
+    // the output, the sources, the long-match records (at most total / kPinfLongMatch of them), the tiles'
+    // flags: about 5.5 bytes of HBM per output byte.  An allocation that fails here declines the stream (the
+    // sequential decoder needs only the output) instead of failing the request.
     const uint64_t mcap = total / kPinfLongMatch, msta = (total + 3) / 4 * 4, tiles = (total + 32767) / 32768;
-    if ((st = ensure(ws, ws->psrc, std::max<uint64_t>(msta + 4 * mcap + tiles, 1), s))) return st;
+    if ((st = ensure(ws, ws->raw, std::max<uint64_t>((total + 15) / 16 * 16, 16), s)) ||
+        (st = ensure(ws, ws->psrc, std::max<uint64_t>(msta + 4 * mcap + tiles, 1), s))) {
+        (void)hipGetLastError();
+        return st == RDX_E_OUT_OF_MEMORY ? kNotDecoded : st;
+    }
     a.src = ws->psrc.p;
     a.mlist = reinterpret_cast<uint4 *>(ws->psrc.p + msta);
     a.mcap = (uint32_t)mcap;
@@ -748,6 +776,12 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
                      "\"survivors\": %llu, \"max_wg\": %u, \"t_staged\": %.1f, \"t_headers\": %.1f, "
                      "\"wg_survivors\": %llu}\n", n, (hi - lo) / 100.0, worst / 100.0, (unsigned long long)surv, wi,
                      us(w[1]), us(w[2]), (unsigned long long)w[4]);
+    }
+    // the sources of an unusually large stream are not kept at their high-water size
+    if (ws->psrc.cap > kPinfKeepSources) {
+        RDX_HIP(hipFree(ws->psrc.p));
+        ws->psrc.p = nullptr;
+        ws->psrc.cap = 0;
     }
     if (!h.final_ok) {
         if (tuning().pinflate_prof)   // tuning / diagnosis: why the parallel path declined
@@ -860,6 +894,14 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
             return RDX_OK;
         }
         if (st != kNotDecoded) return st;
+        // declined (an error anywhere, a chain it cannot follow, memory): the sequential k_inflate takes
+        // 100-220 ms per 4 MiB where one host core's zlib takes 3.5-10 ms, so unless the context asks for the
+        // device's own answer (inflate_fallback) a stream past a few KiB goes back to the caller, whose
+        // host decoder gives the reference's bytes or error (integration/app_gpu.rs)
+        if (!ws->inflate_fallback && len > (uint64_t)std::max(0, tuning().inflate_serial_max)) {
+            g_inflate_path = RDX_INFLATE_PATH_DECLINED;
+            return unsupported(RDX_UNSUPPORTED_INFLATE_DECLINED);
+        }
         g_inflate_path = RDX_INFLATE_PATH_PARALLEL_FALLBACK;
     }
     if ((st = ensure(ws, ws->zout_len, 1, s))) return st;
@@ -895,11 +937,12 @@ rdx_status decompress_request(rdx_workspace *ws, const rdx_request &req, const u
     }
 }
 
-rdx_status create_workspace(int device, rdx_workspace **out) {
+rdx_status create_workspace(int device, rdx_workspace **out, bool inflate_fallback) {
     RDX_HIP(hipSetDevice(device));
     auto *ws = new (std::nothrow) rdx_workspace();
     if (!ws) return RDX_E_OUT_OF_MEMORY;
     ws->device = device;
+    ws->inflate_fallback = inflate_fallback;
 #if RDX_PROBES
     if (tuning().epoch_start > 0) ws->epoch = (uint32_t)std::min(tuning().epoch_start, 0xffff);
 #endif
@@ -908,6 +951,8 @@ rdx_status create_workspace(int device, rdx_workspace **out) {
         ws->cus = prop.multiProcessorCount;
     hipError_t e = hipStreamCreateWithFlags(&ws->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ws->upload_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ws->copy_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ws->done_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         delete ws;
         return map_err(e);
@@ -963,6 +1008,8 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->cbor_rec.p);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
+    if (ws->copy_ev) (void)hipEventDestroy(ws->copy_ev);
+    if (ws->done_ev) (void)hipEventDestroy(ws->done_ev);
     if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
     delete ws;
 }
@@ -1379,7 +1426,7 @@ void rdx_host_free(rdx_context *ctx, void *p) {
 
 rdx_status rdx_workspace_create(rdx_context *ctx, int device, rdx_workspace **out) {
     if (!ctx || !out) return RDX_E_INVALID_ARGUMENT;
-    return create_workspace(device, out);
+    return create_workspace(device, out, ctx->cfg.inflate_fallback != 0);
 }
 
 void rdx_workspace_destroy(rdx_workspace *ws) { destroy_workspace(ws); }
@@ -1631,7 +1678,7 @@ rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease, bool wait 
     ++e.creating;   // counts against the cap while it is created outside the lock
     lk.unlock();
     rdx_workspace *ws = nullptr;
-    const rdx_status st = create_workspace(e.device, &ws);
+    const rdx_status st = create_workspace(e.device, &ws, ctx->cfg.inflate_fallback != 0);
     lk.lock();
     --e.creating;
     if (st) {
@@ -1663,7 +1710,7 @@ rdx_status create_lane(int device, Lane **out, Lane *share = nullptr) {
         L->ws = share->ws;
         L->owns_ws = false;
     } else {
-        st = create_workspace(device, &L->ws);
+        st = create_workspace(device, &L->ws, false);
     }
     if (!st) {
         // fine-grained (coherent): the kernel's system-scope stores land in host memory directly
@@ -1697,6 +1744,9 @@ rdx_status launch_lane(Lane &L) {
     }
     rdx_status st;
     const hipStream_t s = ws->own_stream;
+    // host chunks: the launch waits on the device for their H2D copies (no host synchronisation)
+    for (uint32_t i = 0; i < L.n; ++i)
+        if (L.batch[i]->dep) RDX_HIP(hipStreamWaitEvent(s, L.batch[i]->dep, 0));
     if (L.group) {   // one plan, the chunks in the kernel arguments, chunk i's result into slot i
         const Job &j0 = *L.batch[0];
         KOut out{};
@@ -1834,20 +1884,29 @@ void form_batch(std::deque<Job *> &pending, Lane &L) {
 // it sleeps on job_cv.
 void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
     (void)hipSetDevice(e->device);
+    // this thread's naps: microseconds, not the default 50 us timer slack
+    (void)prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0);
     std::deque<Job *> pending;
-    uint32_t in_flight = 0, idle = 0;
+    std::vector<Waiter *> watched;
+    uint32_t in_flight = 0;
+    auto last_progress = std::chrono::steady_clock::now();
     for (;;) {
         {
             std::unique_lock<std::mutex> lk(e->mu);
-            if (pending.empty() && in_flight == 0) {
+            if (pending.empty() && in_flight == 0 && watched.empty()) {
                 e->dispatcher_idle = true;
-                e->job_cv.wait(lk, [&] { return !e->jobs.empty() || e->stop; });
+                e->job_cv.wait(lk, [&] { return !e->jobs.empty() || !e->watch.empty() || e->stop; });
                 e->dispatcher_idle = false;
-                if (e->jobs.empty() && e->stop) return;
+                if (e->jobs.empty() && e->watch.empty() && e->stop) return;
+                last_progress = std::chrono::steady_clock::now();
             }
             while (!e->jobs.empty()) {
                 pending.push_back(e->jobs.front());
                 e->jobs.pop_front();
+            }
+            if (!e->watch.empty()) {
+                watched.insert(watched.end(), e->watch.begin(), e->watch.end());
+                e->watch.clear();
             }
         }
         bool progressed = false;
@@ -1913,17 +1972,85 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
             }
             if (l->remaining != before) progressed = true;
         }
-        // nothing arrived and nothing completed: yield, and after RDX_DISPATCH_IDLE_PASSES such passes in a
-        // row (a long launch in flight) nap between polls instead of keeping a core busy
+        // callers sleeping on an event of their own stream (wait_event): wake each one whose event completed
+        // (the exchange in job_finish is the last access to its Waiter)
+        for (size_t i = 0; i < watched.size();) {
+            Waiter *w = watched[i];
+            const hipError_t q = hipEventQuery(w->ev);
+            if (q == hipErrorNotReady) {
+                ++i;
+                continue;
+            }
+            watched[i] = watched.back();
+            watched.pop_back();
+            w->st = q == hipSuccess ? RDX_OK : map_err(q);
+            job_finish(w->state);
+            progressed = true;
+        }
+        // nothing arrived and nothing completed: yield for RDX_DISPATCH_IDLE_US, then (a long launch or copy
+        // in flight) nap RDX_DISPATCH_NAP_US between polls instead of keeping a core busy
+        const auto now = std::chrono::steady_clock::now();
         if (progressed) {
-            idle = 0;
-        } else if (++idle < (uint32_t)tuning().idle_passes) {
+            last_progress = now;
+        } else if (std::chrono::duration<double, std::micro>(now - last_progress).count() < tuning().idle_us) {
             std::this_thread::yield();
         } else {
-            const timespec ts{0, 20000};
+            const timespec ts{0, 1000L * std::max(1, tuning().nap_us)};
             nanosleep(&ts, nullptr);
         }
     }
+}
+
+// The entry's dispatcher thread, started on first use (with e.mu held).
+bool ensure_dispatcher(rdx_context *ctx, PoolEntry &e) {
+    if (e.dispatcher.joinable()) return true;
+    try {
+        e.dispatcher = std::thread(dispatcher_loop, ctx, &e);
+    } catch (...) {
+        return false;
+    }
+    return true;
+}
+
+// How long a caller spins for its own result before it sleeps (RDX_HOST_SPIN_US overrides): the time an
+// idle device needs for the request (its PCIe bytes at >= 40 GB/s, its HBM bytes, a launch), so that a lone
+// request is not slowed by a sleep / wake-up; only a short spin when other requests are in flight on the
+// entry (this one queues behind them: the link or the device is busy, and the caller's core is worth
+// more to the server's other threads than the microseconds a wake-up costs).
+double spin_budget_us(const PoolEntry &e, uint64_t own_weight, uint64_t pcie_bytes, uint64_t hbm_bytes) {
+    if (tuning().host_spin_us >= 0) return tuning().host_spin_us;
+    if (e.outstanding.load(std::memory_order_relaxed) > own_weight + own_weight / 2) return 2.0;
+    return 20.0 + (double)pcie_bytes / 40e3 + (double)hbm_bytes / 4e6;
+}
+
+// Wait for `ev` (recorded on a stream the caller owns): spin on it for `budget_us`, then sleep until the
+// entry's dispatcher sees it complete.  HIP's own waits (hipStreamSynchronize / hipEventSynchronize, also
+// with hipEventBlockingSync) spin for as long as the work takes (profiles/r05_wait_probe.jsonl).
+rdx_status wait_event(rdx_context *ctx, PoolEntry &e, hipEvent_t ev, double budget_us) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return RDX_OK;
+        if (q != hipErrorNotReady) return map_err(q);
+        if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >= budget_us) break;
+        for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
+    }
+    Waiter w;
+    w.ev = ev;
+    {
+        std::lock_guard<std::mutex> g(e.mu);
+        if (!ensure_dispatcher(ctx, e)) return RDX_E_OUT_OF_MEMORY;
+        e.watch.push_back(&w);
+        if (e.dispatcher_idle) e.job_cv.notify_one();
+    }
+    job_wait(w.state, 0);
+    return w.st;
+}
+
+// The end of everything queued on the workspace's stream so far (wait_event).
+rdx_status wait_stream(rdx_context *ctx, PoolEntry &e, rdx_workspace *ws, double budget_us) {
+    RDX_HIP(hipEventRecord(ws->done_ev, ws->own_stream));
+    return wait_event(ctx, e, ws->done_ev, budget_us);
 }
 
 // The idle-queue fast path: a coalescible request arriving while its entry's coalescer has nothing queued
@@ -1945,7 +2072,7 @@ void release_direct(PoolEntry &e, bool served) {
     if (served) ++e.direct;
 }
 
-rdx_status run_direct(rdx_workspace *ws, Job &job) {
+rdx_status run_direct(rdx_context *ctx, PoolEntry &e, rdx_workspace *ws, Job &job, double budget_us) {
     RDX_HIP(hipSetDevice(ws->device));
     constexpr size_t slot_bytes = kTableChunks * kSlotWords * sizeof(uint64_t);
     if (!ws->h_slot) {
@@ -1964,13 +2091,19 @@ rdx_status run_direct(rdx_workspace *ws, Job &job) {
     rdx_status st = launch_lane(L);
     if (st) return st;
     // the slot's tag arrives with the fold; the stream query (every 64th poll) catches a launch that ended
-    // without writing it (a device fault: RDX_E_DEVICE)
+    // without writing it (a device fault: RDX_E_DEVICE).  Past the spin budget the caller sleeps until
+    // the launch has ended (wait_event), then reads its slot.
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t polls = 1;; ++polls) {
         const bool kernel_done = polls % 64 == 0 && hipStreamQuery(ws->own_stream) != hipErrorNotReady;
-        if (poll_lane(L, kernel_done)) break;
-        if (polls < 4096) __builtin_ia32_pause();
-        else std::this_thread::yield();
+        if (poll_lane(L, kernel_done)) return job.st;
+        if (polls % 16 == 0 &&
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >= budget_us)
+            break;
+        __builtin_ia32_pause();
     }
+    if ((st = wait_stream(ctx, e, ws, 0.0))) return st;
+    poll_lane(L, true);   // the slot was written before the launch ended, or the request fails: RDX_E_DEVICE
     return job.st;
 }
 
@@ -1979,13 +2112,7 @@ rdx_status run_direct(rdx_workspace *ws, Job &job) {
 rdx_status coalesce(rdx_context *ctx, PoolEntry &e, Job &job) {
     {
         std::lock_guard<std::mutex> g(e.mu);
-        if (!e.dispatcher.joinable()) {
-            try {
-                e.dispatcher = std::thread(dispatcher_loop, ctx, &e);
-            } catch (...) {
-                return RDX_E_OUT_OF_MEMORY;
-            }
-        }
+        if (!ensure_dispatcher(ctx, e)) return RDX_E_OUT_OF_MEMORY;
         e.jobs.push_back(&job);
         if (e.dispatcher_idle) e.job_cv.notify_one();
     }
@@ -2068,7 +2195,7 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             if (claim_direct(entry)) {
                 WsLease lease;
                 if (acquire_ws(ctx, entry, lease, false) == RDX_OK) {
-                    st = run_direct(lease.ws, job);
+                    st = run_direct(ctx, entry, lease.ws, job, spin_budget_us(entry, pl.weight, 0, chunk_len));
                     release_direct(entry, true);
                     return st;
                 }
@@ -2098,11 +2225,13 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             Job job;
             if (coalescible(src, job)) {
                 if (claim_direct(entry)) {   // launched behind the copy on the same stream
-                    r = run_direct(ws, job);
+                    r = run_direct(ctx, entry, ws, job, spin_budget_us(entry, pl.weight, chunk_len, chunk_len));
                     release_direct(entry, true);
                     return r;
                 }
-                RDX_HIP(hipStreamSynchronize(s));   // the chunk is in HBM once the copy completes
+                // the coalesced launch waits for the copy on the device; this thread does not
+                RDX_HIP(hipEventRecord(ws->copy_ev, s));
+                job.dep = ws->copy_ev;
                 return coalesce(ctx, entry, job);
             }
         }
@@ -2145,11 +2274,12 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             RDX_HIP(hipMemcpyAsync(&n, ws->cbor_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
             RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             if (bound <= kCborOneTrip) RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, bound, hipMemcpyDeviceToHost, s));
-            RDX_HIP(hipStreamSynchronize(s));
+            if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, resident ? 0 : chunk_len, len))))
+                return r;
             if (status) return (rdx_status)status;
             if (bound > kCborOneTrip) {
                 RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, n, hipMemcpyDeviceToHost, s));
-                RDX_HIP(hipStreamSynchronize(s));
+                if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, n, 0)))) return r;
             }
             cb->len = n;
             return RDX_OK;
@@ -2158,7 +2288,9 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
         if (p.info.n_counts)
             RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
         RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        RDX_HIP(hipStreamSynchronize(s));
+        const uint64_t d2h = p.info.body_bytes + p.info.n_counts * sizeof(int64_t);
+        if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, (resident ? 0 : chunk_len) + d2h, len))))
+            return r;
         if (status) return (rdx_status)status;
         return RDX_OK;
     };
@@ -2357,7 +2489,7 @@ rdx_status rdx_execute_resident(rdx_context *ctx, int device, const rdx_request 
 }
 
 rdx_status rdx_context_configure(rdx_context *ctx, const rdx_context_config *cfg) {
-    if (!ctx || !cfg || cfg->coalesce > 1) return RDX_E_INVALID_ARGUMENT;
+    if (!ctx || !cfg || cfg->coalesce > 1 || cfg->inflate_fallback > 1) return RDX_E_INVALID_ARGUMENT;
     // the dispatchers, the placement and acquire_ws read the configuration without a lock: it is frozen
     // once the first request has been placed (rdx.h: configure before the context is shared)
     if (ctx->served.load(std::memory_order_relaxed)) return RDX_E_INVALID_ARGUMENT;

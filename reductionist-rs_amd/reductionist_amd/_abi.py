@@ -14,7 +14,7 @@ REPO_ROOT = PKG_ROOT.parent
 # RDX_LIB_PATH: an alternative in-tree build of the same library (A/B tuning measurements only)
 LIB_PATH = Path(os.environ.get("RDX_LIB_PATH", str(PKG_ROOT / "librdx.so")))
 
-RDX_ABI_VERSION = 1
+RDX_ABI_VERSION = 2
 RDX_MAX_NDIM = 32
 
 # rdx_status
@@ -30,7 +30,11 @@ INFLATE_OK, INFLATE_GZIP_HEADER, INFLATE_ZLIB_METHOD, INFLATE_ZLIB_HEADER, INFLA
 
 # rdx_unsupported_reason (cause of E_UNSUPPORTED)
 UNSUPPORTED_NONE, UNSUPPORTED_BLOSC2_CODEC, UNSUPPORTED_RANK, UNSUPPORTED_VIEW_SIZE, UNSUPPORTED_VIEW_DIMS, \
-    UNSUPPORTED_MISSING_LIST, UNSUPPORTED_CBOR_SIZE = range(7)
+    UNSUPPORTED_MISSING_LIST, UNSUPPORTED_CBOR_SIZE, UNSUPPORTED_INFLATE_DECLINED = range(8)
+
+# rdx_inflate_path (rdx_inflate_last_path)
+INFLATE_PATH_NONE, INFLATE_PATH_SERIAL, INFLATE_PATH_PARALLEL, INFLATE_PATH_PARALLEL_FALLBACK, \
+    INFLATE_PATH_DECLINED = range(5)
 
 OPS = {"count": 0, "max": 1, "min": 2, "select": 3, "sum": 4}
 DTYPES = {"int32": 0, "int64": 1, "uint32": 2, "uint64": 3, "float32": 4, "float64": 5}
@@ -93,7 +97,7 @@ class rdx_result(C.Structure):
 
 class rdx_context_config(C.Structure):
     _fields_ = [("max_workspaces", C.c_uint32), ("coalesce", C.c_uint32), ("coalesce_lanes", C.c_uint32),
-                ("reserved", C.c_uint32), ("coalesce_max_bytes", C.c_uint64),
+                ("inflate_fallback", C.c_uint32), ("coalesce_max_bytes", C.c_uint64),
                 ("coalesce_host_max_bytes", C.c_uint64)]
 
 

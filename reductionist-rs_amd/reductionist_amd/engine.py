@@ -107,10 +107,10 @@ class Engine:
         return st, info, bytes(body)[: info.body_bytes], [int(c) for c in counts[: info.n_counts]]
 
     def configure(self, max_workspaces=0, coalesce=True, coalesce_lanes=0, coalesce_max_bytes=0,
-                  coalesce_host_max_bytes=0):
+                  coalesce_host_max_bytes=0, inflate_fallback=False):
         """rdx_context_configure (0 = the engine's default for that field)."""
-        cfg = _abi.rdx_context_config(max_workspaces, 1 if coalesce else 0, coalesce_lanes, 0, coalesce_max_bytes,
-                                      coalesce_host_max_bytes)
+        cfg = _abi.rdx_context_config(max_workspaces, 1 if coalesce else 0, coalesce_lanes,
+                                      1 if inflate_fallback else 0, coalesce_max_bytes, coalesce_host_max_bytes)
         check(self.lib.rdx_context_configure(self.ctx, C.byref(cfg)))
 
     def stats(self, index: int = 0) -> dict:
@@ -187,13 +187,19 @@ class Workspace:
     def decompress_one_device(self, compression: str, d_in: int, length: int, d_out: int, out_capacity: int,
                               stream: int | None = None):
         """rdx_decompress_one_device: one device-resident gzip / zlib stream decoded by the whole device
-        (k_pinflate, or k_inflate for a stream it declines), synchronously.  Returns (rdx_inflate_error,
-        decompressed size, rdx_inflate_last_path)."""
+        (k_pinflate; a stream it declines: k_inflate when the context has inflate_fallback on), synchronously.
+        Returns (rdx_inflate_error, decompressed size, rdx_inflate_last_path); the error is None when the
+        stream was declined (RDX_UNSUPPORTED_INFLATE_DECLINED)."""
         n = C.c_uint64()
         err = C.c_uint32()
-        check(self.lib.rdx_decompress_one_device(self.ws, _abi.COMPRESSION[compression], C.c_void_p(d_in), length,
-                                                 C.c_void_p(d_out), out_capacity, C.byref(n), C.byref(err),
-                                                 C.c_void_p(stream or 0)))
+        st = self.lib.rdx_decompress_one_device(self.ws, _abi.COMPRESSION[compression], C.c_void_p(d_in), length,
+                                                C.c_void_p(d_out), out_capacity, C.byref(n), C.byref(err),
+                                                C.c_void_p(stream or 0))
+        if st == _abi.E_UNSUPPORTED and self.lib.rdx_last_unsupported_reason() == _abi.UNSUPPORTED_INFLATE_DECLINED:
+            # declined by k_pinflate (the workspace's context has inflate_fallback off): no error detail, the
+            # caller's host decoder answers
+            return None, 0, int(self.lib.rdx_inflate_last_path())
+        check(st)
         return int(err.value), int(n.value), int(self.lib.rdx_inflate_last_path())
 
     def decompress_batch_device(self, compression: str, d_streams: Sequence[int], lens: Sequence[int], d_out: int,

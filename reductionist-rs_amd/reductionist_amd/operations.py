@@ -12,8 +12,13 @@ from __future__ import annotations
 
 import threading
 
+import dataclasses
+import gzip
+import zlib
+
 from . import _abi
 from .engine import Engine
+from .errors import Decompression, Unsupported
 from .models import RequestData, Response, to_c_request
 
 _ENGINE = None
@@ -35,7 +40,16 @@ class Operation:
     def execute(cls, request_data: RequestData, data: bytes, engine: Engine | None = None) -> Response:
         eng = engine or default_engine()
         creq = to_c_request(request_data, cls.name)
-        info, body, counts = eng.execute(creq, data)
+        try:
+            info, body, counts = eng.execute(creq, data)
+        except Unsupported:
+            # a lone gzip / zlib stream the device's parallel decoder declined (rdx.h
+            # RDX_UNSUPPORTED_INFLATE_DECLINED): the host decodes it, as integration/app_gpu.rs does, and the
+            # uncompressed chunk runs on the device
+            if _abi.lib().rdx_last_unsupported_reason() != _abi.UNSUPPORTED_INFLATE_DECLINED:
+                raise
+            rd = dataclasses.replace(request_data, compression=None, size=None)
+            info, body, counts = eng.execute(to_c_request(rd, cls.name), host_decompress(request_data.compression, data))
         return Response(body=body, dtype=_abi.DTYPE_NAMES[info.dtype], shape=info.shape_list(), count=counts,
                         option_shape_as_bytes=bool(request_data.option_shape_as_bytes),
                         option_count_as_bytes=bool(request_data.option_count_as_bytes))
@@ -62,6 +76,21 @@ class Sum(Operation):
 
 
 OPERATIONS = {"count": Count, "max": Max, "min": Min, "select": Select, "sum": Sum}
+
+
+def host_decompress(compression: str, data: bytes) -> bytes:
+    """compression::decompress (src/compression.rs:60-82) on the host, for a stream the device declined:
+    one gzip member (trailing bytes ignored, as flate2's GzDecoder) or one zlib stream."""
+    try:
+        if compression == "gzip":
+            d = zlib.decompressobj(16 + zlib.MAX_WBITS)
+            out = d.decompress(data)
+            if not d.eof:
+                raise zlib.error("unexpected end of compressed data")
+            return out
+        return zlib.decompress(data)
+    except (zlib.error, gzip.BadGzipFile, EOFError) as e:
+        raise Decompression(str(e), _abi.E_DECOMPRESSION) from None
 
 
 def operation(op: type[Operation], request_data: RequestData, data: bytes, engine: Engine | None = None) -> Response:

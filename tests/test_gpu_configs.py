@@ -269,3 +269,32 @@ def test_subnormal_inf_mix(engine, dtype, op, r):
                 continue
             for o in range(len(exact)):
                 assert _sum_ok(dtype, float(g[o]), float(c[o]), exact[o]), (o, g[o], c[o], exact[o], req)
+
+
+# ---- f64 sums with heavy cancellation (the group sums' compensation) -------------------
+@pytest.mark.parametrize("shuffled", [False, True])
+@pytest.mark.parametrize("big_endian", [False, True])
+def test_f64_sum_cancellation(engine, shuffled, big_endian):
+    """f64 sums whose terms cancel.  (1) [1e16, 1, -1e16, 1] repeated: every group of four sums to exactly
+    2, which a plain pairwise add inside the group loses entirely (the reference's sequential fold keeps
+    one of the two 1s per group): the device's compensated sum (TwoSum inside each group, Neumaier across)
+    gives the exact total.  (2) random ±1e15 pairs plus [0, 1) noise: within the bar."""
+    n = 1 << 20
+    rng = np.random.default_rng(0x5EEDCA11 + 2 * shuffled + big_endian)
+    big = rng.standard_normal(n // 2) * 1e15
+    noisy = np.stack([big, -big], axis=1).reshape(-1) + rng.random(n)
+    for case, v in (("pattern", np.tile(np.array([1e16, 1.0, -1e16, 1.0]), n // 4)), ("noisy", noisy)):
+        raw = v.astype(">f8" if big_endian else "<f8").tobytes()
+        req = {"dtype": "float64", "byte_order": "big" if big_endian else "little"}
+        if shuffled:
+            raw = np.frombuffer(raw, np.uint8).reshape(n, 8).T.copy().tobytes()
+            req["filters"] = [{"id": "shuffle", "element_size": 8}]
+        creq = make_request("sum", req, oracle.convert)
+        st, info, body, counts = engine.execute_raw(creq, raw)
+        ost, _, obody, ocounts = oracle.execute(creq, raw, body_cap=64, counts_cap=8)
+        assert st == ost == 0 and counts == ocounts == [n]
+        gpu, cpu = struct.unpack("<d", body)[0], struct.unpack("<d", obody)[0]
+        exact = math.fsum(v)
+        assert _sum_ok("float64", gpu, cpu, exact), (case, gpu, cpu, exact)
+        if case == "pattern":
+            assert exact == n // 2 and gpu == exact, (gpu, cpu, exact)

@@ -131,3 +131,27 @@ def test_operation_with_compression_and_filters():
     creq = _abi.CRequest("sum", "int32", compression="blosc2")
     st, *_ = oracle.execute(creq, b"\0" * 64)
     assert st == _abi.E_DECOMPRESSION and oracle.lib().oracle_inflate_last_error() == _abi.BLOSC2_INVALID
+
+
+def test_oracle_decodes_gnu_gzip_members():
+    """A second encoder pins the oracle: members written by GNU gzip 1.10 (its own deflate, not zlib;
+    tests/golden/make_gnu_gzip.py) decode to the inputs' bytes (SHA-256 in the manifest), as CPython's
+    zlib decodes them."""
+    import hashlib
+    import json
+    from pathlib import Path
+    d = Path(__file__).resolve().parent / "golden" / "gnu_gzip"
+    man = json.loads((d / "manifest.json").read_text())
+    for m in man["members"]:
+        s = (d / m["file"]).read_bytes()
+        err, out = oracle.decompress(GZIP, s, m["raw_bytes"] + 64)
+        assert err == 0 and len(out) == m["raw_bytes"], m["file"]
+        assert hashlib.sha256(out).hexdigest() == m["sha256"] == hashlib.sha256(zlib.decompress(s, 31)).hexdigest()
+    # the inputs regenerate bit for bit from the committed script
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_gnu_gzip", d.parent / "make_gnu_gzip.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    ins = mod.inputs()
+    for m in man["members"]:
+        assert hashlib.sha256(ins[m["input"]]).hexdigest() == m["sha256"]

@@ -161,9 +161,10 @@ def test_shim_error_details_match_the_reference():
     assert "FromBytes { type_name: type_name_of(dtype) }" in ops
     for t in ("i32", "i64", "u32", "u64", "f32", "f64"):
         assert f"std::any::type_name::<{t}>()" in ops
-    # RDX_E_UNSUPPORTED: only the blosc2-codec reason becomes UnsupportedOperation (host decompression);
-    # the others run the reference's own operation::<T> on the CPU, in both plugin entry points
-    assert "rdx_last_unsupported_reason() } != unsupported::BLOSC2_CODEC" in ops
+    # RDX_E_UNSUPPORTED: only the chunk-encoding reasons (a blosc2 codec, a gzip / zlib stream k_pinflate
+    # declined) become UnsupportedOperation (host decompression); the others run the reference's own
+    # operation::<T> on the CPU, in both plugin entry points
+    assert "unsupported::BLOSC2_CODEC | unsupported::INFLATE_DECLINED" in ops
     assert ops.count("if planned_on_cpu(st)") == 2
     for op in ("Count", "Max", "Min", "Select", "Sum"):
         assert f"crate::app::operation::<operations::{op}>(rd, data)" in ops
