@@ -189,6 +189,8 @@ pub struct RdxDeviceStats {
     pub direct_requests: u64,
     pub placed_bytes: u64,
     pub peak_outstanding_bytes: u64,
+    pub host_read_requests: u64,
+    pub sleeps: u64,
 }
 
 pub enum RdxContext {}
@@ -349,7 +351,7 @@ const _: () = assert!(size_of::<RdxResponseInfo>() == 280);
 const _: () = assert!(size_of::<RdxMultiItem>() == 48);
 const _: () = assert!(size_of::<RdxResult>() == 312);
 const _: () = assert!(size_of::<RdxContextConfig>() == 32);
-const _: () = assert!(size_of::<RdxDeviceStats>() == 80);
+const _: () = assert!(size_of::<RdxDeviceStats>() == 96);
 const _: () = assert!(offset_of!(RdxContextConfig, coalesce_max_bytes) == 16);
 const _: () = assert!(offset_of!(RdxDeviceStats, requests) == 16);
 const _: () = assert!(offset_of!(RdxRequest, op) == 4);

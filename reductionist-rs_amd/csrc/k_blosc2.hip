@@ -36,7 +36,7 @@ namespace rdx {
 namespace {
 
 constexpr uint32_t kWaves = 4;
-constexpr uint32_t kRing = 8192, kRingMask = kRing - 1, kFlush = kRing / 4;
+constexpr uint32_t kRing = 8192;
 constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4, kStage = 1024;
 constexpr uint32_t kUnit = 4096;   // memcpy'ed / special chunks: bytes per work item
 

@@ -3,6 +3,7 @@
 // point fails with RDX_E_NO_DEVICE / RDX_E_DEVICE.
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
+#include <pthread.h>
 #include <sys/prctl.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -84,6 +85,9 @@ struct Tuning {
     int idle_us = env_int("RDX_DISPATCH_IDLE_US", 30);                 // dispatcher: polling without progress before it naps
     int nap_us = env_int("RDX_DISPATCH_NAP_US", 20);                   // ... and the nap between polls after that
     int host_spin_us = env_int("RDX_HOST_SPIN_US", -1);                // caller's spin before it sleeps (-1: by request size)
+    int host_read_kib = env_int("RDX_HOST_READ_KIB", 4096);            // pinned chunks up to this: the kernel reads them over PCIe
+    int host_read_wgs = env_int("RDX_HOST_READ_WGS", 8);               // ... with this many workgroups (few: profiles/r05_hread_probe)
+    int phases = env_int("RDX_PHASES", 0);                             // phase statistics of the direct path (stderr at destroy)
     int pinflate = env_int("RDX_PINFLATE", 1);                         // a lone gzip / zlib stream: k_pinflate
     int pinflate_min = env_int("RDX_PINFLATE_MIN_BYTES", 1024);        // ... from this many compressed bytes
     int pinflate_prof = env_int("RDX_PINF_PROF", 0);                   // tuning: per-workgroup times to stderr
@@ -147,6 +151,10 @@ struct rdx_workspace {
     DevBuf<uint8_t> cbor;
     DevBuf<uint64_t> cbor_len;
     uint64_t *zback = nullptr;  // pinned: [0] = out_len, [1] = err
+    // page-locked readback of a host-path request: [0] status, [1] CBOR length, then small responses
+    // (a D2H copy into pageable memory — a stack word, a caller's std::vector — is a synchronous, spinning
+    // copy in HIP; into this block it is a DMA the caller can sleep through)
+    uint64_t *h_back = nullptr;
     // the coalescer's idle-queue fast path: this workspace's own page-locked result slots (a one-request
     // lane launched on the caller's thread; rdx_device.hpp put_host_slot)
     uint64_t *h_slot = nullptr;
@@ -163,6 +171,7 @@ struct rdx_workspace {
     // a host chunk's H2D copy (a coalesced launch waits for it on the device), and the end of this
     // workspace's work for a caller that sleeps instead of spinning (wait_event)
     hipEvent_t copy_ev = nullptr, done_ev = nullptr;
+    hipEvent_t ph_ev[3] = {};   // RDX_PHASES: timing events around the copy and the kernel
 };
 
 namespace {
@@ -184,6 +193,7 @@ struct Lane {
     uint32_t remaining = 0;                  // of which not yet seen
     uint32_t tag = 0;                        // the launch's epoch (its slots' tag)
     uint32_t polls = 0;
+    hipEvent_t done = nullptr;               // recorded behind each launch: its end (the fault fallback's test)
     std::chrono::steady_clock::time_point t0;   // when the launch was issued (dispatch statistics)
 };
 
@@ -200,6 +210,7 @@ struct Job {
     KAllStrided strided{};
     const uint8_t *chunk = nullptr;        // device
     hipEvent_t dep = nullptr;              // the chunk's H2D copy (host chunks): the launch waits for it on the device
+    bool host_read = false;                // `chunk` is page-locked host memory the kernel reads over PCIe
     // the heterogeneous form (k_multi), when the request fits it
     bool multi_ok = false;
     KMultiReq q{};                 // chunk / view / op; outputs are bound to the lane's slots at launch
@@ -245,6 +256,8 @@ struct PoolEntry {
     uint64_t direct = 0;                         // requests served by the fast path
     uint64_t placed_bytes = 0;                   // chunk bytes placed here, cumulative
     uint64_t peak_outstanding = 0;               // high-water mark of `outstanding`
+    uint64_t host_reads = 0;                     // direct requests whose kernel read the host chunk itself
+    std::atomic<uint64_t> sleeps{0};             // callers that slept in wait_event
 };
 
 }  // namespace
@@ -1000,6 +1013,7 @@ void destroy_workspace(rdx_workspace *ws) {
     for (hipEvent_t e : ws->piece_ev)
         if (e) (void)hipEventDestroy(e);
     if (ws->zback) (void)hipHostFree(ws->zback);
+    if (ws->h_back) (void)hipHostFree(ws->h_back);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->pinf_back) (void)hipHostFree(ws->pinf_back);
     fr(ws->pinf.p);
@@ -1009,6 +1023,8 @@ void destroy_workspace(rdx_workspace *ws) {
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
     if (ws->copy_ev) (void)hipEventDestroy(ws->copy_ev);
+    for (hipEvent_t e : ws->ph_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ws->done_ev) (void)hipEventDestroy(ws->done_ev);
     if (ws->own_stream) (void)hipStreamDestroy(ws->own_stream);
     delete ws;
@@ -1134,6 +1150,66 @@ bool is_pinned(const void *p) {
         return false;
     }
     return a.type == hipMemoryTypeHost;
+}
+
+// The device address of a page-locked host range (hipHostMalloc / rdx_host_alloc / hipHostRegister), or
+// null for pageable memory.
+const uint8_t *host_alias(const void *p) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost) return nullptr;
+    return static_cast<const uint8_t *>(a.devicePointer ? a.devicePointer : p);
+}
+
+// RDX_PHASES=1: where a direct request's time goes (the idle-entry path a lone host request takes),
+// summed over requests and printed as one JSON line per path when the context is destroyed.
+struct PhaseSums {
+    std::mutex mu;
+    uint64_t n[3] = {};
+    double sum[3][8] = {};   // [path][phase]: see print_phases
+};
+PhaseSums &phase_sums() {
+    static PhaseSums p;
+    return p;
+}
+void phase_add(int path, const double *v) {
+    PhaseSums &P = phase_sums();
+    std::lock_guard<std::mutex> g(P.mu);
+    for (int k = 0; k < 8; ++k) P.sum[path][k] += v[k];
+    ++P.n[path];
+}
+void print_phases() {
+    PhaseSums &p = phase_sums();
+    std::lock_guard<std::mutex> g(p.mu);
+    static const char *const paths[3] = {"host_read", "dma_copy", "coalesced_host"};
+    static const char *const fields[3][8] = {
+        {"plan_place_lease_us", "copy_issue_us", "launch_issue_us", "issue_to_result_seen_us", "result_to_return_us",
+         "total_us", "device_copy_us", "device_kernel_us"},
+        {"plan_place_lease_us", "copy_issue_us", "launch_issue_us", "issue_to_result_seen_us", "result_to_return_us",
+         "total_us", "device_copy_us", "device_kernel_us"},
+        {"plan_place_lease_us", "copy_issue_us", "queued_to_woken_us", "total_us", "plan_place_lease_cpu_us",
+         "copy_issue_cpu_us", "queued_to_woken_cpu_us", "total_cpu_us"}};
+    for (int k = 0; k < 3; ++k) {
+        if (!p.n[k]) continue;
+        const double n = (double)p.n[k];
+        std::string line = std::string("{\"rdx_phases\": {\"path\": \"") + paths[k] + "\", \"requests\": " +
+                           std::to_string(p.n[k]);
+        for (int f = 0; f < 8; ++f) {
+            char b[96];
+            std::snprintf(b, sizeof b, ", \"%s\": %.2f", fields[k][f], p.sum[k][f] / n);
+            line += b;
+        }
+        std::fprintf(stderr, "%s}}\n", line.c_str());
+    }
+}
+double thread_cpu_us() {
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
 }
 
 // Select / axis=[] (Mode::Map) from page-locked host memory into page-locked host memory, pipelined:
@@ -1335,6 +1411,7 @@ void rdx_context_destroy(rdx_context *ctx) {
     }
     for (auto &kv : ctx->pinned_free)
         for (void *p : kv.second) (void)hipHostFree(p);
+    if (tuning().phases) print_phases();
     delete ctx;
 }
 
@@ -1696,6 +1773,7 @@ rdx_status acquire_ws(rdx_context *ctx, PoolEntry &e, WsLease &lease, bool wait 
 void destroy_lane(Lane *L) {
     if (!L) return;
     if (L->ws && L->owns_ws) destroy_workspace(L->ws);   // synchronises its stream first
+    if (L->done) (void)hipEventDestroy(L->done);
     if (L->h_res) (void)hipHostFree(L->h_res);
     delete L;
 }
@@ -1717,6 +1795,7 @@ rdx_status create_lane(int device, Lane **out, Lane *share = nullptr) {
         hipError_t e = hipHostMalloc((void **)&L->h_res, kTableChunks * kSlotWords * sizeof(uint64_t),
                                      hipHostMallocCoherent);
         if (e == hipSuccess) std::memset(L->h_res, 0, kTableChunks * kSlotWords * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&L->done, hipEventDisableTiming);
         st = map_err(e);
     }
     if (st) {
@@ -1760,6 +1839,10 @@ rdx_status launch_lane(Lane &L) {
             for (uint32_t i = 0; i < L.n; ++i) a.tbl.p[i] = L.batch[i]->chunk;
             const uint64_t te = a.src.fused ? 4096 : 16384 / j0.esz;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, L.n, ws->cus);
+            // a chunk in host memory: a few workgroups stream it over PCIe (every workgroup reading its own
+            // pages at once slows the link: 1 MiB in 27 us with 8, 50 us with 32, 258 us with 256)
+            if (j0.host_read)
+                a.blocks_per_chunk = std::min<uint32_t>(a.blocks_per_chunk, (uint32_t)std::max(1, tuning().host_read_wgs));
             if ((st = ensure(ws, ws->partials, (uint64_t)L.n * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, (uint64_t)L.n * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
@@ -1791,6 +1874,7 @@ rdx_status launch_lane(Lane &L) {
         }
         if ((st = launch_multi_group(ws, g, L.n, s, kMultiHostSlots))) return st;
     }
+    if (L.done) RDX_HIP(hipEventRecord(L.done, s));
     L.tag = ws->epoch;
     L.remaining = L.n;
     L.polls = 0;
@@ -1840,7 +1924,7 @@ bool poll_lane(Lane &L, bool kernel_done) {
 
 // Same plan and launch descriptor but the chunk: one batched launch serves both.
 bool same_group(const Job &a, const Job &b) {
-    if (a.mode != b.mode || a.dtype != b.dtype || a.op != b.op) return false;
+    if (a.mode != b.mode || a.dtype != b.dtype || a.op != b.op || a.host_read != b.host_read) return false;
     return a.mode == Mode::AllContig ? std::memcmp(&a.contig, &b.contig, sizeof a.contig) == 0
                                      : std::memcmp(&a.strided, &b.strided, sizeof a.strided) == 0;
 }
@@ -1884,6 +1968,7 @@ void form_batch(std::deque<Job *> &pending, Lane &L) {
 // it sleeps on job_cv.
 void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
     (void)hipSetDevice(e->device);
+    (void)pthread_setname_np(pthread_self(), "rdx-dispatch");
     // this thread's naps: microseconds, not the default 50 us timer slack
     (void)prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0);
     std::deque<Job *> pending;
@@ -1959,8 +2044,9 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
         for (Lane *l : e->lanes) {
             if (l->n == 0) continue;
             bool kernel_done = false;
-            if (++l->polls % 64 == 0) {   // the lane's stream holds nothing but this launch (and its twin's)
-                const hipError_t q = hipStreamQuery(l->ws->own_stream);
+            if (++l->polls % 64 == 0) {   // the launch's end (an event query: a stream query on a busy stream
+                                          // costs a HIP runtime thread spinning on a marker)
+                const hipError_t q = hipEventQuery(l->done);
                 kernel_done = q != hipErrorNotReady;
             }
             const uint32_t before = l->remaining;
@@ -2037,6 +2123,7 @@ rdx_status wait_event(rdx_context *ctx, PoolEntry &e, hipEvent_t ev, double budg
     }
     Waiter w;
     w.ev = ev;
+    e.sleeps.fetch_add(1, std::memory_order_relaxed);
     {
         std::lock_guard<std::mutex> g(e.mu);
         if (!ensure_dispatcher(ctx, e)) return RDX_E_OUT_OF_MEMORY;
@@ -2066,13 +2153,20 @@ bool claim_direct(PoolEntry &e) {
     return true;
 }
 
-void release_direct(PoolEntry &e, bool served) {
+void release_direct(PoolEntry &e, bool served, bool host_read = false) {
     std::lock_guard<std::mutex> g(e.mu);
     --e.direct_active;
     if (served) ++e.direct;
+    if (served && host_read) ++e.host_reads;
 }
 
-rdx_status run_direct(rdx_context *ctx, PoolEntry &e, rdx_workspace *ws, Job &job, double budget_us) {
+// RDX_PHASES: when the launch call returned and when the result was seen (execute_host's phase record)
+struct DirectTimes {
+    std::chrono::steady_clock::time_point launched, seen;
+};
+
+rdx_status run_direct(rdx_context *ctx, PoolEntry &e, rdx_workspace *ws, Job &job, double budget_us,
+                      DirectTimes *tm = nullptr) {
     RDX_HIP(hipSetDevice(ws->device));
     constexpr size_t slot_bytes = kTableChunks * kSlotWords * sizeof(uint64_t);
     if (!ws->h_slot) {
@@ -2088,22 +2182,31 @@ rdx_status run_direct(rdx_context *ctx, PoolEntry &e, rdx_workspace *ws, Job &jo
     L.group = true;
     L.batch[0] = &job;
     L.n = 1;
+    L.done = ws->done_ev;   // recorded behind the launch
     rdx_status st = launch_lane(L);
     if (st) return st;
+    if (tm) {
+        RDX_HIP(hipEventRecord(ws->ph_ev[2], ws->own_stream));
+        tm->launched = std::chrono::steady_clock::now();
+    }
     // the slot's tag arrives with the fold; the stream query (every 64th poll) catches a launch that ended
     // without writing it (a device fault: RDX_E_DEVICE).  Past the spin budget the caller sleeps until
     // the launch has ended (wait_event), then reads its slot.
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t polls = 1;; ++polls) {
-        const bool kernel_done = polls % 64 == 0 && hipStreamQuery(ws->own_stream) != hipErrorNotReady;
-        if (poll_lane(L, kernel_done)) return job.st;
+        const bool kernel_done = polls % 64 == 0 && hipEventQuery(ws->done_ev) != hipErrorNotReady;
+        if (poll_lane(L, kernel_done)) {
+            if (tm) tm->seen = std::chrono::steady_clock::now();
+            return job.st;
+        }
         if (polls % 16 == 0 &&
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >= budget_us)
             break;
         __builtin_ia32_pause();
     }
-    if ((st = wait_stream(ctx, e, ws, 0.0))) return st;
+    if ((st = wait_event(ctx, e, ws->done_ev, 0.0))) return st;
     poll_lane(L, true);   // the slot was written before the launch ended, or the request fails: RDX_E_DEVICE
+    if (tm) tm->seen = std::chrono::steady_clock::now();
     return job.st;
 }
 
@@ -2128,6 +2231,7 @@ struct CborOut {
     uint64_t len = 0;       // encoded bytes
 };
 constexpr uint64_t kCborOneTrip = 1ull << 20;   // bounds up to this come back whole, in one round trip
+constexpr uint64_t kBackStage = 64ull << 10;    // rdx_workspace::h_back: small responses staged page-locked
 
 // operation<T>() for a chunk in host memory (app.rs:163-183): plan, bind the response buffers
 // (caller-provided or pooled), H2D, kernels, D2H; blocks until the response is in host memory.
@@ -2138,6 +2242,8 @@ constexpr uint64_t kCborOneTrip = 1ull << 20;   // bounds up to this come back w
 rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t *chunk, uint64_t chunk_len,
                         const std::function<rdx_status(const rdx_response_info &, void **, int64_t **)> &bind,
                         rdx_response_info *info, CborOut *cb = nullptr, int resident_device = -1) {
+    const auto t_enter = std::chrono::steady_clock::now();
+    const double c_enter = tuning().phases ? thread_cpu_us() : 0.0;
     const bool resident = resident_device >= 0;
     const bool compressed = req.compression != RDX_COMPRESSION_NONE;
     ExecPlan p;
@@ -2154,9 +2260,12 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
     if (!place(ctx, chunk_len, resident_device, pl)) return resident ? RDX_E_INVALID_ARGUMENT : RDX_E_NO_DEVICE;
     PoolEntry &entry = *pl.e;
     // a small all-axes request joins the entry's coalesced k_multi launches (chunk at d_base in HBM)
-    auto coalescible = [&](const uint8_t *d_base, Job &job) -> bool {
+    // (`host_read`: the direct host-read path's own size bound, RDX_HOST_READ_KIB)
+    auto coalescible = [&](const uint8_t *d_base, Job &job, bool host_read = false) -> bool {
         if (compressed || cb || !ctx->cfg.coalesce) return false;
-        if (chunk_len > (resident ? ctx->cfg.coalesce_max_bytes : ctx->cfg.coalesce_host_max_bytes)) return false;
+        const uint64_t cap = host_read ? (uint64_t)std::max(0, tuning().host_read_kib) * 1024
+                                       : resident ? ctx->cfg.coalesce_max_bytes : ctx->cfg.coalesce_host_max_bytes;
+        if (chunk_len > cap) return false;
         if ((p.mode != Mode::AllContig && p.mode != Mode::AllStrided) || !p.unfused_es.empty() || !p.miss_list.empty())
             return false;
         job.mode = p.mode;
@@ -2218,21 +2327,76 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             return map_pipelined(ws, p, chunk, chunk_len, static_cast<uint8_t *>(body), counts);
         }
         const uint8_t *src = chunk;
+        // RDX_PHASES: the direct path's record (phase_sums)
+        const bool ph = tuning().phases != 0;
+        auto phase_record = [&](int path, std::chrono::steady_clock::time_point t_ready,
+                                std::chrono::steady_clock::time_point t_issued, const DirectTimes &tm) -> rdx_status {
+            const auto t_ret = std::chrono::steady_clock::now();
+            RDX_HIP(hipEventSynchronize(ws->ph_ev[2]));
+            float copy_ms = 0, kern_ms = 0;
+            if (path == 1) RDX_HIP(hipEventElapsedTime(&copy_ms, ws->ph_ev[0], ws->ph_ev[1]));
+            RDX_HIP(hipEventElapsedTime(&kern_ms, ws->ph_ev[1], ws->ph_ev[2]));
+            auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+                return std::chrono::duration<double, std::micro>(b - a).count();
+            };
+            const double v[8] = {us(t_enter, t_ready), us(t_ready, t_issued), us(t_issued, tm.launched),
+                                 us(tm.launched, tm.seen), us(tm.seen, t_ret), us(t_enter, t_ret), 1e3 * copy_ms,
+                                 1e3 * kern_ms};
+            phase_add(path, v);
+            return RDX_OK;
+        };
+        if (ph)
+            for (hipEvent_t &ev : ws->ph_ev)
+                if (!ev) RDX_HIP(hipEventCreate(&ev));
         if (!resident) {
+            Job job;
+            // a small page-locked chunk on an idle entry: no copy — the all-axes kernel reads it over PCIe
+            // with a few workgroups (Job::host_read) and writes its result into the page-locked slot
+            const uint8_t *alias = chunk_len <= (uint64_t)std::max(0, tuning().host_read_kib) * 1024 ? host_alias(chunk) : nullptr;
+            if (alias && coalescible(alias, job, true) && job.mode == Mode::AllContig && claim_direct(entry)) {
+                job.host_read = true;
+                job.multi_ok = false;
+                const auto t_ready = std::chrono::steady_clock::now();
+                if (ph) RDX_HIP(hipEventRecord(ws->ph_ev[1], s));
+                DirectTimes tm;
+                r = run_direct(ctx, entry, ws, job, spin_budget_us(entry, pl.weight, chunk_len, 0), ph ? &tm : nullptr);
+                release_direct(entry, true, true);
+                if (ph && !r && (r = phase_record(0, t_ready, t_ready, tm))) return r;
+                return r;
+            }
             if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
+            const auto t_ready = std::chrono::steady_clock::now();
+            const double c_ready = ph ? thread_cpu_us() : 0.0;
+            if (ph) RDX_HIP(hipEventRecord(ws->ph_ev[0], s));
             if (chunk_len) RDX_HIP(hipMemcpyAsync(ws->chunk.p, chunk, chunk_len, hipMemcpyHostToDevice, s));
             src = ws->chunk.p;
-            Job job;
             if (coalescible(src, job)) {
                 if (claim_direct(entry)) {   // launched behind the copy on the same stream
-                    r = run_direct(ctx, entry, ws, job, spin_budget_us(entry, pl.weight, chunk_len, chunk_len));
+                    const auto t_issued = std::chrono::steady_clock::now();
+                    if (ph) RDX_HIP(hipEventRecord(ws->ph_ev[1], s));
+                    DirectTimes tm;
+                    r = run_direct(ctx, entry, ws, job, spin_budget_us(entry, pl.weight, chunk_len, chunk_len),
+                                   ph ? &tm : nullptr);
                     release_direct(entry, true);
+                    if (ph && !r && (r = phase_record(1, t_ready, t_issued, tm))) return r;
                     return r;
                 }
                 // the coalesced launch waits for the copy on the device; this thread does not
                 RDX_HIP(hipEventRecord(ws->copy_ev, s));
                 job.dep = ws->copy_ev;
-                return coalesce(ctx, entry, job);
+                if (!ph) return coalesce(ctx, entry, job);
+                const auto t_q = std::chrono::steady_clock::now();
+                const double c_q = thread_cpu_us();
+                r = coalesce(ctx, entry, job);
+                const auto t_w = std::chrono::steady_clock::now();
+                const double c_w = thread_cpu_us();
+                auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+                    return std::chrono::duration<double, std::micro>(b - a).count();
+                };
+                const double v[8] = {us(t_enter, t_ready), us(t_ready, t_q), us(t_q, t_w), us(t_enter, t_w),
+                                     c_ready - c_enter, c_q - c_ready, c_w - c_q, c_w - c_enter};
+                phase_add(2, v);
+                return r;
             }
         }
         if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
@@ -2260,7 +2424,9 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
         RDX_HIP(hipMemsetAsync(ws->status.p, 0, sizeof(uint32_t), s));
         if ((r = run_device(ws, p, src, nullptr, 1, len, ws->body.p, ws->counts.p, ws->status.p, s)))
             return r;
-        uint32_t status = 0;
+        if (!ws->h_back) RDX_HIP(hipHostMalloc((void **)&ws->h_back, 16 + kBackStage, hipHostMallocDefault));
+        uint32_t &status = *reinterpret_cast<uint32_t *>(ws->h_back);
+        status = 0;
         if (cb) {   // encode on the device; the length (and, for small bounds, the bytes) in one trip
             const uint64_t bound = rdx_cbor_bound(&p.info, cb->flags);
             if (!bound) return RDX_E_INVALID_ARGUMENT;
@@ -2270,7 +2436,8 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             if ((r = cbor_device(ws, &p.info, ws->body.p, ws->counts.p, cb->flags, ws->cbor.p, bound, ws->cbor_len.p,
                                  nullptr, s)))
                 return r;
-            uint64_t n = 0;
+            uint64_t &n = ws->h_back[1];
+            n = 0;
             RDX_HIP(hipMemcpyAsync(&n, ws->cbor_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
             RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             if (bound <= kCborOneTrip) RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, bound, hipMemcpyDeviceToHost, s));
@@ -2284,14 +2451,21 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             cb->len = n;
             return RDX_OK;
         }
-        if (p.info.body_bytes) RDX_HIP(hipMemcpyAsync(body, ws->body.p, p.info.body_bytes, hipMemcpyDeviceToHost, s));
-        if (p.info.n_counts)
-            RDX_HIP(hipMemcpyAsync(counts, ws->counts.p, p.info.n_counts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        // a small response into pageable buffers goes through the page-locked block (then one host memcpy)
+        const uint64_t bb = p.info.body_bytes, cbytes = p.info.n_counts * sizeof(int64_t);
+        const uint64_t bb16 = (bb + 15) / 16 * 16;
+        const bool stage = bb16 + cbytes <= kBackStage && ((bb && !is_pinned(body)) || (cbytes && !is_pinned(counts)));
+        uint8_t *const st_body = reinterpret_cast<uint8_t *>(ws->h_back + 2);
+        if (bb) RDX_HIP(hipMemcpyAsync(stage ? st_body : body, ws->body.p, bb, hipMemcpyDeviceToHost, s));
+        if (cbytes) RDX_HIP(hipMemcpyAsync(stage ? st_body + bb16 : (uint8_t *)counts, ws->counts.p, cbytes, hipMemcpyDeviceToHost, s));
         RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        const uint64_t d2h = p.info.body_bytes + p.info.n_counts * sizeof(int64_t);
-        if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, (resident ? 0 : chunk_len) + d2h, len))))
+        if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, (resident ? 0 : chunk_len) + bb + cbytes, len))))
             return r;
         if (status) return (rdx_status)status;
+        if (stage) {
+            if (bb) std::memcpy(body, st_body, bb);
+            if (cbytes) std::memcpy(counts, st_body + bb16, cbytes);
+        }
         return RDX_OK;
     };
     return run();
@@ -2514,6 +2688,8 @@ rdx_status rdx_context_stats(rdx_context *ctx, uint32_t index, rdx_device_stats 
     out->direct_requests = e.direct;
     out->placed_bytes = e.placed_bytes;
     out->peak_outstanding_bytes = e.peak_outstanding;
+    out->host_read_requests = e.host_reads;
+    out->sleeps = e.sleeps.load(std::memory_order_relaxed);
     return RDX_OK;
 }
 

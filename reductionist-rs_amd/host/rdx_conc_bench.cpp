@@ -2,8 +2,10 @@
 // issues them — one process (app_state.rs:21-37), every Tokio / Rayon worker running one request at a time
 // to completion (src/app.rs:147-152, thread_limit = num_cpus - 1, src/app_state.rs:22).
 //
-//   rdx_conc_bench <config c1|c2|c3|c4|s1> <threads> <requests per thread> [path] [devices] [lanes]
+//   rdx_conc_bench <config c1|c2|c3|c4|s1|h4f32|h4f64> <threads> <requests per thread> [path] [devices] [lanes]
 //     config  s1: a 1 MiB f32 contiguous sum (a host chunk at the default coalesce_host_max_bytes)
+//             h4f32 / h4f64: one 4 MiB f32 / f64 chunk, shuffled (es = sizeof T), big-endian, sum (the
+//             north_star's host-inclusive 4 MiB rows)
 //     path    device:   each thread its own rdx_workspace + stream, rdx_execute_device on an HBM-resident
 //                       chunk + a stream synchronize (independent launches; round-2 form)
 //             resident: rdx_execute_resident on an HBM-resident chunk, response into host memory; small
@@ -15,8 +17,15 @@
 //             host / resident requests are placed by the pool (least outstanding bytes)
 //     lanes   coalescer launches in flight per device (default: the engine's)
 // Chunks rotate over buffers larger than the Infinity Cache (per device).  Prints one JSON line.
+#include <dirent.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <sys/resource.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <fstream>
+#include <map>
 
 #include <algorithm>
 #include <atomic>
@@ -74,6 +83,14 @@ static Config make_config(const std::string &n) {
         c.dtype = RDX_DTYPE_FLOAT32;
         c.bytes = 1u << 20;
         c.alg_bytes = c.bytes;
+    } else if (n == "h4f32" || n == "h4f64") {  // 4 MiB shuffled big-endian f32 / f64 sum
+        const bool f64 = n == "h4f64";
+        c.op = RDX_OP_SUM;
+        c.dtype = f64 ? RDX_DTYPE_FLOAT64 : RDX_DTYPE_FLOAT32;
+        c.byte_order = RDX_BYTE_ORDER_BIG;
+        c.filters = {{RDX_FILTER_SHUFFLE, 0, f64 ? 8u : 4u}};
+        c.bytes = 4u << 20;
+        c.alg_bytes = c.bytes;
     } else if (n == "c4") {  // configs[3]'s chunk: f32 4 MiB, shuffle es=4, native order, sum
         c.op = RDX_OP_SUM;
         c.dtype = RDX_DTYPE_FLOAT32;
@@ -91,6 +108,34 @@ static Config make_config(const std::string &n) {
         c.alg_bytes = 112ull * 64 * 96 * 8;
     }
     return c;
+}
+
+// CPU time (us) of every thread of this process by thread name (/proc/self/task/*/stat utime + stime)
+static std::map<std::string, double> thread_cpu() {
+    std::map<std::string, double> m;
+    const double tick = 1e6 / (double)sysconf(_SC_CLK_TCK);
+    DIR *d = opendir("/proc/self/task");
+    if (!d) return m;
+    while (dirent *e = readdir(d)) {
+        if (e->d_name[0] == '.') continue;
+        const std::string base = std::string("/proc/self/task/") + e->d_name;
+        std::ifstream fc(base + "/comm"), fs(base + "/stat");
+        std::string name, stat;
+        std::getline(fc, name);
+        std::getline(fs, stat);
+        const size_t rp = stat.rfind(')');
+        if (rp == std::string::npos) continue;
+        std::stringstream ss(stat.substr(rp + 2));
+        std::string f;
+        double ut = 0, st = 0;
+        for (int k = 3; k <= 15 && ss >> f; ++k) {
+            if (k == 14) ut = std::atof(f.c_str());
+            if (k == 15) st = std::atof(f.c_str());
+        }
+        m[name] += (ut + st) * tick;
+    }
+    closedir(d);
+    return m;
 }
 
 int main(int argc, char **argv) {
@@ -174,9 +219,27 @@ int main(int argc, char **argv) {
             }
         }
     }
+    // host paths: a plain page-locked H2D copy of the same bytes, one at a time with its wait (the link's
+    // time for this request: the reference line the host-inclusive rows are read against)
+    double copy_us = 0;
+    if (host) {
+        void *dst = nullptr;
+        hipStream_t cs = nullptr;
+        CHECK_HIP(hipSetDevice(devs[0]));
+        CHECK_HIP(hipMalloc(&dst, cfg.bytes));
+        CHECK_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        for (int i = 0; i < 220; ++i) {
+            const auto t0 = std::chrono::steady_clock::now();
+            CHECK_HIP(hipMemcpyAsync(dst, bufs[0][i % nbuf], cfg.bytes, hipMemcpyHostToDevice, cs));
+            CHECK_HIP(hipStreamSynchronize(cs));
+            if (i >= 20) copy_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / 200;
+        }
+        CHECK_HIP(hipStreamDestroy(cs));
+        CHECK_HIP(hipFree(dst));
+    }
     std::atomic<int> errors{0}, ready{0};
     std::atomic<bool> go{false};
-    std::vector<double> per_thread_us(T);
+    std::vector<double> per_thread_us(T), per_thread_cpu(T);
     // each thread: (device path) its workspace, stream and output buffers, set up before the clock starts;
     // a warm-up request, then R timed requests once every thread is ready
     auto worker = [&](int t) {
@@ -215,12 +278,17 @@ int main(int argc, char **argv) {
         };
         if (!ok) ++errors;
         else for (int i = 0; i < 3; ++i) one(i);
+        (void)pthread_setname_np(pthread_self(), "rdx-caller");
         ++ready;
         while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
         const auto t0 = std::chrono::steady_clock::now();
+        timespec c0{}, c1{};
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
         if (ok)
             for (int i = 0; i < R; ++i) one(i);
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
         per_thread_us[t] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
+        per_thread_cpu[t] = (c1.tv_sec - c0.tv_sec) * 1e6 + (c1.tv_nsec - c0.tv_nsec) * 1e-3;
         if (path == "device") {
             (void)hipFree(d_body);
             (void)hipFree(d_counts);
@@ -233,10 +301,25 @@ int main(int argc, char **argv) {
     for (int t = 0; t < T; ++t) th.emplace_back(worker, t);
     while (ready.load() < T) std::this_thread::yield();
     rusage ru0{}, ru1{};
+    const auto tc0 = thread_cpu();
     getrusage(RUSAGE_SELF, &ru0);
     go.store(true, std::memory_order_release);
     for (auto &x : th) x.join();
     getrusage(RUSAGE_SELF, &ru1);
+    const auto tc1 = thread_cpu();
+    // per request: the callers' own CPU, and every other thread by name (the engine's dispatcher, HIP's)
+    double callers = 0;
+    for (double v : per_thread_cpu) callers += v;
+    std::string others;
+    for (auto &kv : tc1) {
+        if (kv.first == "rdx-caller") continue;
+        auto it = tc0.find(kv.first);
+        const double dv = kv.second - (it == tc0.end() ? 0.0 : it->second);
+        if (dv <= 0) continue;
+        char buf[160];
+        std::snprintf(buf, sizeof buf, "%s\"%s\": %.2f", others.empty() ? "" : ", ", kv.first.c_str(), dv / ((double)T * R));
+        others += buf;
+    }
     auto tv = [](const timeval &t) { return t.tv_sec * 1e6 + t.tv_usec; };
     // host CPU time of the whole process over the timed region (callers, dispatchers, HIP's threads)
     const double cpu_us = tv(ru1.ru_utime) - tv(ru0.ru_utime) + tv(ru1.ru_stime) - tv(ru0.ru_stime);
@@ -246,7 +329,7 @@ int main(int argc, char **argv) {
     const double reqs = (double)T * R;
     double lat = 0;
     for (double v : per_thread_us) lat += v / T;
-    uint64_t creq = 0, claunch = 0, waits = 0, wsn = 0, direct = 0;
+    uint64_t creq = 0, claunch = 0, waits = 0, wsn = 0, direct = 0, hreads = 0, sleeps = 0;
     std::string per_dev;
     for (int d = 0; d < D; ++d) {
         rdx_device_stats st{};
@@ -255,6 +338,8 @@ int main(int argc, char **argv) {
             claunch += st.coalesced_launches;
             waits += st.waits;
             direct += st.direct_requests;
+            hreads += st.host_read_requests;
+            sleeps += st.sleeps;
             wsn += st.workspaces;
             per_dev += (d ? "," : "") + std::to_string(st.requests);
         }
@@ -266,12 +351,15 @@ int main(int argc, char **argv) {
                 "\"requests_per_s\": %.1f, \"us_per_request_aggregate\": %.3f, \"us_per_request_per_thread\": %.3f, "
                 "\"GBs_alg\": %.1f, \"GiBs_chunk\": %.1f, \"roofline_frac\": %.4f, \"coalesced_requests\": %llu, "
                 "\"coalesced_launches\": %llu, \"direct_requests\": %llu, \"workspaces\": %llu, \"waits\": %llu, "
-                "\"requests_per_device\": [%s], \"cpu_us_per_request\": %.2f, \"cpu_cores_busy\": %.2f, \"errors\": %d}\n",
+                "\"requests_per_device\": [%s], \"cpu_us_per_request\": %.2f, \"cpu_cores_busy\": %.2f, \"errors\": %d, "
+                "\"host_read_requests\": %llu, \"sleeps\": %llu, \"pinned_copy_us_one\": %.2f, "
+                "\"cpu_us_per_request_callers\": %.2f, \"cpu_us_per_request_other_threads\": {%s}}\n",
                 cfg.name.c_str(), pname, D, T, reqs, reqs / el, el / reqs * 1e6, lat, reqs * cfg.alg_bytes / el / 1e9,
                 reqs * cfg.bytes / el / (1024.0 * 1024 * 1024), reqs * cfg.alg_bytes / el / 1e9 / (8000.0 * D),
                 (unsigned long long)creq, (unsigned long long)claunch, (unsigned long long)direct,
                 (unsigned long long)wsn, (unsigned long long)waits, per_dev.c_str(), cpu_us / reqs, cpu_us / (el * 1e6),
-                errors.load());
+                errors.load(), (unsigned long long)hreads, (unsigned long long)sleeps, copy_us, callers / reqs,
+                others.c_str());
     for (size_t d = 0; d < bufs.size(); ++d)
         for (auto &b : bufs[d]) {
             if (host) rdx_host_free(ctx, b);

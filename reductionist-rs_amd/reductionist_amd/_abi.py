@@ -106,7 +106,8 @@ class rdx_device_stats(C.Structure):
                 ("max_workspaces", C.c_uint32), ("requests", C.c_uint64), ("coalesced_requests", C.c_uint64),
                 ("coalesced_launches", C.c_uint64), ("outstanding_bytes", C.c_uint64), ("waits", C.c_uint64),
                 ("direct_requests", C.c_uint64), ("placed_bytes", C.c_uint64),
-                ("peak_outstanding_bytes", C.c_uint64)]
+                ("peak_outstanding_bytes", C.c_uint64), ("host_read_requests", C.c_uint64),
+                ("sleeps", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -114,3 +114,43 @@ def test_pipelined_map_layouts(engine, case):
     creq = make_request(op, req, oracle.convert)
     got = _pinned_run(engine, creq, raw)
     _check(op, req, got, oracle.execute(creq, raw.tobytes()))
+
+
+def test_host_read_pinned_chunks(engine):
+    """Small page-locked chunks on an idle entry are read by the all-axes kernel itself over PCIe (no H2D
+    copy; rdx_device_stats.host_read_requests counts them).  Every dtype / op / byte order / shuffle, chunk
+    sizes from a few elements to the 4 MiB bound (and past it: the DMA path), starting at offsets inside the
+    pinned block; the block is rewritten between requests and every result must follow (no stale line of a
+    previous request survives in a device cache) — bit-exact against the oracle."""
+    rng = np.random.default_rng(0x5EED4EAD)
+    cap = (4 << 20) + (1 << 16) + 64
+    ptr, view = engine.host_alloc(cap)
+    try:
+        before = engine.stats(0)["host_read_requests"]
+        n_cases = 0
+        for dtype in ("int32", "int64", "uint32", "uint64", "float32", "float64"):
+            es = _abi.DTYPE_SIZE[dtype]
+            for nbytes in (8 * es, 4096 + 8 * es, 1 << 20, 4 << 20, (4 << 20) + (1 << 16)):
+                for off in (0, 16, 8):
+                    op = ("sum", "count", "min", "max")[n_cases % 4]
+                    req = {"dtype": dtype}
+                    if rng.random() < 0.5:
+                        req["byte_order"] = "big"
+                    if rng.random() < 0.5:
+                        req["filters"] = [{"id": "shuffle", "element_size": es}]
+                    creq = make_request(op, req, oracle.convert)
+                    for rewrite in range(2):
+                        if dtype.startswith("float"):
+                            vals = rng.integers(-1000, 1000, nbytes // es).astype(np.float64 if es == 8 else np.float32)
+                        else:
+                            vals = rng.integers(0, 1000, nbytes // es).astype(np.dtype(dtype))
+                        raw = vals.astype(vals.dtype.newbyteorder(">")).tobytes() if req.get("byte_order") else vals.tobytes()
+                        data = encode_filters(raw, req.get("filters"), oracle.shuffle)
+                        view[off:off + nbytes] = np.frombuffer(data, np.uint8)
+                        got = engine.execute_owned(creq, (ptr + off, nbytes))
+                        _check(op, req, got, oracle.execute(creq, data))
+                    n_cases += 1
+        used = engine.stats(0)["host_read_requests"] - before
+        assert used > 0, "the host-read path never ran"
+    finally:
+        engine.host_free(ptr)
