@@ -240,8 +240,8 @@ typedef struct rdx_device_stats {
     uint64_t peak_outstanding_bytes;/* high-water mark of outstanding_bytes (each request weighs its chunk
                                        bytes + 64 KiB): least-outstanding placement keeps it near
                                        ceil(concurrent requests / entries) requests' weight                    */
-    uint64_t host_read_requests;    /* of direct_requests: page-locked host chunks the kernel read over PCIe itself
-                                       (no H2D copy; RDX_HOST_READ_KIB)                                        */
+    uint64_t host_read_requests;    /* page-locked host chunks the kernel read over PCIe itself (no H2D copy;
+                                       RDX_HOST_READ_KIB), direct or coalesced                                 */
     uint64_t sleeps;                /* callers that slept (futex) instead of spinning until their result          */
 } rdx_device_stats;
 rdx_status rdx_context_stats(rdx_context *ctx, uint32_t index, rdx_device_stats *out);

@@ -1839,10 +1839,11 @@ rdx_status launch_lane(Lane &L) {
             for (uint32_t i = 0; i < L.n; ++i) a.tbl.p[i] = L.batch[i]->chunk;
             const uint64_t te = a.src.fused ? 4096 : 16384 / j0.esz;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, L.n, ws->cus);
-            // a chunk in host memory: a few workgroups stream it over PCIe (every workgroup reading its own
-            // pages at once slows the link: 1 MiB in 27 us with 8, 50 us with 32, 258 us with 256)
+            // chunks in host memory: a few workgroups in all stream them over PCIe (each workgroup that reads
+            // host memory adds ~0.9 us to the launch: 1 MiB in 27 us with 8, 50 us with 32, 258 us with 256;
+            // profiles/r05_hread_probe.jsonl)
             if (j0.host_read)
-                a.blocks_per_chunk = std::min<uint32_t>(a.blocks_per_chunk, (uint32_t)std::max(1, tuning().host_read_wgs));
+                a.blocks_per_chunk = std::max<uint32_t>(1, (uint32_t)std::max(1, tuning().host_read_wgs) / L.n);
             if ((st = ensure(ws, ws->partials, (uint64_t)L.n * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, (uint64_t)L.n * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
@@ -2021,6 +2022,7 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
             }
             form_batch(pending, *lane);
             const uint32_t n = lane->n;
+            const bool host_reads = lane->group && lane->batch[0]->host_read;
             const auto t0 = std::chrono::steady_clock::now();
             const rdx_status st = launch_lane(*lane);
             lane->t0 = std::chrono::steady_clock::now();
@@ -2036,6 +2038,7 @@ void dispatcher_loop(rdx_context *ctx, PoolEntry *e) {
                 std::lock_guard<std::mutex> g(e->mu);
                 ++e->launches;
                 e->coalesced += n;
+                if (host_reads && !st) e->host_reads += n;
             }
             progressed = true;
         }
@@ -2186,7 +2189,7 @@ rdx_status run_direct(rdx_context *ctx, PoolEntry &e, rdx_workspace *ws, Job &jo
     rdx_status st = launch_lane(L);
     if (st) return st;
     if (tm) {
-        RDX_HIP(hipEventRecord(ws->ph_ev[2], ws->own_stream));
+        if (ws->ph_ev[2]) RDX_HIP(hipEventRecord(ws->ph_ev[2], ws->own_stream));
         tm->launched = std::chrono::steady_clock::now();
     }
     // the slot's tag arrives with the fold; the stream query (every 64th poll) catches a launch that ended
@@ -2313,6 +2316,40 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             return coalesce(ctx, entry, job);
         }
     }
+    // a small page-locked host chunk, all-axes over a contiguous run: no H2D copy and no workspace buffer —
+    // the kernel reads the chunk over PCIe with a few workgroups (Job::host_read) and its fold writes the
+    // result into a page-locked slot.  On an idle entry the caller launches it itself (direct); otherwise
+    // same-plan host chunks share one coalesced launch that keeps the readers few (launch_lane).
+    if (!resident && !compressed && !cb && chunk_len <= (uint64_t)std::max(0, tuning().host_read_kib) * 1024) {
+        const uint8_t *alias = host_alias(chunk);
+        Job job;
+        if (alias && coalescible(alias, job, true) && job.mode == Mode::AllContig) {
+            job.host_read = true;
+            job.multi_ok = false;
+            if (claim_direct(entry)) {
+                WsLease lease;
+                if (acquire_ws(ctx, entry, lease, false) == RDX_OK) {
+                    DirectTimes tm;
+                    const bool ph = tuning().phases != 0;
+                    const auto t_ready = std::chrono::steady_clock::now();
+                    st = run_direct(ctx, entry, lease.ws, job, spin_budget_us(entry, pl.weight, chunk_len, 0), &tm);
+                    release_direct(entry, true, true);
+                    if (ph && !st) {
+                        const auto t_ret = std::chrono::steady_clock::now();
+                        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+                            return std::chrono::duration<double, std::micro>(b - a).count();
+                        };
+                        const double v[8] = {us(t_enter, t_ready), 0.0, us(t_ready, tm.launched), us(tm.launched, tm.seen),
+                                             us(tm.seen, t_ret), us(t_enter, t_ret), 0.0, 0.0};
+                        phase_add(0, v);
+                    }
+                    return st;
+                }
+                release_direct(entry, false);
+            }
+            return coalesce(ctx, entry, job);
+        }
+    }
     WsLease lease;
     if ((st = acquire_ws(ctx, entry, lease))) return st;
     rdx_workspace *ws = lease.ws;
@@ -2350,20 +2387,6 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
                 if (!ev) RDX_HIP(hipEventCreate(&ev));
         if (!resident) {
             Job job;
-            // a small page-locked chunk on an idle entry: no copy — the all-axes kernel reads it over PCIe
-            // with a few workgroups (Job::host_read) and writes its result into the page-locked slot
-            const uint8_t *alias = chunk_len <= (uint64_t)std::max(0, tuning().host_read_kib) * 1024 ? host_alias(chunk) : nullptr;
-            if (alias && coalescible(alias, job, true) && job.mode == Mode::AllContig && claim_direct(entry)) {
-                job.host_read = true;
-                job.multi_ok = false;
-                const auto t_ready = std::chrono::steady_clock::now();
-                if (ph) RDX_HIP(hipEventRecord(ws->ph_ev[1], s));
-                DirectTimes tm;
-                r = run_direct(ctx, entry, ws, job, spin_budget_us(entry, pl.weight, chunk_len, 0), ph ? &tm : nullptr);
-                release_direct(entry, true, true);
-                if (ph && !r && (r = phase_record(0, t_ready, t_ready, tm))) return r;
-                return r;
-            }
             if ((r = ensure(ws, ws->chunk, std::max<uint64_t>(chunk_len, 16), s))) return r;
             const auto t_ready = std::chrono::steady_clock::now();
             const double c_ready = ph ? thread_cpu_us() : 0.0;

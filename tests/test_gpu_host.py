@@ -154,3 +154,39 @@ def test_host_read_pinned_chunks(engine):
         assert used > 0, "the host-read path never ran"
     finally:
         engine.host_free(ptr)
+
+
+def test_host_read_concurrent_callers(engine):
+    """Many callers with small page-locked chunks at once: besides the idle-entry direct launch, the
+    dispatcher groups same-plan host chunks into one launch of a few workgroups that read them all over
+    PCIe.  Each caller rewrites its own block every request; every result is exact (integer-valued data)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = 1 << 18
+    threads, iters = 8, 40
+    blocks = [engine.host_alloc(4 * n + 64) for _ in range(threads)]
+    before = engine.stats(0)["host_read_requests"]
+    creq = {dt: make_request("sum", {"dtype": dt}, oracle.convert) for dt in ("int32", "float32")}
+
+    def worker(t):
+        ptr, view = blocks[t]
+        rng = np.random.default_rng(0x5EED7000 + t)
+        bad = []
+        for i in range(iters):
+            dt = ("int32", "float32")[(i + t) % 2]
+            v = rng.integers(-100, 100, n).astype(np.int32 if dt == "int32" else np.float32)
+            view[16:16 + 4 * n] = np.frombuffer(v.tobytes(), np.uint8)
+            st, info, body, counts = engine.execute_owned(creq[dt], (ptr + 16, 4 * n))
+            want = int(v.astype(np.int64).sum())
+            got = int(np.frombuffer(body, np.int32 if dt == "int32" else np.float32)[0])
+            if st != 0 or counts != [n] or got != want:
+                bad.append((t, i, dt, st, got, want))
+        return bad
+
+    try:
+        with ThreadPoolExecutor(threads) as ex:
+            bad = [b for r in ex.map(worker, range(threads)) for b in r]
+        assert not bad, bad[:5]
+        assert engine.stats(0)["host_read_requests"] - before > 0
+    finally:
+        for ptr, _ in blocks:
+            engine.host_free(ptr)
