@@ -933,8 +933,11 @@ def leg_native_concurrent(cx):
                 coalesced by the pool's dispatcher into shared launches (same-plan groups / k_multi), each
                 caller's result written to page-locked host memory by the fold; an idle entry runs the
                 request on the caller's own thread (the direct fast path, direct_requests);
-      owned:    rdx_execute_owned of a 1 MiB page-locked host chunk (s1: the plugin's own call; host chunks
-                of 1 MiB or less coalesce by default)."""
+      owned:    rdx_execute_owned of a page-locked host chunk (the plugin's own call): s1 1 MiB f32 sum,
+                h4f32 / h4f64 one 4 MiB shuffled big-endian f32 / f64 sum (the north_star's host-inclusive
+                4 MiB rows; pinned_copy_us_one is a plain pinned H2D copy of the same bytes, same run).
+                Page-locked chunks up to 4 MiB are read by the kernel itself over PCIe (host_read_requests);
+                every row carries the process's CPU per request and its split by thread."""
     exe = ROOT / "reductionist-rs_amd" / "rdx_conc_bench"
     if not exe.exists():
         return {"skipped": f"{exe} not built"}
@@ -946,6 +949,7 @@ def leg_native_concurrent(cx):
                                      ("c1", 1, 2000, "resident"), ("c1", pool, 2000, "resident"),
                                      ("c1", 4 * pool, 1000, "resident"),
                                      ("s1", 1, 2000, "owned"), ("s1", pool, 2000, "owned"),
+                                     ("h4f32", 1, 1000, "owned"), ("h4f64", 1, 1000, "owned"),
                                      ("c2", 1, 300, "device"), ("c2", 4, 300, "device")):
         out.append(conc_bench(cfg, threads, reqs, path))
     return out
@@ -1043,7 +1047,8 @@ def leg_host(cx):
     torch, lib, _abi = cx.torch, cx.lib, cx.abi
     out = {}
 
-    def pcie(nbytes_h2d, nbytes_d2h, reps=5):
+    def pcie(nbytes_h2d, nbytes_d2h, reps=0):
+        reps = reps or int(max(5, min(200, (256 << 20) // max(1, nbytes_h2d))))
         h = torch.empty(max(nbytes_h2d, 16), dtype=torch.uint8).pin_memory()
         d = torch.empty(max(nbytes_h2d, 16), dtype=torch.uint8, device="cuda")
         hd = torch.empty(max(nbytes_d2h, 16), dtype=torch.uint8).pin_memory()
@@ -1105,6 +1110,12 @@ def leg_host(cx):
     run("c2_sum_64mib", cx.abi.CRequest("sum", "float32", byte_order="big",
                                         filters=[{"id": "shuffle", "element_size": 4}]), c2, 20)
     run("c3_min_16mib", _c3_req(_abi, "min"), _c3_host(), 40)
+    # the north_star's 4 MiB rows: one shuffled big-endian f32 / f64 chunk (page-locked chunks of this size
+    # are read by the kernel over PCIe: no separate copy)
+    for es, dt, name in ((4, "float32", "f32_sum_4mib_shuffled_be"), (8, "float64", "f64_sum_4mib_shuffled_be")):
+        v = np.random.default_rng(40 + es).random((4 << 20) // es).astype(">f4" if es == 4 else ">f8")
+        h4 = np.ascontiguousarray(v.view(np.uint8).reshape(-1, es).T).reshape(-1)
+        run(name, cx.abi.CRequest("sum", dt, byte_order="big", filters=[{"id": "shuffle", "element_size": es}]), h4, 300)
     c5 = np.random.default_rng(6).integers(-2 ** 62, 2 ** 62, 512 * 256 * 256, dtype=np.int64)
     run("c5_select_256mib", _abi.CRequest("select", "int64", shape=[512, 256, 256], selection=C5_SEL), c5, 6)
     return out

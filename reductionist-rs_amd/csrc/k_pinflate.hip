@@ -841,6 +841,11 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
     __shared__ uint32_t s_wm[kLanes / 64];
     __shared__ uint64_t s_body;
     __shared__ uint32_t s_ok, s_nlen, s_ndist, s_first;
+    // the tabulated walk: lane exits from each of the kOff starts their predecessor can hand them
+    constexpr uint32_t kOff = 48, kG = kLanes / kOff, kWalk = 4;
+    __shared__ uint64_t s_tx[kG * kOff];
+    __shared__ uint32_t s_tnb[kG * kOff];
+    __shared__ uint8_t s_ted[kG * kOff];
     __shared__ uint32_t win[kWinDwords];
     const uint32_t n = min(a.state->n_cand, kPinfMaxCand);
     const uint32_t ci = first + blockIdx.x;
@@ -950,15 +955,74 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
                 __syncthreads();
             }
             if (done) break;
-            // the data keeps the parses apart: the first mismatched lane walks on sequentially
+            // the data keeps the parses apart (periodic data: a parse that starts out of phase stays out of
+            // phase, so rounds verify one lane each).  The true start of lane j is the first symbol boundary
+            // at or past lo(j): one of the kOff bit offsets after it (a symbol — length, distance and their
+            // extra bits — is at most 48 bits).  So lane j's exit is tabulated for every one of those starts,
+            // kG lanes per pass with all threads, and thread 0 composes the true chain through the tables:
+            // a pass verifies kG lanes in the time of one lane's decode (the walk it replaces verified one)
             ++walks;
+            // first the cheap form: thread 0 walks on from the first break, lane by lane, for up to kWalk
+            // lanes (most breaks heal within a lane or two); only parses still apart after that are tabulated
             if (t == 0) {
                 uint32_t m = 1;
                 while (m < L && (s_ed[m - 1] != 0 || s_st[m] == s_x[m - 1])) ++m;
-                for (uint32_t j = m; j < L; ++j) {
+                uint32_t j = m;
+                for (uint32_t w = 0; j < L && w < kWalk; ++w, ++j) {
                     if (j > m && (s_ed[j - 1] != 0 || s_st[j] == s_x[j - 1])) break;
                     run(j, s_x[j - 1]);
                 }
+                // the next break, if the walk did not heal it
+                while (j < L && s_ed[j - 1] == 0 && s_st[j] == s_x[j - 1]) ++j;
+                s_first = j < L && s_ed[j - 1] == 0 && j < m + kWalk + 1 ? j : L;
+            }
+            __syncthreads();
+            if (s_first >= L) continue;   // healed (or the block ended): back to the rounds
+            // each pass tabulates the kG lanes from the first break; thread 0 composes them, then skips to
+            // the next lane whose start disagrees with its predecessor's exit (lanes whose parses agree need
+            // no table), so data with few breaks costs one pass and periodic data one pass per kG lanes
+            uint32_t base = s_first;
+            for (;;) {
+                const uint32_t k = base + t / kOff, o = t % kOff;
+                if (t < kG * kOff && k < L) {
+                    Bits br;
+                    br.seek(S, lo(k) + o);
+                    uint64_t x, nb;
+                    const uint32_t r = run_lane<false>(T, S, br, lo(k + 1), a.end_bits, &x, &nb, nullptr, 0);
+                    s_tx[t] = x;
+                    s_tnb[t] = (uint32_t)nb;
+                    s_ted[t] = (uint8_t)r;
+                }
+                __syncthreads();
+                if (t == 0) {
+                    uint32_t next = L;
+                    const uint32_t hi = base + kG < L ? base + kG : L;
+                    uint32_t j = base;
+                    for (; j < hi; ++j) {
+                        if (s_ed[j - 1] != 0) break;   // the block ended before lane j
+                        const uint64_t st = s_x[j - 1];
+                        if (s_st[j] == st) continue;   // already decoded from its true start
+                        const uint64_t off = st - lo(j);
+                        if (off < kOff) {
+                            const uint32_t q = (j - base) * kOff + (uint32_t)off;
+                            s_st[j] = st;
+                            s_x[j] = s_tx[q];
+                            s_nb[j] = s_tnb[q];
+                            s_ed[j] = s_ted[q];
+                        } else {
+                            run(j, st);   // (a symbol longer than kOff bits cannot occur)
+                        }
+                    }
+                    if (j == hi) {   // the next break past the pass, if the block goes on
+                        while (j < L && s_ed[j - 1] == 0 && s_st[j] == s_x[j - 1]) ++j;
+                        if (j < L && s_ed[j - 1] == 0) next = j;
+                    }
+                    s_wm[0] = next;
+                }
+                __syncthreads();
+                if (s_wm[0] >= L) break;
+                base = s_wm[0];
+                __syncthreads();
             }
             __syncthreads();
         }
@@ -1478,36 +1542,38 @@ __global__ __launch_bounds__(kXThreads) void k_pinf_xout(PinfArgs a) {
 // ---- 6. bytes + checksums -----------------------------------------------------------------------------------
 constexpr uint32_t kAdler = 65521;
 
-// GF(2) polynomial arithmetic modulo the CRC-32 polynomial, restated from zlib's crc32.c (multmodp /
-// x2nmodp; zlib 1.2.12+, (C) Jean-loup Gailly and Mark Adler, zlib license): a third-party algorithm, not
-// the reference's code.
-__device__ uint32_t multmodp(uint32_t a, uint32_t b) {   // a(x) b(x) mod P (reflected)
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0) break;
-        }
-        m >>= 1;
-        b = b & 1 ? (b >> 1) ^ 0xedb88320u : b >> 1;
+// GF(2) polynomial arithmetic modulo the CRC-32 polynomial (reflected: bit 31 is x^0), the operation of
+// zlib's crc32.c multmodp / x2nmodp (zlib 1.2.12+, (C) Jean-loup Gailly and Mark Adler, zlib license): a
+// third-party algorithm, not the reference's code.  Branch-free here (32 steps), and the shifts x^(8n)
+// come from a compile-time table: x^(8 n) = T0[n & 255] T1[(n >> 8) & 255] T2[..] T3[..], three products
+// instead of an exponentiation by squaring per thread (which cost k_pinf_finish 150 us on a 4 MiB gzip).
+__host__ __device__ constexpr uint32_t gf2_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int k = 0; k < 32; ++k) {
+        p ^= (a & (0x80000000u >> k)) ? b : 0u;
+        b = (b & 1u) ? (b >> 1) ^ 0xedb88320u : b >> 1;
     }
     return p;
 }
-// x^(8n) mod P
-__device__ uint32_t x8n(uint64_t n) {
-    uint32_t p = 1u << 31, x = 1u << 30;   // x^0, x^1
-    // x^(2^k) for k = 0, 1, 2 (x^8 = x^(2^3)) first
-    for (int k = 0; k < 3; ++k) x = multmodp(x, x);
-    while (n) {
-        if (n & 1) p = multmodp(x, p);
-        n >>= 1;
-        if (n) x = multmodp(x, x);
+struct X8nTable {
+    uint32_t t[4][256];
+};
+constexpr X8nTable make_x8n_table() {
+    X8nTable r{};
+    uint32_t e = 0x00800000u;   // x^8 (reflected: bit 31 - 8)
+    for (int i = 0; i < 4; ++i) {
+        r.t[i][0] = 0x80000000u;   // x^0
+        for (int j = 1; j < 256; ++j) r.t[i][j] = gf2_mul(r.t[i][j - 1], e);
+        // x^(8 * 256^(i+1)) = (x^(8 * 256^i))^256: eight squarings
+        for (int k = 0; k < 8; ++k) e = gf2_mul(e, e);
     }
-    return p;
+    return r;
 }
+__constant__ X8nTable c_x8n = make_x8n_table();
 
 __global__ __launch_bounds__(256) void k_pinf_finish(PinfArgs a) {
     __shared__ uint32_t crc_tab[256];
+    __shared__ uint32_t x8[4][256];
     __shared__ uint64_t r1[4], r2[4];
     __shared__ uint32_t rc[4];
     PinfState *st = a.state;
@@ -1518,6 +1584,7 @@ __global__ __launch_bounds__(256) void k_pinf_finish(PinfArgs a) {
         uint32_t c = t;
         for (int k = 0; k < 8; ++k) c = c & 1 ? (c >> 1) ^ 0xedb88320u : c >> 1;
         crc_tab[t] = c;
+        for (int i = 0; i < 4; ++i) x8[i][t] = c_x8n.t[i][t];
     }
     __syncthreads();
     // segment of this workgroup, slice of this thread (multiples of 4 bytes)
@@ -1543,7 +1610,11 @@ __global__ __launch_bounds__(256) void k_pinf_finish(PinfArgs a) {
     const uint64_t after = N - b1;
     uint64_t p1 = sa % kAdler, p2 = (sw % kAdler + (after % kAdler) * p1) % kAdler;
     uint32_t pc = 0;
-    if (gz) pc = b1 > b0 ? multmodp(x8n(after), c ^ 0xffffffffu) : 0u;
+    if (gz && b1 > b0) {   // the slice's CRC shifted past the bytes after it (after < 2^31)
+        const uint32_t sh = gf2_mul(gf2_mul(x8[0][after & 255], x8[1][(after >> 8) & 255]),
+                                    gf2_mul(x8[2][(after >> 16) & 255], x8[3][(after >> 24) & 255]));
+        pc = gf2_mul(sh, c ^ 0xffffffffu);
+    }
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
         p1 += (uint64_t)__shfl_xor((long long)p1, m, 64);

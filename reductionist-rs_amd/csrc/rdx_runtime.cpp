@@ -1219,8 +1219,11 @@ double thread_cpu_us() {
 // (C5: 256 MiB in + 128 MiB out).
 constexpr int kMapPieces = 8;
 
-rdx_status map_pipelined(rdx_workspace *ws, const ExecPlan &p, const uint8_t *chunk, uint64_t len, uint8_t *body,
-                         int64_t *counts) {
+rdx_status wait_event(rdx_context *ctx, PoolEntry &e, hipEvent_t ev, double budget_us);
+constexpr uint64_t kBackStage = 64ull << 10;    // rdx_workspace::h_back: small responses staged page-locked
+
+rdx_status map_pipelined(rdx_context *ctx, PoolEntry &entry, rdx_workspace *ws, const ExecPlan &p, const uint8_t *chunk,
+                         uint64_t len, uint8_t *body, int64_t *counts) {
     const KView &v = p.map.view;
     const int outer = v.ndim - 1;
     const uint64_t N = v.count[outer], inner = v.n / N;
@@ -1262,11 +1265,15 @@ rdx_status map_pipelined(rdx_workspace *ws, const ExecPlan &p, const uint8_t *ch
         if (p.map.kind != 0)
             RDX_HIP(hipMemcpyAsync(counts + a * inner, d_counts, inner * (b - a) * sizeof(int64_t), hipMemcpyDeviceToHost, sb));
     }
-    int64_t piece_counts[kMapPieces];
-    uint32_t piece_status[kMapPieces];
+    // the pieces' counts and statuses through the page-locked readback block (a copy into the stack would
+    // be a synchronous, spinning one), then the caller sleeps through the transfers (wait_event)
+    if (!ws->h_back) RDX_HIP(hipHostMalloc((void **)&ws->h_back, 16 + kBackStage, hipHostMallocDefault));
+    int64_t *const piece_counts = reinterpret_cast<int64_t *>(ws->h_back + 2);
+    uint32_t *const piece_status = reinterpret_cast<uint32_t *>(ws->h_back + 2 + kMapPieces);
     if (p.map.kind == 0) RDX_HIP(hipMemcpyAsync(piece_counts, ws->counts.p, S * sizeof(int64_t), hipMemcpyDeviceToHost, sb));
     RDX_HIP(hipMemcpyAsync(piece_status, ws->status.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, sb));
-    RDX_HIP(hipStreamSynchronize(sb));
+    RDX_HIP(hipEventRecord(ws->done_ev, sb));
+    if ((st = wait_event(ctx, entry, ws->done_ev, 20.0))) return st;
     uint32_t any = 0;
     for (int k = 0; k < S; ++k) any |= piece_status[k];
     if (any) return (rdx_status)any;
@@ -2234,7 +2241,6 @@ struct CborOut {
     uint64_t len = 0;       // encoded bytes
 };
 constexpr uint64_t kCborOneTrip = 1ull << 20;   // bounds up to this come back whole, in one round trip
-constexpr uint64_t kBackStage = 64ull << 10;    // rdx_workspace::h_back: small responses staged page-locked
 
 // operation<T>() for a chunk in host memory (app.rs:163-183): plan, bind the response buffers
 // (caller-provided or pooled), H2D, kernels, D2H; blocks until the response is in host memory.
@@ -2361,7 +2367,7 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             p.map.view.count[p.map.view.ndim - 1] >= 2 && chunk_len >= (32ull << 20) && is_pinned(chunk) &&
             is_pinned(body) && (p.map.kind == 0 || is_pinned(counts))) {
             if ((r = ensure_aux(ws))) return r;
-            return map_pipelined(ws, p, chunk, chunk_len, static_cast<uint8_t *>(body), counts);
+            return map_pipelined(ctx, entry, ws, p, chunk, chunk_len, static_cast<uint8_t *>(body), counts);
         }
         const uint8_t *src = chunk;
         // RDX_PHASES: the direct path's record (phase_sums)
