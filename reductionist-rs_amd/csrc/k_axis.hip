@@ -207,7 +207,10 @@ __device__ __forceinline__ void cols_combine(Red<T, OP> (&r)[VW], uint64_t *lds,
 template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK>
 __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
-    constexpr int kU = VW * sizeof(T) >= 16 ? 8 : 16;   // loads in flight per lane
+#ifndef RDX_AXIS_COLS_U16
+#define RDX_AXIS_COLS_U16 16
+#endif
+    constexpr int kU = VW * sizeof(T) >= 16 ? RDX_AXIS_COLS_U16 : 16;   // loads in flight per lane
     constexpr int kWaves = kBlock / 64;
     constexpr int kW = packed_words<T, OP>();
     __shared__ uint64_t lds[(kWaves - 1) * 64 * VW * kW];

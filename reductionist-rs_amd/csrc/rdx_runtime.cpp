@@ -329,8 +329,8 @@ rdx_status ensure_aux(rdx_workspace *ws) {
     return RDX_OK;
 }
 
-uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus) {
-    const uint64_t target = (uint64_t)cus * (uint64_t)tuning().blocks_per_cu;
+uint32_t pick_bpc(uint64_t tiles, uint64_t n_chunks, int cus, int per_cu = 0) {
+    const uint64_t target = (uint64_t)cus * (uint64_t)(per_cu > 0 ? per_cu : tuning().blocks_per_cu);
     uint64_t bpc = (target + n_chunks - 1) / n_chunks;
     const uint64_t min_tiles = (uint64_t)tuning().min_tiles;
     uint64_t cap = (tiles + min_tiles - 1) / min_tiles;
@@ -433,7 +433,12 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
         case Mode::AllContig: {
             KAllContig a = p.all_contig;
             const uint64_t te = p.fused ? 4096 : 16384 / p.esz;
-            a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus);
+            // unshuffled f64 sums: the compensated arithmetic is exposed at one wave per SIMD, so two
+            // workgroups per CU (8 x 64 MiB: 86-88 -> 81-82 us; an i64 sum of the same bytes is slower so,
+            // 77 -> 80 us: profiles/r05_f64_variants.jsonl)
+            const int per_cu = p.dtype == RDX_DTYPE_FLOAT64 && p.op == RDX_OP_SUM && !p.fused && p.miss.kind == 0 &&
+                               tuning().blocks_per_cu == 1 ? 2 : 0;
+            a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus, per_cu);
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
@@ -559,7 +564,10 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 const uint32_t vtop = tuning().axis_cols_vw ? vmax : std::min<uint32_t>(vmax, 2);
                 for (uint32_t vw = vtop; vw >= 1; vw /= 2) {
                     if (!vec_ok(vw)) continue;
-                    if (tuning().axis_cols_vw && vw != (uint32_t)tuning().axis_cols_vw) continue;
+                    // (tuning: a forced width the dtype cannot take is ignored)
+                    if (tuning().axis_cols_vw && (uint32_t)tuning().axis_cols_vw <= vmax &&
+                        vw != (uint32_t)tuning().axis_cols_vw)
+                        continue;
                     const uint64_t nkv = a.n_out / vw;
                     uint32_t W = 64;
                     while (W > 1 && W / 2 >= nkv) W /= 2;
