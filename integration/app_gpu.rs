@@ -40,11 +40,11 @@ pub fn operation_gpu<T: operation::Operation + operations_gpu::GpuOp>(
 ) -> Result<models::Response, ActiveStorageError> {
     // gzip / zlib: a lone request's DEFLATE stream is decoded by the whole device (k_pinflate, DESIGN.md
     // §9.1: candidate block starts, blocks and the symbols inside them decoded in parallel, then the copies
-    // resolved): a 4 MiB zlib-1 chunk in 0.59 ms against 3.6 ms for zlib on one host core, integer-valued
-    // chunks 0.6 ms against 6-10 ms (profiles/r04_pinflate_probe_xhop.jsonl, r04_bench.json).  A stream the
-    // device declines (a block chain it does not follow, e.g. many fixed-Huffman blocks, or a corrupt
-    // stream) comes back as UnsupportedOperation after the parallel attempt and is decompressed here, by the
-    // reference's own decoder (its bytes or its error).  A stream whose request states it expands more than
+    // resolved): a 4 MiB zlib-1 chunk in 0.59 ms against 3.5 ms for zlib on one host core
+    // (profiles/r05_pinflate_probe.jsonl, r05_bench.json).  A stream the device declines (a block chain it
+    // does not follow, e.g. many fixed-Huffman blocks, a corrupt stream, device memory) comes back within
+    // 0.2-0.8 ms as UnsupportedOperation (rdx_last_unsupported_reason() == RDX_UNSUPPORTED_INFLATE_DECLINED)
+    // and is decompressed here, by the reference's own decoder (its bytes or its error).  A stream whose request states it expands more than
     // 16-fold keeps the host path, as does any request when REDUCTIONIST_GPU_INFLATE=0.
     // blosc2: a chunk is hundreds of independent block streams that the device decodes in parallel
     // (k_blosc2), but a lone 4 MiB chunk takes 1.6 ms (LZ4) / 3.3 ms (zstd) there against
