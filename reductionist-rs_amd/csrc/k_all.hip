@@ -156,6 +156,31 @@ __device__ __forceinline__ void load_tiles(Tile<T, FUSED> (&x)[UNR], const uint8
     }
 }
 
+// Byte-shuffled 8-byte elements, split in time (RDX_F8_SPLIT=1, measured, off): planes 0-3 of the UNR
+// tiles, a wait until they have all landed, then planes 4-7, so a lane keeps four plane streams busy at a
+// time instead of eight.  The stand-alone probe's integer sums liked it (tools/probe_f64lds.hip: 85.3 ->
+// 79.3 us for 8 x 64 MiB) but inside this kernel it lost to the pipelined form: f64 84.8 / 82.4 vs 82.4 /
+// 82.8 us, i64 86.8 / 87.1 vs 80.7 / 81.0 (profiles/r05_f64_split.jsonl).
+#ifndef RDX_F8_SPLIT
+#define RDX_F8_SPLIT 0
+#endif
+template <typename T, int OP, bool FUSED>
+constexpr bool kSplit8 = RDX_F8_SPLIT && FUSED && sizeof(T) == 8 && !Red<T, OP>::kRank;
+
+template <typename T, bool FUSED, int UNR>
+__device__ __forceinline__ void load_tiles_split(Tile<T, FUSED> (&x)[UNR], const uint8_t *base, uint64_t plane,
+                                                 const uint64_t (&t0)[UNR]) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[u].p[k] = gld_stream<uint4>(base + (uint64_t)k * plane + t0[u] + threadIdx.x * 16);
+    __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int k = 4; k < 8; ++k) x[u].p[k] = gld_stream<uint4>(base + (uint64_t)k * plane + t0[u] + threadIdx.x * 16);
+}
+
 template <typename T, int OP, bool FUSED, int MK, bool FULL>
 __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED> &tl, const KAllContig &a, uint64_t t0,
                                              uint64_t vb, uint32_t selA, uint32_t selB) {
@@ -275,7 +300,8 @@ __device__ __forceinline__ void consume_tile(Red<T, OP> &r, const Tile<T, FUSED>
 #define RDX_PIPE_SUM 2   // byte-shuffled 8-byte sums (f64 8 x 64 MiB: 85.0 -> 83.4 us; every sum (1): f32 slower)
 #endif
 template <typename T, int OP, bool FUSED>
-constexpr bool kPipelined = Red<T, OP>::kRank || (OP == OP_SUM && (RDX_PIPE_SUM == 1 || (RDX_PIPE_SUM == 2 && FUSED && sizeof(T) == 8)));
+constexpr bool kPipelined = !kSplit8<T, OP, FUSED> &&
+                            (Red<T, OP>::kRank || (OP == OP_SUM && (RDX_PIPE_SUM == 1 || (RDX_PIPE_SUM == 2 && FUSED && sizeof(T) == 8))));
 
 template <typename T, int OP, bool FUSED, int MK, int UNR>
 __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
@@ -375,6 +401,16 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
             k += UNR;
             if (!m2) break;
         }
+    }
+    } else if constexpr (kSplit8<T, OP, FUSED>) {
+    for (; k + UNR <= nk; k += UNR) {
+        Tile<T, FUSED> x[UNR];
+        uint64_t t[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) t[u] = tile(k + u);
+        load_tiles_split<T, FUSED, UNR>(x, base, a.src.plane, t);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, t[u], vb, selA, selB);
     }
     } else {
     for (; k + UNR <= nk; k += UNR) {

@@ -238,10 +238,233 @@ __global__ __launch_bounds__(kBlock) void k_cbor([[maybe_unused]] const KCbor ar
     if (m.copy_raw) copy_share(m.out + m.c_off + m.d_len, reinterpret_cast<const uint8_t *>(m.counts), m.raw_len);
 }
 
+// ---- the staged form (round 5): pack -> scan -> place -----------------------------------------------------
+// The count array is read ONCE.  k_cbor_pack: one wavefront per tile (resident waves loop over the tiles),
+// its 32 counts per lane loaded as agg loads them (all 16 loads in flight), encoded into the wave's LDS
+// region in count order (per load round a wave-wide exclusive scan of the lanes' lengths), and the tile's
+// bytes written to a staging slot (16-byte stores); its length to records[t].  The last workgroup to finish
+// turns the lengths into exclusive offsets (+ the total).  k_cbor_place: one wavefront per tile copies the
+// staged bytes to their offset (dword stores built with v_alignbyte from 16-byte loads), the segments and
+// the trailer as k_cbor does.  Bytes moved: counts (8 B per count) once + the encoded bytes three times
+// (staged write, read, final write), against counts twice + encoded once for agg / scan / encode: less for
+// every count array whose counts take under ~3.5 bytes on average (axis = []: 0 / 1 counts, 1 byte).
+constexpr uint32_t kStageWave = (uint32_t)kCborTile * 9 + 16;   // a tile's worst case, 16-byte multiple
+static_assert(kStageWave % 16 == 0, "staging slots stay 16-byte aligned");
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, uint32_t &total) {
+    uint32_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+    }
+    total = __shfl(inc, 63, 64);
+    return inc - x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
+    const KCbor &m = *(const KCbor *)__builtin_amdgcn_kernarg_segment_ptr();
+    __shared__ uint32_t buf32[(kBlock / 64) * (kStageWave / 4)];
+    __shared__ uint32_t s_last;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t *const w8 = reinterpret_cast<uint8_t *>(buf32 + wave * (kStageWave / 4));
+    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + wave; t < m.n_tiles; t += nw) {
+        const uint64_t e0 = t * kCborTile;
+        const bool full = m.vec && e0 + kCborTile <= m.n;
+        uint4 q[kAggQ];
+        if (full) {
+#pragma unroll
+            for (int k = 0; k < kAggQ; ++k) q[k] = gld_stream<uint4>(m.counts + e0 + 2 * (lane + 64 * k));
+        } else {
+#pragma unroll
+            for (int k = 0; k < kAggQ; ++k) {
+                const uint64_t e = e0 + 2 * (lane + 64 * k);
+                const uint64_t a = e < m.n ? (uint64_t)gld<int64_t>(m.counts + e) : 0, b = e + 1 < m.n ? (uint64_t)gld<int64_t>(m.counts + e + 1) : 0;
+                q[k] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+            }
+        }
+        // round k holds counts e0 + 128 k .. + 127 (lane pairs): encode round by round.  A round whose 128
+        // counts all take one byte (0 <= v < 24: the counts of axis = [] responses, 0 / 1) is two bytes per
+        // lane at 2 * lane, one 16-bit store, no scan and no branches.
+        uint32_t base = 0;
+#pragma unroll
+        for (int k = 0; k < kAggQ; ++k) {
+            const uint64_t e = e0 + 2 * (lane + 64 * k);
+            const int64_t v0 = (int64_t)(((uint64_t)q[k].y << 32) | q[k].x), v1 = (int64_t)(((uint64_t)q[k].w << 32) | q[k].z);
+            const bool in0 = full || e < m.n, in1 = full || e + 1 < m.n;
+            const bool small = (!in0 || (uint64_t)v0 < 24) && (!in1 || (uint64_t)v1 < 24) && in0 == in1;
+            if (__builtin_amdgcn_ballot_w64(!small) == 0 && (full || e0 + 128 * (k + 1) <= m.n)) {
+                if (base & 1) {   // (wave-uniform) an odd start: two byte stores instead of an unaligned one
+                    w8[base + 2 * lane] = (uint8_t)v0;
+                    w8[base + 2 * lane + 1] = (uint8_t)v1;
+                } else {
+                    *reinterpret_cast<uint16_t *>(w8 + base + 2 * lane) = (uint16_t)((uint32_t)v0 | (uint32_t)v1 << 8);
+                }
+                base += 128;
+                continue;
+            }
+            const uint32_t l0 = in0 ? int_len(v0) : 0u, l1 = in1 ? int_len(v1) : 0u;
+            uint32_t tot;
+            const uint32_t off = base + wave_excl_scan(l0 + l1, lane, tot);
+            if (l0) put_int(w8 + off, v0);
+            if (l1) put_int(w8 + off + l0, v1);
+            base += tot;
+        }
+        // (LDS writes of this wave before its reads: the wave's own, in program order after a waitcnt)
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        uint8_t *dst = m.stage + t * kStageWave;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(w8);
+        for (uint32_t i = lane; i * 16 < base; i += 64) {
+            const uint4 x = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
+            gst<uint4>(reinterpret_cast<uint4 *>(dst + 16 * i), x);
+        }
+        if (lane == 0) put_granule(m.tagged + t, base, m.epoch);
+        __builtin_amdgcn_wave_barrier();   // the region is rewritten by this wave's next tile
+    }
+    // the last workgroup to arrive turns the lengths into exclusive offsets, records[n_tiles] = the total.
+    // The lengths travel as tagged granules and the arrival counters are relaxed (rdx_device.hpp's hand-off):
+    // a release fence per workgroup (buffer_wbl2 of the XCD's dirty L2 lines, the staged bytes among them)
+    // made this kernel 245 us for 32 Mi counts.
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = arrive_last(m.arrive, gridDim.x, blockIdx.x);
+    __syncthreads();
+    if (!s_last) return;
+    uint64_t *sm = reinterpret_cast<uint64_t *>(buf32);   // kBlock x 16 words of LDS per pass
+    uint64_t carry = 0;
+    uint32_t fault = 0;
+    constexpr uint32_t kPer = 16;
+    for (uint64_t b0 = 0; b0 < m.n_tiles; b0 += (uint64_t)kBlock * kPer) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint64_t j = b0 + k * kBlock + threadIdx.x;
+            uint64_t v = 0;
+            if (j < m.n_tiles) {
+                v = __hip_atomic_load(m.tagged + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_expect((uint32_t)(v >> 48) != m.epoch, 0)) {
+                    if (!fault) v = poll_granule(m.tagged + j, m.epoch);   // (one spin budget per lane)
+                    fault |= (uint32_t)(v >> 48) != m.epoch;
+                }
+            }
+            sm[k * kBlock + threadIdx.x] = v & kPayload;
+        }
+        __syncthreads();
+        uint64_t vv[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) vv[k] = sm[kPer * threadIdx.x + k];   // thread-contiguous runs
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) sum += vv[k];
+        const uint32_t ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        uint64_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = (uint64_t)__shfl_up((long long)x, d, 64);
+            if (ln >= (uint32_t)d) x += y;
+        }
+        __shared__ uint64_t ws4[kBlock / 64];
+        if (ln == 63) ws4[wv] = x;
+        __syncthreads();
+        uint64_t pre = carry, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kBlock / 64; ++w) {
+            pre += w < wv ? ws4[w] : 0;
+            tot += ws4[w];
+        }
+        uint64_t run = pre + x - sum;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            sm[kPer * threadIdx.x + k] = run;
+            run += vv[k];
+        }
+        carry += tot;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint64_t j = b0 + k * kBlock + threadIdx.x;
+            if (j < m.n_tiles) m.records[j] = sm[k * kBlock + threadIdx.x];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        m.records[m.n_tiles] = carry;
+        __hip_atomic_store(m.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the top counter
+    }
+    if (fault && m.status) __hip_atomic_fetch_or(m.status, (uint32_t)RDX_E_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the staged tile t -> out + c_off + offset: lane i writes destination dwords 4i..4i+3 (relative to the
+// dword-aligned base below dst) built from the staged dwords 4i-1..4i+3 (v_alignbyte), bytes at the ends
+__global__ __launch_bounds__(kBlock) void k_cbor_place(const KCbor args) {
+    const KCbor &m = *(const KCbor *)__builtin_amdgcn_kernarg_segment_ptr();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (blockIdx.x == 0) {   // A at 0, B after the body
+        for (uint32_t i = threadIdx.x; i < m.a_len; i += kBlock) gst8(m.out + i, m.fixed[i]);
+        for (uint32_t i = threadIdx.x; i < m.b_len; i += kBlock) gst8(m.out + m.b_off + i, m.fixed[m.a_len + i]);
+        if (m.n_tiles == 0) {
+            put_tail(m, 0);
+            if (threadIdx.x == 0) gst<uint64_t>(m.out_len, m.c_off + m.d_len + m.raw_len + m.f_len);
+        }
+    }
+    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + wave; t < m.n_tiles; t += nw) {
+        const uint64_t off = m.records[t], len = m.records[t + 1] - off;
+        const uint8_t *src = m.stage + t * kStageWave;
+        uint8_t *dst = m.out + m.c_off + off;
+        const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
+        uint8_t *const dst0 = dst - sh;
+        // destination dword w (0 <= w < nd) holds tile bytes [4w - sh, 4w - sh + 4)
+        const uint64_t nd = (sh + len + 3) / 4;
+        uint32_t carry = 0;   // staged dword 4i - 1 (the previous lane's last, or the previous pass's)
+        for (uint64_t i0 = 0; 4 * i0 < nd; i0 += 64) {
+            const uint64_t i = i0 + lane;
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (16 * i < len + 16) x = gld<uint4>(reinterpret_cast<const uint4 *>(src + 16 * i));   // (slot holds >= len + 16)
+            uint32_t prev = __shfl_up(x.w, 1, 64);
+            if (lane == 0) prev = carry;
+            carry = __shfl(x.w, 63, 64);
+            const uint32_t s4 = sh ? 4 - sh : 0;
+            uint32_t d[4];
+            if (sh) {
+                d[0] = __builtin_amdgcn_alignbyte(x.x, prev, s4);
+                d[1] = __builtin_amdgcn_alignbyte(x.y, x.x, s4);
+                d[2] = __builtin_amdgcn_alignbyte(x.z, x.y, s4);
+                d[3] = __builtin_amdgcn_alignbyte(x.w, x.z, s4);
+            } else {
+                d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t w = 4 * i + k;
+                const int64_t b = (int64_t)(4 * w) - (int64_t)sh;   // first tile byte of this dword
+                if (b >= 0 && (uint64_t)b + 4 <= len) {
+                    gst32(dst0 + 4 * w, d[k]);
+                } else if (b + 4 > 0 && b < (int64_t)len) {   // a partial dword: its tile bytes only
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t bj = b + j;
+                        if (bj >= 0 && bj < (int64_t)len) gst8(dst0 + 4 * w + j, (uint8_t)(d[k] >> (8 * j)));
+                    }
+                }
+            }
+        }
+        if (t == m.n_tiles - 1 && lane == 0) gst<uint64_t>(m.out_len, m.c_off + off + len + m.d_len + m.raw_len + m.f_len);
+    }
+    if (m.n_tiles && blockIdx.x == gridDim.x - 1) put_tail(m, m.records[m.n_tiles]);
+    if (m.copy_body) copy_share(m.out + m.a_len, m.body, m.body_len);
+    if (m.copy_raw) copy_share(m.out + m.c_off + m.d_len, reinterpret_cast<const uint8_t *>(m.counts), m.raw_len);
+}
+
 }  // namespace
 
 hipError_t launch_cbor(const KCbor &m, uint32_t blocks, hipStream_t s) {
     if (blocks < m.n_tiles || blocks == 0) return hipErrorInvalidValue;
+    if (m.staged) {   // pack -> place (the scan inside pack's last workgroup)
+        const uint32_t waves_grid = std::max<uint32_t>(1, std::min<uint32_t>((m.n_tiles + 3) / 4, 2048));
+        if (m.n_tiles) hipLaunchKernelGGL(k_cbor_pack, dim3(waves_grid), dim3(kBlock), 0, s, m);
+        const uint32_t pgrid = std::max<uint32_t>({1, std::min<uint32_t>((m.n_tiles + 3) / 4, 2048), blocks / 4});
+        hipLaunchKernelGGL(k_cbor_place, dim3(pgrid), dim3(kBlock), 0, s, m);
+        return hipGetLastError();
+    }
     if (m.n_tiles) {
         hipLaunchKernelGGL(k_cbor_agg, dim3(std::min<uint32_t>((m.n_tiles + 3) / 4, 2048)), dim3(kBlock), 0, s, m);
         hipLaunchKernelGGL(k_cbor_scan, dim3(1), dim3(kScanThreads), 0, s, m);
@@ -249,5 +472,7 @@ hipError_t launch_cbor(const KCbor &m, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(k_cbor, dim3(blocks), dim3(kBlock), 0, s, m);
     return hipGetLastError();
 }
+
+uint64_t cbor_stage_bytes(uint64_t n_tiles) { return n_tiles * kStageWave; }
 
 }  // namespace rdx

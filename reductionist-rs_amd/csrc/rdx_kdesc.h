@@ -193,6 +193,12 @@ struct KCbor {
     uint64_t raw_len;           // bytes of the count_as_bytes payload between D and F (copied by the host)
     uint64_t *out_len;          // device: total encoded length
     uint64_t *records;          // one word per tile: k_cbor_agg's encoded length, k_cbor_scan's offset
+                                //   (staged form: n_tiles + 1 words, k_cbor_pack's lengths -> offsets + total)
+    uint8_t *stage;             // staged form: tile t's encoded bytes at stage + t * kStageWave (k_cbor.hip)
+    uint32_t *arrive;           // staged form: k_cbor_pack's sharded arrival counters (self-resetting)
+    uint64_t *tagged;           // staged form: tile t's length as a tagged granule (the hand-off of rdx_device.hpp)
+    uint32_t staged, epoch;
+    uint32_t *status;           // staged form: RDX_E_DEVICE when a tile length never arrived (a device fault)
     const uint8_t *body;        // the response body (device), copied in-kernel when copy_body
     uint64_t body_len;
     uint32_t n_tiles, vec;

@@ -88,6 +88,7 @@ struct Tuning {
     int host_read_kib = env_int("RDX_HOST_READ_KIB", 4096);            // pinned chunks up to this: the kernel reads them over PCIe
     int host_read_wgs = env_int("RDX_HOST_READ_WGS", 8);               // ... with this many workgroups (few: profiles/r05_hread_probe)
     int phases = env_int("RDX_PHASES", 0);                             // phase statistics of the direct path (stderr at destroy)
+    int cbor_staged = env_int("RDX_CBOR_STAGED", 1);                   // CBOR count arrays: pack -> place (0: agg / scan / encode)
     int pinflate = env_int("RDX_PINFLATE", 1);                         // a lone gzip / zlib stream: k_pinflate
     int pinflate_min = env_int("RDX_PINFLATE_MIN_BYTES", 1024);        // ... from this many compressed bytes
     int pinflate_prof = env_int("RDX_PINF_PROF", 0);                   // tuning: per-workgroup times to stderr
@@ -164,6 +165,7 @@ struct rdx_workspace {
     DevBuf<uint32_t> psrc;
     DevBuf<uint64_t> pprof;
     DevBuf<uint64_t> cbor_rec;   // k_cbor_agg / k_cbor_scan: per-tile lengths, then offsets
+    DevBuf<uint8_t> cbor_stage;  // k_cbor_pack: the tiles' encoded bytes (the staged form)
     PinfState *pinf_back = nullptr;
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
@@ -1028,6 +1030,7 @@ void destroy_workspace(rdx_workspace *ws) {
     fr(ws->psrc.p);
     fr(ws->pprof.p);
     fr(ws->cbor_rec.p);
+    fr(ws->cbor_stage.p);
     if (ws->pinned) (void)hipHostFree(ws->pinned);
     if (ws->upload_done) (void)hipEventDestroy(ws->upload_done);
     if (ws->copy_ev) (void)hipEventDestroy(ws->copy_ev);
@@ -1089,8 +1092,25 @@ rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const v
     // tiles with the next one prefetched: 142 vs 136 us for 32 Mi counts, profiles/r04_cbor_variants.jsonl)
     const uint32_t blocks = (uint32_t)std::max<uint64_t>({1, tiles, copy_blocks});
     rdx_status st;
+    // the staged form (k_cbor_pack / k_cbor_place: the counts read once) unless RDX_CBOR_STAGED=0 or its
+    // scratch (18 KiB per tile of 2048 counts) cannot be had
+    m.staged = m.n_tiles && tuning().cbor_staged ? 1u : 0u;
+    if (m.staged) {
+        // tile lengths as tagged granules in the hand-off records, the sharded arrival counters
+        if (ensure(ws, ws->cbor_stage, cbor_stage_bytes(m.n_tiles), s) || ensure(ws, ws->partials, m.n_tiles, s, true) ||
+            ensure(ws, ws->tickets, kTicketWords, s, true)) {
+            (void)hipGetLastError();
+            m.staged = 0;
+        } else {
+            m.stage = ws->cbor_stage.p;
+            m.tagged = ws->partials.p;
+            m.arrive = ws->tickets.p;
+            m.status = d_status;
+            if ((st = next_epoch(ws, s, m.epoch))) return st;
+        }
+    }
     if (m.n_tiles) {
-        if ((st = ensure(ws, ws->cbor_rec, m.n_tiles, s))) return st;   // (not the tagged hand-off records)
+        if ((st = ensure(ws, ws->cbor_rec, m.n_tiles + 1, s))) return st;   // (not the tagged hand-off records)
         m.records = ws->cbor_rec.p;
     }
     if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));

@@ -9,7 +9,7 @@ Infinity Cache, one kernel family per case so a dispatch's kernel name identifie
   axis0_cols   k_axis_cols    f32 [4096,4096] axis 0 sum                             (64 MiB read)
   axis1_rows   k_axis_rows    f32 [4096,4096] axis 1 sum                             (64 MiB read)
   mixed_multi  k_multi        10 x C1 + 10 x C3 requests in one launch               (97 MB read)
-  cbor_counts  k_cbor         32 Mi counts (0/1) -> CBOR integers, no body            (256 MiB read, 32 MiB written)
+  cbor_counts  k_cbor_pack + k_cbor_place  32 Mi counts (0/1) -> CBOR integers, no body (256 MiB read, 32 MiB written)
 
 tools/pmc_traffic.py turns the counter CSVs into profiles/r02_pmc_<case>.json."""
 import ctypes as C

@@ -25,6 +25,10 @@ CASES = {
     "k_multi": ("mixed_multi", 10 * ((4 << 20) + C3_NSEL * 8), 0),
     "k_cbor": ("cbor_counts", 8 * (512 * 256 * 256), 512 * 256 * 256),
     "k_cbor_agg": ("cbor_agg", 8 * (512 * 256 * 256), 0),   # (round 4: the tile lengths' pass re-reads the counts)
+    # round 5's staged form: the counts read once by k_cbor_pack (the encoded bytes staged), k_cbor_place
+    # moves the staged bytes to their offsets
+    "k_cbor_pack": ("cbor_pack", 8 * (512 * 256 * 256), 512 * 256 * 256),
+    "k_cbor_place": ("cbor_place", 512 * 256 * 256, 512 * 256 * 256),
 }
 
 

@@ -18,4 +18,5 @@ class _A:
 
 
 cx = bench.Ctx(torch, dist, _A(), 1, 0, 0)
-print(json.dumps({"bpcu": os.environ.get("RDX_CBOR_BLOCKS_PER_CU", "default"), "r": bench.leg_cbor(cx, False)}), flush=True)
+print(json.dumps({"bpcu": os.environ.get("RDX_CBOR_BLOCKS_PER_CU", "default"), "staged": os.environ.get("RDX_CBOR_STAGED", "1"),
+                  "r": bench.leg_cbor(cx, False)}), flush=True)
