@@ -239,17 +239,22 @@ __global__ __launch_bounds__(kBlock) void k_cbor([[maybe_unused]] const KCbor ar
 }
 
 // ---- the staged form (round 5): pack -> scan -> place -----------------------------------------------------
-// The count array is read ONCE.  k_cbor_pack: one wavefront per tile (resident waves loop over the tiles),
-// its 32 counts per lane loaded as agg loads them (all 16 loads in flight), encoded into the wave's LDS
-// region in count order (per load round a wave-wide exclusive scan of the lanes' lengths), and the tile's
-// bytes written to a staging slot (16-byte stores); its length to records[t].  The last workgroup to finish
-// turns the lengths into exclusive offsets (+ the total).  k_cbor_place: one wavefront per tile copies the
-// staged bytes to their offset (dword stores built with v_alignbyte from 16-byte loads), the segments and
-// the trailer as k_cbor does.  Bytes moved: counts (8 B per count) once + the encoded bytes three times
-// (staged write, read, final write), against counts twice + encoded once for agg / scan / encode: less for
-// every count array whose counts take under ~3.5 bytes on average (axis = []: 0 / 1 counts, 1 byte).
+// The count array is read ONCE.  k_cbor_pack: workgroup g owns the contiguous tiles [g T, g T + T) and its
+// waves take them in turn; a tile's 32 counts per lane are loaded as agg loads them (all 16 loads in
+// flight) and encoded straight into the tile's staging slot in global memory, round by round (per load
+// round a wave-wide exclusive scan of the lanes' lengths; a round whose 128 counts all take one byte — the
+// counts of axis = [] responses — is one 16-bit store per lane, no scan).  The workgroup then scans its
+// tiles' lengths (records[t] = local offset << 32 | length) and publishes its total as a tagged granule;
+// the last workgroup to arrive scans the G totals into group offsets (records[n_tiles + 1 + g]) and the
+// grand total (records[n_tiles]).  k_cbor_place: one wavefront per tile copies the staged bytes to their
+// offset (dword stores built with v_alignbyte from 16-byte loads), the segments and the trailer as k_cbor
+// does.  Bytes moved: counts (8 B per count) once + the encoded bytes three times (staged write, read, final
+// write), against counts twice + encoded once for agg / scan / encode: less for every count array whose
+// counts take under ~3.5 bytes on average.  (Records: profiles/r05_cbor_staged.jsonl.)
 constexpr uint32_t kStageWave = (uint32_t)kCborTile * 9 + 16;   // a tile's worst case, 16-byte multiple
 static_assert(kStageWave % 16 == 0, "staging slots stay 16-byte aligned");
+constexpr uint32_t kPackMaxT = 1024;   // tiles per workgroup (host: n_tiles <= 2048 * 1024, i.e. < 2^32 counts)
+constexpr uint32_t kPackMaxG = 2048;   // workgroups
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, uint32_t &total) {
     uint32_t inc = x;
@@ -262,15 +267,30 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, ui
     return inc - x;
 }
 
+__device__ __forceinline__ uint32_t put_int_global(uint8_t *p, int64_t v) {
+    const uint8_t major = v < 0 ? 0x20 : 0x00;
+    const uint64_t u = v < 0 ? ~(uint64_t)v : (uint64_t)v;
+    if (u < 24) {
+        gst8(p, (uint8_t)(major | u));
+        return 1;
+    }
+    const int n = u <= 0xffu ? 1 : u <= 0xffffu ? 2 : u <= 0xffffffffull ? 4 : 8;
+    gst8(p, (uint8_t)(major | (n == 1 ? 24 : n == 2 ? 25 : n == 4 ? 26 : 27)));
+    for (int i = 0; i < n; ++i) gst8(p + 1 + i, (uint8_t)(u >> (8 * (n - 1 - i))));
+    return 1u + (uint32_t)n;
+}
+
 __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
     const KCbor &m = *(const KCbor *)__builtin_amdgcn_kernarg_segment_ptr();
-    __shared__ uint32_t buf32[(kBlock / 64) * (kStageWave / 4)];
+    __shared__ uint32_t s_len[kPackMaxT];
+    __shared__ uint64_t s_tot[kBlock / 64];
     __shared__ uint32_t s_last;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint8_t *const w8 = reinterpret_cast<uint8_t *>(buf32 + wave * (kStageWave / 4));
-    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + wave; t < m.n_tiles; t += nw) {
-        const uint64_t e0 = t * kCborTile;
+    const uint32_t T = m.tpg, g = blockIdx.x;
+    const uint64_t t0 = (uint64_t)g * T;
+    const uint32_t nt = (uint32_t)(t0 < m.n_tiles ? std::min<uint64_t>(T, m.n_tiles - t0) : 0);
+    for (uint32_t i = wave; i < nt; i += kBlock / 64) {
+        const uint64_t t = t0 + i, e0 = t * kCborTile;
         const bool full = m.vec && e0 + kCborTile <= m.n;
         uint4 q[kAggQ];
         if (full) {
@@ -284,9 +304,7 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
                 q[k] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
             }
         }
-        // round k holds counts e0 + 128 k .. + 127 (lane pairs): encode round by round.  A round whose 128
-        // counts all take one byte (0 <= v < 24: the counts of axis = [] responses, 0 / 1) is two bytes per
-        // lane at 2 * lane, one 16-bit store, no scan and no branches.
+        uint8_t *const dst = m.stage + t * kStageWave;
         uint32_t base = 0;
 #pragma unroll
         for (int k = 0; k < kAggQ; ++k) {
@@ -296,10 +314,10 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
             const bool small = (!in0 || (uint64_t)v0 < 24) && (!in1 || (uint64_t)v1 < 24) && in0 == in1;
             if (__builtin_amdgcn_ballot_w64(!small) == 0 && (full || e0 + 128 * (k + 1) <= m.n)) {
                 if (base & 1) {   // (wave-uniform) an odd start: two byte stores instead of an unaligned one
-                    w8[base + 2 * lane] = (uint8_t)v0;
-                    w8[base + 2 * lane + 1] = (uint8_t)v1;
+                    gst8(dst + base + 2 * lane, (uint8_t)v0);
+                    gst8(dst + base + 2 * lane + 1, (uint8_t)v1);
                 } else {
-                    *reinterpret_cast<uint16_t *>(w8 + base + 2 * lane) = (uint16_t)((uint32_t)v0 | (uint32_t)v1 << 8);
+                    *(__attribute__((address_space(1))) uint16_t *)(dst + base + 2 * lane) = (uint16_t)((uint32_t)v0 | (uint32_t)v1 << 8);
                 }
                 base += 128;
                 continue;
@@ -307,87 +325,73 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
             const uint32_t l0 = in0 ? int_len(v0) : 0u, l1 = in1 ? int_len(v1) : 0u;
             uint32_t tot;
             const uint32_t off = base + wave_excl_scan(l0 + l1, lane, tot);
-            if (l0) put_int(w8 + off, v0);
-            if (l1) put_int(w8 + off + l0, v1);
+            if (l0) put_int_global(dst + off, v0);
+            if (l1) put_int_global(dst + off + l0, v1);
             base += tot;
         }
-        // (LDS writes of this wave before its reads: the wave's own, in program order after a waitcnt)
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-        __builtin_amdgcn_wave_barrier();
-        uint8_t *dst = m.stage + t * kStageWave;
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(w8);
-        for (uint32_t i = lane; i * 16 < base; i += 64) {
-            const uint4 x = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
-            gst<uint4>(reinterpret_cast<uint4 *>(dst + 16 * i), x);
-        }
-        if (lane == 0) put_granule(m.tagged + t, base, m.epoch);
-        __builtin_amdgcn_wave_barrier();   // the region is rewritten by this wave's next tile
+        if (lane == 0) s_len[i] = base;
     }
-    // the last workgroup to arrive turns the lengths into exclusive offsets, records[n_tiles] = the total.
-    // The lengths travel as tagged granules and the arrival counters are relaxed (rdx_device.hpp's hand-off):
-    // a release fence per workgroup (buffer_wbl2 of the XCD's dirty L2 lines, the staged bytes among them)
-    // made this kernel 245 us for 32 Mi counts.
     __syncthreads();
-    if (threadIdx.x == 0) s_last = arrive_last(m.arrive, gridDim.x, blockIdx.x);
+    // this workgroup's tiles: local exclusive offsets (wave 0, 64 tiles per step) and the group total
+    if (wave == 0) {
+        uint64_t run = 0;
+        for (uint32_t i0 = 0; i0 < nt; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint32_t len = i < nt ? s_len[i] : 0u;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan(len, lane, tot);
+            if (i < nt) m.records[t0 + i] = (run + ex) << 32 | len;
+            run += tot;
+        }
+        if (lane == 0) {
+            put_granule(m.tagged + g, run, m.epoch);
+            s_last = arrive_last(m.arrive, gridDim.x, g);
+        }
+    }
     __syncthreads();
     if (!s_last) return;
-    uint64_t *sm = reinterpret_cast<uint64_t *>(buf32);   // kBlock x 16 words of LDS per pass
-    uint64_t carry = 0;
+    // the last workgroup: group offsets (thread-contiguous runs of kPer totals, tagged granules polled)
+    constexpr uint32_t kPer = kPackMaxG / kBlock;
+    const uint32_t G = gridDim.x;
+    uint64_t v[kPer], sum = 0;
     uint32_t fault = 0;
-    constexpr uint32_t kPer = 16;
-    for (uint64_t b0 = 0; b0 < m.n_tiles; b0 += (uint64_t)kBlock * kPer) {
 #pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            const uint64_t j = b0 + k * kBlock + threadIdx.x;
-            uint64_t v = 0;
-            if (j < m.n_tiles) {
-                v = __hip_atomic_load(m.tagged + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_expect((uint32_t)(v >> 48) != m.epoch, 0)) {
-                    if (!fault) v = poll_granule(m.tagged + j, m.epoch);   // (one spin budget per lane)
-                    fault |= (uint32_t)(v >> 48) != m.epoch;
-                }
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t j = threadIdx.x * kPer + k;
+        uint64_t x = 0;
+        if (j < G) {
+            x = __hip_atomic_load(m.tagged + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_expect((uint32_t)(x >> 48) != m.epoch, 0)) {
+                if (!fault) x = poll_granule(m.tagged + j, m.epoch);   // (one spin budget per lane)
+                fault |= (uint32_t)(x >> 48) != m.epoch;
             }
-            sm[k * kBlock + threadIdx.x] = v & kPayload;
         }
-        __syncthreads();
-        uint64_t vv[kPer], sum = 0;
+        v[k] = x & kPayload;
+        sum += v[k];
+    }
+    uint64_t x = sum;
 #pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) vv[k] = sm[kPer * threadIdx.x + k];   // thread-contiguous runs
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = (uint64_t)__shfl_up((long long)x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_tot[wave] = x;
+    __syncthreads();
+    uint64_t pre = 0, all = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) sum += vv[k];
-        const uint32_t ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        uint64_t x = sum;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+        pre += w < wave ? s_tot[w] : 0;
+        all += s_tot[w];
+    }
+    uint64_t run = pre + x - sum;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = (uint64_t)__shfl_up((long long)x, d, 64);
-            if (ln >= (uint32_t)d) x += y;
-        }
-        __shared__ uint64_t ws4[kBlock / 64];
-        if (ln == 63) ws4[wv] = x;
-        __syncthreads();
-        uint64_t pre = carry, tot = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kBlock / 64; ++w) {
-            pre += w < wv ? ws4[w] : 0;
-            tot += ws4[w];
-        }
-        uint64_t run = pre + x - sum;
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            sm[kPer * threadIdx.x + k] = run;
-            run += vv[k];
-        }
-        carry += tot;
-        __syncthreads();
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            const uint64_t j = b0 + k * kBlock + threadIdx.x;
-            if (j < m.n_tiles) m.records[j] = sm[k * kBlock + threadIdx.x];
-        }
-        __syncthreads();
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t j = threadIdx.x * kPer + k;
+        if (j < G) m.records[m.n_tiles + 1 + j] = run;
+        run += v[k];
     }
     if (threadIdx.x == 0) {
-        m.records[m.n_tiles] = carry;
+        m.records[m.n_tiles] = all;
         __hip_atomic_store(m.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the top counter
     }
     if (fault && m.status) __hip_atomic_fetch_or(m.status, (uint32_t)RDX_E_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -408,7 +412,8 @@ __global__ __launch_bounds__(kBlock) void k_cbor_place(const KCbor args) {
     }
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + wave; t < m.n_tiles; t += nw) {
-        const uint64_t off = m.records[t], len = m.records[t + 1] - off;
+        const uint64_t r = m.records[t];
+        const uint64_t off = m.records[m.n_tiles + 1 + t / m.tpg] + (r >> 32), len = r & 0xffffffffu;
         const uint8_t *src = m.stage + t * kStageWave;
         uint8_t *dst = m.out + m.c_off + off;
         const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
@@ -459,8 +464,9 @@ __global__ __launch_bounds__(kBlock) void k_cbor_place(const KCbor args) {
 hipError_t launch_cbor(const KCbor &m, uint32_t blocks, hipStream_t s) {
     if (blocks < m.n_tiles || blocks == 0) return hipErrorInvalidValue;
     if (m.staged) {   // pack -> place (the scan inside pack's last workgroup)
-        const uint32_t waves_grid = std::max<uint32_t>(1, std::min<uint32_t>((m.n_tiles + 3) / 4, 2048));
-        if (m.n_tiles) hipLaunchKernelGGL(k_cbor_pack, dim3(waves_grid), dim3(kBlock), 0, s, m);
+        if (m.tpg == 0 || m.tpg > kPackMaxT || (uint64_t)m.tpg * kPackMaxG < m.n_tiles) return hipErrorInvalidValue;
+        const uint32_t groups = (m.n_tiles + m.tpg - 1) / m.tpg;
+        if (m.n_tiles) hipLaunchKernelGGL(k_cbor_pack, dim3(groups), dim3(kBlock), 0, s, m);
         const uint32_t pgrid = std::max<uint32_t>({1, std::min<uint32_t>((m.n_tiles + 3) / 4, 2048), blocks / 4});
         hipLaunchKernelGGL(k_cbor_place, dim3(pgrid), dim3(kBlock), 0, s, m);
         return hipGetLastError();
@@ -474,5 +480,9 @@ hipError_t launch_cbor(const KCbor &m, uint32_t blocks, hipStream_t s) {
 }
 
 uint64_t cbor_stage_bytes(uint64_t n_tiles) { return n_tiles * kStageWave; }
+uint32_t cbor_pack_tpg(uint64_t n_tiles) {   // tiles per k_cbor_pack workgroup: >= 4 (a tile per wave), <= 2048 groups
+    const uint64_t t = std::max<uint64_t>(4, (n_tiles + kPackMaxG - 1) / kPackMaxG);
+    return t <= kPackMaxT ? (uint32_t)t : 0u;   // 0: too many tiles for the staged form
+}
 
 }  // namespace rdx

@@ -198,6 +198,7 @@ struct KCbor {
     uint32_t *arrive;           // staged form: k_cbor_pack's sharded arrival counters (self-resetting)
     uint64_t *tagged;           // staged form: tile t's length as a tagged granule (the hand-off of rdx_device.hpp)
     uint32_t staged, epoch;
+    uint32_t tpg, pad_;         // staged form: tiles per k_cbor_pack workgroup (records[n_tiles + 1 + g]: group offsets)
     uint32_t *status;           // staged form: RDX_E_DEVICE when a tile length never arrived (a device fault)
     const uint8_t *body;        // the response body (device), copied in-kernel when copy_body
     uint64_t body_len;

@@ -21,6 +21,7 @@ hipError_t launch_unshuffle(const uint8_t *in, uint8_t *out, uint64_t len, uint6
 hipError_t launch_multi(const KMultiArgs &m, uint32_t blocks, hipStream_t s);
 hipError_t launch_cbor(const KCbor &m, uint32_t blocks, hipStream_t s);
 uint64_t cbor_stage_bytes(uint64_t n_tiles);   // the staged form's scratch (k_cbor.hip)
+uint32_t cbor_pack_tpg(uint64_t n_tiles);      // ... its tiles per k_cbor_pack workgroup
 // k_inflate.hip: gzip / zlib streams (format = rdx_compression), one wavefront per stream
 hipError_t launch_inflate(uint32_t format, const uint8_t *const *d_in, const uint64_t *d_in_len, uint64_t n,
                           uint8_t *d_out, uint64_t cap, uint64_t *d_out_len, uint32_t *d_err, hipStream_t s);

@@ -1097,7 +1097,8 @@ rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const v
     m.staged = m.n_tiles && tuning().cbor_staged ? 1u : 0u;
     if (m.staged) {
         // tile lengths as tagged granules in the hand-off records, the sharded arrival counters
-        if (ensure(ws, ws->cbor_stage, cbor_stage_bytes(m.n_tiles), s) || ensure(ws, ws->partials, m.n_tiles, s, true) ||
+        m.tpg = cbor_pack_tpg(m.n_tiles);
+        if (!m.tpg || ensure(ws, ws->cbor_stage, cbor_stage_bytes(m.n_tiles), s) || ensure(ws, ws->partials, 2048, s, true) ||
             ensure(ws, ws->tickets, kTicketWords, s, true)) {
             (void)hipGetLastError();
             m.staged = 0;
@@ -1110,7 +1111,8 @@ rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const v
         }
     }
     if (m.n_tiles) {
-        if ((st = ensure(ws, ws->cbor_rec, m.n_tiles + 1, s))) return st;   // (not the tagged hand-off records)
+        // (not the tagged hand-off records; the staged form: + 1 total + the group offsets)
+        if ((st = ensure(ws, ws->cbor_rec, m.n_tiles + 1 + (m.staged ? 2048 : 0), s))) return st;
         m.records = ws->cbor_rec.p;
     }
     if (d_status) RDX_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), s));
