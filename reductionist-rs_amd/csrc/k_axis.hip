@@ -103,10 +103,24 @@ __device__ __forceinline__ void fold_in(Red<T, OP> &r, const KMissing &miss, T x
     else r.add(x, [&]() { return rank; });
 }
 
+// Without a missing predicate every element is counted: the loops add the value only and count the
+// elements once per load (one 64-bit add per load instead of one per element and output).
+template <typename T, int OP, int MK>
+__device__ __forceinline__ void fold_value(Red<T, OP> &r, const KMissing &miss, T x, int64_t rank) {
+    if constexpr (MK == MK_NONE) {
+        if constexpr (OP != OP_COUNT) r.add_value(x, [&]() { return rank; });
+    } else {
+        fold_in<T, OP, MK>(r, miss, x, rank);
+    }
+}
+
 template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK>
 __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
-    constexpr int kU = 4;
+#ifndef RDX_AXIS_ROWS_U
+#define RDX_AXIS_ROWS_U 4
+#endif
+    constexpr int kU = RDX_AXIS_ROWS_U;   // loads in flight per lane
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t L = a.group, G = 64 / L;        // lanes per item, items per wave pass
     const uint32_t l = lane & (L - 1), g = lane / L;
@@ -143,7 +157,8 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
                 T x[VW];
                 raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) fold_in<T, OP, MK>(r, a.miss, x[j], rk[u] + (int64_t)j * rg.s0);
+                for (int j = 0; j < VW; ++j) fold_value<T, OP, MK>(r, a.miss, x[j], rk[u] + (int64_t)j * rg.s0);
+                if constexpr (MK == MK_NONE) r.cnt += VW;
             }
         }
         group_reduce(r, L);
@@ -231,6 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
     Red<T, OP> r[VW];
 #pragma unroll
     for (int j = 0; j < VW; ++j) r[j].init();
+    int64_t rows = 0;   // (MK_NONE: the elements each output of this lane folded)
     if (active) {
         const uint64_t step = (uint64_t)kWaves * R;      // rows between a lane's consecutive loads
         for (uint64_t r0 = r_lo + wave * R + rsub; r0 < r_hi; r0 += step * kU) {
@@ -250,9 +266,14 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
                 T x[VW];
                 raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) fold_in<T, OP, MK>(r[j], a.miss, x[j], rk[u]);
+                for (int j = 0; j < VW; ++j) fold_value<T, OP, MK>(r[j], a.miss, x[j], rk[u]);
+                if constexpr (MK == MK_NONE) ++rows;
             }
         }
+    }
+    if constexpr (MK == MK_NONE) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) r[j].cnt = rows;
     }
     cols_combine<T, OP, VW>(r, lds, W);
 #if RDX_PROBES

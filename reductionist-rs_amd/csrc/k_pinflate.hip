@@ -681,6 +681,96 @@ struct WinStream {   // bit reads from the staged window only (positions inside 
     }
 };
 
+// The survivors' header test with the code-length code expanded first into a 128-entry table (one byte per
+// 7-bit MSB-first peek: symbol | length << 5) in the lane's own LDS slot, so a code-length symbol is one
+// table read instead of header_lengths' compares and packed lookups (~170 instructions per symbol with the
+// exec-mask bookkeeping, and the workgroup holding a real header walks ~250 of them).  Same rules and
+// result as dyn_candidate_rest.
+#ifndef RDX_PINF_FIND_LUT
+#define RDX_PINF_FIND_LUT 1
+#endif
+typedef __attribute__((address_space(3))) uint8_t *lds_u8p;
+constexpr uint32_t kFindLutStride = 132;   // bytes per lane's table: 33 dwords, lanes in different banks
+static_assert(kFindList * 4 >= 256 * kFindLutStride, "the survivor list's memory holds 256 tables");
+
+__device__ bool dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb, lds_u8p lut) {
+    constexpr int kField[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};   // symbol -> field
+    const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
+    uint64_t pos = p + 17 + 3 * nc;
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 19; ++i) cnt += 1ull << (8 * ((cb >> (3 * i)) & 7));
+    int left = 1;
+    uint64_t Sp = 0, Op = 0;
+    uint32_t st = 0, of = 0;
+#pragma unroll
+    for (int l = 1; l < 8; ++l) {
+        const uint32_t c = (uint32_t)(cnt >> (8 * l)) & 0xff;
+        left = (left << 1) - (int)c;
+        Sp |= (uint64_t)st << (8 * l);
+        Op |= (uint64_t)of << (8 * l);
+        st += c << (7 - l);
+        of += c;
+    }
+    if (left != 0) return false;
+    uint64_t pk0 = 0, pk1 = 0, run = 0;
+#pragma unroll
+    for (int sy = 0; sy < 19; ++sy) {
+        const uint32_t l = (uint32_t)(cb >> (3 * kField[sy])) & 7;
+        const uint32_t r = (uint32_t)((Op + run) >> (8 * l)) & 0xff;
+        run += l ? 1ull << (8 * l) : 0;
+        pk0 |= l && r < 12 ? (uint64_t)sy << (5 * r) : 0;
+        pk1 |= l && r >= 12 ? (uint64_t)sy << (5 * (r - 12)) : 0;
+    }
+    const uint64_t E = Sp >> 16;
+    for (uint32_t j = 0; j < 128; ++j) {
+        uint32_t len = 1;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) len += ((uint32_t)(E >> (8 * l)) & 0xff) <= j ? 1u : 0u;
+        const uint32_t Sl = (uint32_t)(Sp >> (8 * len)) & 0xff, Ol = (uint32_t)(Op >> (8 * len)) & 0xff;
+        const uint32_t si = Ol + ((j - Sl) >> (7 - len));
+        const uint32_t sym = (uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31;
+        lut[j] = (uint8_t)(sym | len << 5);
+    }
+    const uint32_t total = nl + nd;
+    uint64_t nxt = pos >> 5;
+    uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
+    uint32_t bc = 64 - (uint32_t)(pos & 31);
+    nxt += 2;
+    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0;
+    bool eob = false, bad = false;
+    uint32_t w = S.ld(nxt);
+    while (!bad && idx < total) {
+        const bool need = bc < 32;
+        bb |= need ? (uint64_t)w << (bc & 63) : 0;
+        bc += need ? 32 : 0;
+        nxt += need ? 1 : 0;
+        if (need) w = S.ld(nxt);
+        const uint32_t e = lut[__builtin_bitreverse32((uint32_t)bb) >> 25];
+        const uint32_t len = e >> 5, sym = e & 31;
+        const uint32_t x = (uint32_t)(bb >> len);
+        const bool s16 = sym == 16, s17 = sym == 17, s18 = sym == 18;
+        const uint32_t rep = s16 ? 3 + (x & 3) : s17 ? 3 + (x & 7) : s18 ? 11 + (x & 127) : 1;
+        const uint32_t used = len + (s16 ? 2 : s17 ? 3 : s18 ? 7 : 0);
+        const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
+        bad |= (s16 && idx == 0) || idx + rep > total;
+        const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
+        eob |= idx <= 256 && 256 < idx + nlit && val != 0;
+        const uint32_t sh = 15 - val;
+        kl += val ? nlit << sh : 0u;
+        kd += val ? ndst << sh : 0u;
+        used_d += val ? ndst : 0u;
+        bad |= kl > (1u << 15) || kd > (1u << 15);
+        pos += used;
+        bb >>= used;
+        bc -= used;
+        idx += rep;
+        prev = val;
+        bad |= pos > end_bits;
+    }
+    return !bad && eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
+}
+
 __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     __shared__ uint32_t win[kFindWin];
     __shared__ uint32_t list[kFindList];   // survivors: bit offsets from 8 * q0
@@ -774,7 +864,28 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
         if (n >= 256 || r + 1 == kFindBytes / 1024) {
             // the survivors' full header test, one per lane
             if (prof) ts2 = wall_clock64();
-            for (uint32_t i = t; i < n; i += 256) {
+#ifndef RDX_PINF_FIND_HDR
+#define RDX_PINF_FIND_HDR 1   // tuning probes: 0 skips the survivors' header decode (tools/probe_pinf_find)
+#endif
+#ifndef RDX_PINF_FIND_SPREAD
+#define RDX_PINF_FIND_SPREAD 0   // tuning probes: 1 deals the survivors to the 4 waves round-robin
+#endif
+            if (RDX_PINF_FIND_LUT && RDX_PINF_FIND_HDR && n <= 256) {
+                // one survivor per thread; the list's memory becomes the threads' tables once each has its
+                // position
+                const uint32_t mine = t < n ? list[t] : 0u;
+                __syncthreads();
+                if (t < n) {
+                    const uint64_t p = 8 * q0 + mine;
+                    const uint32_t h = S.at(p);
+                    const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
+                                        ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
+                    if (dyn_candidate_lut(S, p, a.end_bits, h, cb, (lds_u8p)list + t * kFindLutStride)) push(p << 2 | 2);
+                }
+            } else
+            for (uint32_t i0 = t; RDX_PINF_FIND_HDR && i0 < n + 255; i0 += 256) {
+                const uint32_t i = RDX_PINF_FIND_SPREAD ? (i0 - t) + (t & 63) * 4 + (t >> 6) : i0;
+                if (i >= n) continue;
                 const uint64_t p = 8 * q0 + list[i];
                 const uint32_t h = S.at(p);
                 const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &

@@ -264,6 +264,20 @@ def test_declined_stream_costs_little(torch, workspace, comp):
             assert s is fixed and err == 0 and path == PATH_PARALLEL
 
 
+def test_candidate_overflow_declines(torch, workspace):
+    """More block-start candidates than one stream's list holds (kPinfMaxCand, 4096): a Z_HUFFMAN_ONLY stream
+    at memLevel 9 writes a block per 32 K literals, so 160 MiB is ~5100 blocks.  The parallel path declines it (the caller's
+    host decoder answers) quickly instead of failing or taking the sequential decoder."""
+    import time
+    b = np.random.default_rng(77).integers(0, 16, 160 << 20, dtype=np.uint8).tobytes()
+    s = zl(b, 1, zlib.Z_HUFFMAN_ONLY)
+    t0 = time.perf_counter()
+    err, _, path = one(torch, workspace, ZLIB, s, cap=len(b) + 64)
+    dt = time.perf_counter() - t0
+    assert path == PATH_DECLINED and err is None, (err, path)
+    assert dt < 0.5, dt
+
+
 def test_output_capacity(torch, workspace):
     b = np.arange(300000, dtype=np.uint32).tobytes()
     s = zl(b, 6)
