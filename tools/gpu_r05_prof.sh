@@ -16,6 +16,7 @@ timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $OUT/cfg_write -o run --output
 RDX_PHASES=1 timeout -k 10 60 $B s1 1 2000 owned >> $OUT/phases_conc.jsonl 2>> $OUT/phases_s1.jsonl &&
 RDX_PHASES=1 timeout -k 10 60 $B c1 1 2000 owned >> $OUT/phases_conc.jsonl 2>> $OUT/phases_c1.jsonl &&
 timeout -k 10 60 $B s1 1 2000 owned >> $OUT/phases_conc.jsonl &&
-timeout -k 10 60 $B c1 1 2000 owned >> $OUT/phases_conc.jsonl
+timeout -k 10 60 $B c1 1 2000 owned >> $OUT/phases_conc.jsonl &&
+RDX_PINF_PROF=1 timeout -k 10 120 python3 tools/probe_pinflate.py 2 > $OUT/pinf_prof_probe.jsonl 2> $OUT/pinf_prof.txt
 rc=$?
 exit $rc
