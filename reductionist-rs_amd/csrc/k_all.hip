@@ -522,6 +522,8 @@ __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) raw_load(raw[u], base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
+        for (int u = 0; u < kU; ++u) raw_pin(raw[u]);   // (no load sunk into its ok[u] branch)
+#pragma unroll
         for (int u = 0; u < kU; ++u) raw_cvt(raw[u], bswap, x[u]);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {

@@ -142,15 +142,31 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
         r.init();
         for (uint64_t r0 = r_lo + l; r0 < r_hi; r0 += (uint64_t)L * kU) {
             int64_t off[kU], rk[kU];
+            if (!GEN && rg.nd <= 1) {
+                // one reduced dim: a lane's loads are L vectors apart, so the offsets (and ranks) are a base plus
+                // multiples of one step: adds, not the general decomposition's 64-bit multiplies per load
+                int64_t rk0;
+                const int64_t o0 = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)(r0 * VW), rk0);
+                const int64_t od = (int64_t)L * VW * rg.v0, kd = (int64_t)L * VW * rg.s0;
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                uint64_t rv = r0 + (uint64_t)u * L;
-                if (rv >= r_hi) rv = r0;  // clamped: every load issues, the value is dropped below
-                off[u] = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)(rv * VW), rk[u]);
+                for (int u = 0; u < kU; ++u) {
+                    const bool in = r0 + (uint64_t)u * L < r_hi;   // clamped: every load issues, the value is dropped below
+                    off[u] = in ? o0 + u * od : o0;
+                    rk[u] = in ? rk0 + u * kd : rk0;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    uint64_t rv = r0 + (uint64_t)u * L;
+                    if (rv >= r_hi) rv = r0;  // clamped: every load issues, the value is dropped below
+                    off[u] = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)(rv * VW), rk[u]);
+                }
             }
             Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
+#pragma unroll
+            for (int u = 0; u < kU; ++u) raw_pin(raw[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 if (r0 + (uint64_t)u * L >= r_hi) continue;
@@ -251,15 +267,32 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
         const uint64_t step = (uint64_t)kWaves * R;      // rows between a lane's consecutive loads
         for (uint64_t r0 = r_lo + wave * R + rsub; r0 < r_hi; r0 += step * kU) {
             int64_t off[kU], rk[kU];
+            if (!GEN && rg.nd <= 1) {
+                // one reduced dim ([R, C] axis 0): a lane's rows are `step` apart, so the offsets (and ranks) are a
+                // base plus multiples of one step (the general decomposition's 64-bit multiplies per load held
+                // the loads back: ~200 dependent instructions before the first one issued)
+                int64_t rk0;
+                const int64_t o0 = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)r0, rk0);
+                const int64_t od = (int64_t)step * rg.v0, kd = (int64_t)step * rg.s0;
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                uint64_t rr = r0 + (uint64_t)u * step;
-                if (rr >= r_hi) rr = r0;  // clamped: every load issues, the value is dropped below
-                off[u] = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)rr, rk[u]);
+                for (int u = 0; u < kU; ++u) {
+                    const bool in = r0 + (uint64_t)u * step < r_hi;   // clamped: every load issues, the value is dropped below
+                    off[u] = in ? o0 + u * od : o0;
+                    rk[u] = in ? rk0 + u * kd : rk0;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    uint64_t rr = r0 + (uint64_t)u * step;
+                    if (rr >= r_hi) rr = r0;  // clamped: every load issues, the value is dropped below
+                    off[u] = koff + red_offset<RANK, GEN>(rg, a.red, (uint32_t)rr, rk[u]);
+                }
             }
             Raw<T, FUSED, VW> raw[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
+#pragma unroll
+            for (int u = 0; u < kU; ++u) raw_pin(raw[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 if (r0 + (uint64_t)u * step >= r_hi) continue;

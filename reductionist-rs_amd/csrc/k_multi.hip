@@ -93,6 +93,8 @@ __device__ __forceinline__ void multi_body(const KMultiArgs &m, const KMultiReq 
 #pragma unroll
         for (int u = 0; u < kU; ++u) raw_load(raw[u], base, 0, (uint64_t)off[u]);
 #pragma unroll
+        for (int u = 0; u < kU; ++u) raw_pin(raw[u]);   // (no load sunk into its ok[u] branch)
+#pragma unroll
         for (int u = 0; u < kU; ++u) raw_cvt(raw[u], bswap, x[u]);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {

@@ -139,6 +139,22 @@ __device__ __forceinline__ void raw_load(Raw<T, FUSED, VW> &r, const uint8_t *ba
     }
 }
 
+// The loaded registers "used" in place (an empty asm): a load whose value is consumed only under a condition
+// (a clamped row past the slice end) is otherwise sunk into that condition's block by the compiler, where it
+// issues after the earlier loads' values came back and waits on all of them (k_axis_cols: two round trips
+// per pass instead of one).
+template <typename T, bool FUSED, int VW>
+__device__ __forceinline__ void raw_pin(Raw<T, FUSED, VW> &r) {
+    if constexpr (FUSED) {
+#pragma unroll
+        for (int k = 0; k < (int)sizeof(T); ++k) asm volatile("" : "+v"(r.b[k]));
+    } else if constexpr (sizeof(r.w) == 16) {
+        asm volatile("" : "+v"(r.w.x), "+v"(r.w.y), "+v"(r.w.z), "+v"(r.w.w));
+    } else {
+        asm volatile("" : "+v"(r.w));
+    }
+}
+
 template <typename T, bool FUSED, int VW>
 __device__ __forceinline__ void raw_cvt(const Raw<T, FUSED, VW> &r, bool bswap, T (&x)[VW]) {
     using U = typename UIntOf<T>::type;
