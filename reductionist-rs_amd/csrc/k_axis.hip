@@ -241,7 +241,10 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
 #ifndef RDX_AXIS_COLS_U16
 #define RDX_AXIS_COLS_U16 16
 #endif
-    constexpr int kU = VW * sizeof(T) >= 16 ? RDX_AXIS_COLS_U16 : 16;   // loads in flight per lane
+#ifndef RDX_AXIS_COLS_U8
+#define RDX_AXIS_COLS_U8 16
+#endif
+    constexpr int kU = VW * sizeof(T) >= 16 ? RDX_AXIS_COLS_U16 : RDX_AXIS_COLS_U8;   // loads in flight per lane
     constexpr int kWaves = kBlock / 64;
     constexpr int kW = packed_words<T, OP>();
     __shared__ uint64_t lds[(kWaves - 1) * 64 * VW * kW];
