@@ -183,3 +183,42 @@ def test_execute_cbor_end_to_end(engine):
     bad = make_request("sum", {"dtype": "float32", "shape": [7, 7]}, oracle.convert)
     st, _, _ = engine.execute_cbor(bad, bytes(4 * 48), 0)
     assert st == oracle.execute(bad, bytes(4 * 48))[0] != 0
+
+
+_UNSTAGED = r'''
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[2], sys.argv[3]]
+import numpy as np, torch
+from oracle import cbor_oracle as cb
+from reductionist_amd import Engine
+from test_cbor_cpu import _info, random_counts
+from test_gpu_cbor import device_encode
+eng = Engine([0]); ws = eng.workspace(0)
+for n in (1, 2049, 3 * 2048 + 17, 100_003):
+    rng = np.random.default_rng(0xCB9 + n)
+    counts = random_counts(rng, n)
+    body = rng.integers(0, 256, 40 + n % 97, dtype=np.uint8).tobytes()
+    dc = torch.from_numpy(counts.copy()).cuda()
+    db = torch.from_numpy(np.frombuffer(body, dtype=np.uint8).copy()).cuda()
+    for flags in range(4):
+        shape = [n, 1] if flags & 1 else [n]
+        got = device_encode(ws, _info("int64", shape, len(body), n), db.data_ptr(), dc.data_ptr(), flags, torch)
+        assert got == cb.cbor_response(body, "int64", shape, counts.tolist(), bool(flags & 1), bool(flags & 2)), (n, flags)
+ws.close(); eng.close()
+print("UNSTAGED-OK")
+'''
+
+
+def test_unstaged_form_matches_oracle(workspace):
+    """The round-4 form (k_cbor_agg / k_cbor_scan / k_cbor), which the runtime keeps for count arrays the staged
+    form cannot take (2^32 counts or more, staging memory unavailable): forced with RDX_CBOR_STAGED=0 in a
+    child process (the tuning is read once per process), byte-identical to the oracle."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, RDX_CBOR_STAGED="0")
+    r = subprocess.run([sys.executable, "-c", _UNSTAGED, str(root / "reductionist-rs_amd"), str(root),
+                        str(root / "tests")], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "UNSTAGED-OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
