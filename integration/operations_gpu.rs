@@ -28,6 +28,15 @@ unsafe impl Sync for Ctx {} // rdx_execute* are thread-safe (include/rdx.h, rdx_
 static CTX: OnceLock<Ctx> = OnceLock::new();
 
 pub fn init(devices: &[i32]) -> Result<(), ActiveStorageError> {
+    // a plugin built against another rdx.h refuses to start: struct sizes differ between ABI versions
+    // (version 2: rdx_device_stats grew, rdx_context_config.inflate_fallback)
+    let abi = unsafe { rdx_abi_version() };
+    if abi != RDX_ABI_VERSION {
+        return Err(ActiveStorageError::GpuEngine {
+            status: -1,
+            error: format!("librdx implements ABI {abi}, the plugin was built for {RDX_ABI_VERSION}"),
+        });
+    }
     let mut ctx = std::ptr::null_mut();
     check(unsafe { rdx_context_create(devices.as_ptr(), devices.len() as i32, &mut ctx) }, None, DType::Float64)?;
     let _ = CTX.set(Ctx(ctx));
