@@ -822,8 +822,16 @@ __device__ void arrive_and_fold(const KOut &out, const uint64_t *P, uint32_t chu
                 break;
             }
             // backing off: a folder whose publishers are far from done (a batch launch that fills the chip)
-            // must not flood the fabric with re-reads while they stream
-            if (it < 2) __builtin_amdgcn_s_sleep(1);
+            // must not flood the fabric with re-reads while they stream.  (RDX_FOLD_POLL_SHORT=1: ~0.1 us sleeps
+            // for the few folders of a fold_last launch — measured no better: C3 7.98 -> 8.22 us, C1 within
+            // noise, profiles/r05_fold_poll_ab.jsonl)
+#ifndef RDX_FOLD_POLL_SHORT
+#define RDX_FOLD_POLL_SHORT 0
+#endif
+            if (RDX_FOLD_POLL_SHORT && out.fold_last) {
+                if (it < 8) __builtin_amdgcn_s_sleep(1);
+                else __builtin_amdgcn_s_sleep(4);
+            } else if (it < 2) __builtin_amdgcn_s_sleep(1);
             else if (it < 6) __builtin_amdgcn_s_sleep(8);
             else __builtin_amdgcn_s_sleep(32);
 #pragma unroll
