@@ -114,13 +114,10 @@ __device__ __forceinline__ void fold_value(Red<T, OP> &r, const KMissing &miss, 
     }
 }
 
-template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK>
+template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK, int KU>
 __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
-#ifndef RDX_AXIS_ROWS_U
-#define RDX_AXIS_ROWS_U 4
-#endif
-    constexpr int kU = RDX_AXIS_ROWS_U;   // loads in flight per lane
+    constexpr int kU = KU;   // loads in flight per lane (4; 16 for long rows, launch_axis_k)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t L = a.group, G = 64 / L;        // lanes per item, items per wave pass
     const uint32_t l = lane & (L - 1), g = lane / L;
@@ -440,8 +437,16 @@ void launch_axis_k(const KAxis &a, int cus, hipStream_t st) {
         const uint64_t cap = (uint64_t)cus * 16;
         if (blocks > cap) blocks = cap;
         if (blocks == 0) blocks = 1;
-        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true, 1, GEN, MK>), dim3((uint32_t)blocks), block, 0, st, a);
-        else hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW, GEN, MK>), dim3((uint32_t)blocks), block, 0, st, a);
+        // rows whose slice gives every lane of its group 16 or more vectors (e.g. [4096, 4096] f32 axis 1: 1024
+        // vectors per 64-lane row) keep 16 loads in flight per lane; shorter ones 4 (a load past the row's
+        // end still issues, clamped, and would only cost)
+#ifndef RDX_AXIS_ROWS_DEEP
+#define RDX_AXIS_ROWS_DEEP 1
+#endif
+        const bool deep = RDX_AXIS_ROWS_DEEP && !a.src.fused && a.n_red / VW / a.slices >= 16ull * a.group;
+        if (a.src.fused) hipLaunchKernelGGL((k_axis_rows<T, OP, true, 1, GEN, MK, 4>), dim3((uint32_t)blocks), block, 0, st, a);
+        else if (deep) hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW, GEN, MK, 16>), dim3((uint32_t)blocks), block, 0, st, a);
+        else hipLaunchKernelGGL((k_axis_rows<T, OP, false, VW, GEN, MK, 4>), dim3((uint32_t)blocks), block, 0, st, a);
     } else {
         const dim3 grid((uint32_t)((a.n_out / VW + a.group - 1) / a.group), a.slices);
         if (a.src.fused) hipLaunchKernelGGL((k_axis_cols<T, OP, true, 1, GEN, MK>), grid, block, 0, st, a);
