@@ -107,6 +107,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // ---- CRC-32 (reflected 0xEDB88320) algebra, as in zlib's crc32_combine ---------------------------
+// multmodp restates zlib's crc32.c function of that name (zlib 1.2.12+, (C) Jean-loup Gailly and Mark Adler,
+// zlib license): a(x) * b(x) modulo the CRC-32 polynomial, a's bits taken from the top.
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
     uint32_t m = 1u << 31, p = 0;
     for (;;) {
