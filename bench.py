@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--no-configs", action="store_true")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--primary-only", action="store_true", help="only the headline batched C2 loop (profiling)")
+    ap.add_argument("--full-out", default="gpurun_out/bench_full.json",
+                    help="where rank 0 writes the full record (every leg); '' = stderr only")
     return ap.parse_args()
 
 
@@ -1222,6 +1224,106 @@ def devices_used(cx):
     return allv
 
 
+LINE_MAX_BYTES = 8192      # the driver did not parse round 5's 21.5 KB line
+
+
+def _dig(d, *path):
+    for p in path:
+        if isinstance(d, dict):
+            d = d.get(p)
+        elif isinstance(d, list) and isinstance(p, int) and -len(d) <= p < len(d):
+            d = d[p]
+        else:
+            return None
+    return d
+
+
+def compact_extra(extra):
+    """One scalar per leg (µs or GiB/s, plus the roofline fraction where the leg has one) out of the full
+    record's `extra`; missing legs are left out.  The full record goes to a file (main())."""
+    out = {}
+
+    def put(key, *path, nd=4):
+        v = _dig(extra, *path)
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            out[key] = round(float(v), nd)
+
+    put("c2_single_chunk_us", "c2_single_chunk", "kernel_us_avg", nd=3)
+    put("c2_single_chunk_frac", "c2_single_chunk", "roofline_frac")
+    put("c2_concurrent_us_per_request", "c2_concurrent_requests", "us_per_request", nd=3)
+    put("c2_concurrent_frac", "c2_concurrent_requests", "roofline_frac")
+    put("headline_step_median_us", "headline_per_step", "median_us", nd=2)
+    put("c4_batch_GiBs", "c4_batch", "value", nd=2)
+    put("c4_batch_frac", "c4_batch", "roofline_frac")
+    put("c4_cpu_GiBs", "c4_batch", "cpu_baseline", "value", nd=3)
+    put("c4_cpu_cores", "c4_batch", "cpu_baseline", "cores", nd=0)
+    put("f64_64mib_us", "f64_64mib", "kernel_us_avg", nd=3)
+    put("f64_64mib_frac", "f64_64mib", "roofline_frac")
+    put("f64_4mib_us", "f64_4mib", "kernel_us_avg", nd=3)
+    put("f64_4mib_frac", "f64_4mib", "roofline_frac")
+    put("c4z_inflate_GBs", "c4z_inflate", "value", nd=2)
+    put("c4z_inflate_cpu_GBs", "c4z_inflate", "cpu_baseline", "value", nd=2)
+    put("inflate_lone_ms", "c4z_inflate", "lone", "device_ms", nd=3)
+    put("inflate_lone_cpu_ms", "c4z_inflate", "lone", "cpu_baseline", "value", nd=3)
+    for codec in ("lz4", "blosclz", "lz4_lib", "zstd"):
+        put(f"blosc2_{codec}_GBs", "c4b_blosc2", codec, "value", nd=2)
+    put("blosc2_lz4_lib_cpu_GBs", "c4b_blosc2", "cpu_baseline_lz4_lib", "value", nd=2)
+    put("blosc2_zstd_cpu_GBs", "c4b_blosc2", "cpu_baseline_zstd", "value", nd=2)
+    for k in ("c1_sum_4mib", "c3_min_missing_value", "c3_max_missing_value", "c3_max_valid_range", "c5_select",
+              "c1_batch64", "c3_min_batch20"):
+        put(f"{k}_us", "configs", k, "us_per_launch", nd=2)
+        put(f"{k}_frac", "configs", k, "roofline_frac")
+    put("mixed20_us", "mixed_requests", "us_per_launch", nd=2)
+    put("mixed20_frac", "mixed_requests", "roofline_frac")
+    native = extra.get("concurrent_native")
+    for i, r in enumerate(native if isinstance(native, list) else []):
+        if not isinstance(r, dict) or "config" not in r:
+            continue
+        tag = {"rdx_execute_device + synchronize": "device", "rdx_execute_resident (coalesced)": "resident"}.get(
+            r.get("path"), "owned")
+        key = f"native_{r['config']}_{tag}_t{r.get('threads')}"
+        put(key + "_us", "concurrent_native", i, "us_per_request_aggregate", nd=3)
+        put(key + "_frac", "concurrent_native", i, "roofline_frac")
+    put("cbor_count_array_us", "cbor_response", "count_array", "us_per_call", nd=2)
+    put("cbor_kernel_only_frac", "cbor_response", "count_array_kernel_only", "roofline_frac")
+    for k in ("c2_sum_64mib", "c3_min_16mib", "f32_sum_4mib_shuffled_be", "f64_sum_4mib_shuffled_be",
+              "c5_select_256mib"):
+        put(f"host_{k}_pinned_ms", "host_inclusive", k, "pinned_ms", nd=3)
+        put(f"host_{k}_pcie_copy_ms", "host_inclusive", k, "pcie_pinned_copy_ms", nd=3)
+    put("pool_host_GiBs", "pool", "host", "GiBs_chunk", nd=2)
+    put("pool_resident_frac", "pool", "resident", "roofline_frac")
+    put("cpu_c1_clone_us", "cpu_baselines", "c1_sum_4mib_clone", "us_per_request", nd=1)
+    put("cpu_c3_min_us", "cpu_baselines", "c3_min_missing_value", "us_per_request", nd=1)
+    put("cpu_c5_select_ms", "cpu_baselines", "c5_select", "ms_per_request", nd=2)
+    return out
+
+
+def compact_line(line, full_path=None):
+    """The one stdout line the driver parses: the contract's keys, `roofline`, `cpu_baseline` and a flat
+    `extra` of scalars; the full record is named by `full_record`.  Asserted at most LINE_MAX_BYTES
+    (tests/test_bench_line_cpu.py)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "oversubscribed")
+    out = {k: line[k] for k in keep if k in line}
+    cfg = dict(out.get("config") or {})
+    if isinstance(cfg.get("devices"), list) and len(cfg["devices"]) > 8:
+        cfg["devices"] = cfg["devices"][:8] + ["…"]
+    out["config"] = cfg
+    if isinstance(out.get("cpu_baseline"), dict):
+        cb = dict(out["cpu_baseline"])
+        if isinstance(cb.get("sample"), str) and len(cb["sample"]) > 240:
+            cb["sample"] = cb["sample"][:237] + "..."
+        out["cpu_baseline"] = cb
+    out["extra"] = compact_extra(line.get("extra") or {})
+    if full_path:
+        out["full_record"] = str(full_path)
+    s = json.dumps(out, separators=(",", ":"))
+    if len(s.encode()) > LINE_MAX_BYTES:     # never hand the driver an unparseable line: drop extra first
+        out["extra"] = {"dropped": "line over %d B" % LINE_MAX_BYTES}
+        s = json.dumps(out, separators=(",", ":"))
+    return s
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "LOCAL_RANK" not in os.environ:
@@ -1313,7 +1415,22 @@ def main():
     if cpu_line:
         line["cpu_baseline"] = cpu_line
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        # the full record: a file (gpurun_out/ travels back from a GPU box) and stderr, BEFORE the compact
+        # stdout line, so the last line of either stream or of both merged is the parseable one
+        full = json.dumps(line)
+        full_path = Path(args.full_out) if args.full_out else None
+        if full_path is not None:
+            try:
+                if not full_path.is_absolute():
+                    full_path = ROOT / full_path
+                full_path.parent.mkdir(parents=True, exist_ok=True)
+                full_path.write_text(full + "\n")
+            except OSError as e:
+                print(f"bench.py: could not write {full_path}: {e}", file=sys.stderr)
+                full_path = None
+        print(full, file=sys.stderr, flush=True)
+        print(compact_line(line, full_path.relative_to(ROOT) if full_path and full_path.is_relative_to(ROOT)
+                           else full_path), flush=True)
     cx.ws.close()
     cx.eng.close()
     if world > 1:
