@@ -216,7 +216,11 @@ typedef struct rdx_context_config {
                                        or its error; 100-220 ms per 4 MiB).  Workspaces keep the value they were
                                        created with.                                                          */
     uint64_t coalesce_max_bytes;    /* rdx_execute_resident chunks up to this many bytes coalesce (0: 64 MiB)  */
-    uint64_t coalesce_host_max_bytes; /* rdx_execute / _owned host chunks up to this many (0: 1 MiB)           */
+    uint64_t coalesce_host_max_bytes; /* rdx_execute / _owned host chunks up to this many (0: 1 MiB) coalesce   *
+                                       after their H2D copy.  It does not bound page-locked all-axes chunks   *
+                                       of up to RDX_HOST_READ_KIB (env, default 4096 KiB): those are read by  *
+                                       the kernel over PCIe, direct or in a shared launch whose few readers  *
+                                       keep the link, not HBM, the bound                     */
 } rdx_context_config;
 /* Call it before the context is shared: once a request has been placed the configuration is frozen and
  * this returns RDX_E_INVALID_ARGUMENT (the dispatchers and the placement read it without a lock). */

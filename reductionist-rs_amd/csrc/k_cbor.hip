@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
     const KCbor &m = *(const KCbor *)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ uint32_t s_len[kPackMaxT];
     __shared__ uint64_t s_tot[kBlock / 64];
-    __shared__ uint32_t s_last;
+    __shared__ uint32_t s_last, s_fault;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t T = m.tpg, g = blockIdx.x;
     const uint64_t t0 = (uint64_t)g * T;
@@ -375,6 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
         if (lane == 0) {
             put_granule(m.tagged + g, run, m.epoch);
             s_last = arrive_last(m.arrive, gridDim.x, g);
+            s_fault = 0;
         }
     }
     __syncthreads();
@@ -405,7 +406,12 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
         if (lane >= (uint32_t)d) x += y;
     }
     if (lane == 63) s_tot[wave] = x;
+    if (fault) s_fault = 1;   // (benign race: every writer stores 1)
     __syncthreads();
+    // a group total that never arrived (a device fault) leaves stale payloads behind: every group offset and
+    // the total are then 0, so k_cbor_place writes only inside the output bound (tiles overlap; the status
+    // word carries RDX_E_DEVICE and the response is discarded)
+    const bool bad = s_fault != 0;
     uint64_t pre = 0, all = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64; ++w) {
@@ -416,11 +422,11 @@ __global__ __launch_bounds__(kBlock) void k_cbor_pack(const KCbor args) {
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
         const uint32_t j = threadIdx.x * kPer + k;
-        if (j < G) m.records[m.n_tiles + 1 + j] = run;
+        if (j < G) m.records[m.n_tiles + 1 + j] = bad ? 0 : run;
         run += v[k];
     }
     if (threadIdx.x == 0) {
-        m.records[m.n_tiles] = all;
+        m.records[m.n_tiles] = bad ? 0 : all;
         __hip_atomic_store(m.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the top counter
     }
     if (fault && m.status) __hip_atomic_fetch_or(m.status, (uint32_t)RDX_E_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

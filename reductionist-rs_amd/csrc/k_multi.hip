@@ -114,7 +114,7 @@ __device__ __forceinline__ void multi_body(const KMultiArgs &m, const KMultiReq 
     out.partials = m.partials + (uint64_t)q.block0 * kRecordU64;
     out.tickets = m.tickets + (uint64_t)item * kTicketWords;
     out.epoch = m.epoch;
-    out.fold_last = (m.flags & kMultiFoldLast) != 0;
+    out.fold_last = (m.flags & kMultiFoldLast) ? ((m.flags & kMultiAtomicFold) ? 2u : 1u) : 0u;
     out.host_slots = (m.flags & kMultiHostSlots) != 0;
     finalize_all<T, OP>(r, out, 0, bpc, b);
 }

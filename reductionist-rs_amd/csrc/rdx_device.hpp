@@ -905,12 +905,178 @@ __device__ __forceinline__ void write_folded(const KOut &out, uint32_t chunk, co
     }
 }
 
+// ---- order-free folds through device-scope atomics (KOut::fold_last == 2) ---------------------------------
+// Count, integer sums (wrapping: u64 adds commute) and min / max of every dtype — the float ±0 tie ranks
+// are a min / max of ranks and the NaN flag an OR, so they commute too — need no record per workgroup:
+// each workgroup merges its partial into 8 per-XCD accumulator lines of the chunk (the arrival-counter
+// lines of the ticket area, which fold-last launches leave unused) with no-return atomics, waits for
+// their acknowledgement (`s_waitcnt vmcnt(0)`: on gfx9 no-return atomics stay counted until performed),
+// then adds {count << 20 | 1} to its line — the arrival and the count in one word.  The chunk's last
+// block polls the 8 count words (one load per lane of 8 lanes) until the other bpc - 1 arrivals are in,
+// then takes every accumulator with an atomic exchange to 0 (the value it returns is final: each
+// publisher's merge was performed before its arrival, and nobody else adds; the exchange also leaves the
+// lines zeroed for the next launch).  Stored forms make 0 the identity of every word: a value as its
+// order-preserving key (min: the key's complement, so both are atomic max), a ±0 rank likewise.
+// Float sums keep the records: their fold order is part of the result.
+template <typename T, int OP>
+constexpr bool kAtomicFold = OP == OP_COUNT || OP == OP_MAX || OP == OP_MIN || (OP == OP_SUM && !std::is_floating_point_v<T>);
+
+template <typename T>
+__device__ __forceinline__ uint64_t okey(T v) {   // order-preserving unsigned key
+    using U = typename UIntOf<T>::type;
+    constexpr U kSign = (U)1 << (8 * sizeof(U) - 1);
+    U u = to_u<T>(v);
+    if constexpr (std::is_floating_point_v<T>) u = (u & kSign) ? (U)~u : (U)(u | kSign);
+    else if constexpr (std::is_signed_v<T>) u ^= kSign;
+    return (uint64_t)u;
+}
+template <typename T>
+__device__ __forceinline__ T from_okey(uint64_t k) {
+    using U = typename UIntOf<T>::type;
+    constexpr U kSign = (U)1 << (8 * sizeof(U) - 1);
+    U u = (U)k;
+    if constexpr (std::is_floating_point_v<T>) u = (u & kSign) ? (U)(u & ~kSign) : (U)~u;
+    else if constexpr (std::is_signed_v<T>) u ^= kSign;
+    return from_u<T>(u);
+}
+template <typename T, int OP>
+__device__ __forceinline__ uint64_t stored_value(T v) {   // 0 = identity; larger = further from it
+    using U = typename UIntOf<T>::type;
+    const uint64_t k = okey<T>(v);
+    return OP == OP_MIN ? (uint64_t)(U)~(U)k : k;
+}
+template <typename T, int OP>
+__device__ __forceinline__ T value_of_stored(uint64_t s) {
+    using U = typename UIntOf<T>::type;
+    return from_okey<T>(OP == OP_MIN ? (uint64_t)(U)~(U)s : s);
+}
+template <int OP>
+__device__ __forceinline__ uint64_t stored_rank(int64_t r) {   // max keeps the largest rank, min the smallest
+    const uint64_t k = (uint64_t)r ^ (1ull << 63);
+    return OP == OP_MAX ? k : ~k;
+}
+template <int OP>
+__device__ __forceinline__ int64_t rank_of_stored(uint64_t s) {   // 0 (nothing stored) -> the identity
+    if (s == 0) return OP == OP_MAX ? -1 : INT64_MAX;
+    return (int64_t)((OP == OP_MAX ? s : ~s) ^ (1ull << 63));
+}
+
+constexpr uint32_t kArriveBits = 20;   // {count << 20 | arrivals}: arrivals per line < 2^20, count < 2^44
+// accumulator line of shard s (0..7) of the chunk: u64 words [0] count | arrivals, [1] value / sum,
+// [2] +0 rank, [3] -0 rank, [4] NaN flag
+__device__ __forceinline__ uint64_t *acc_line(const KOut &out, uint32_t chunk, uint32_t s) {
+    return reinterpret_cast<uint64_t *>(out.tickets + (uint64_t)chunk * kTicketWords + (1 + s) * kTicketStride);
+}
+
+template <typename T, int OP>
+__device__ void atomic_fold(const Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
+    constexpr bool kRank = Red<T, OP>::kRank;
+    const int64_t rid = OP == OP_MAX ? -1 : INT64_MAX;
+#if RDX_PROBES
+    const bool drop = out.drop_block == 1 + blockIdx.x;
+#else
+    constexpr bool drop = false;
+#endif
+    if (b != bpc - 1) {   // a publisher: merge, wait for the merges, arrive
+        if (threadIdx.x == 0 && !drop) {
+            uint64_t *L = acc_line(out, chunk, b % kTicketShards);
+            bool merged = false;
+            if constexpr (OP == OP_SUM) {
+                __hip_atomic_fetch_add(L + 1, r.si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                merged = true;
+            } else if constexpr (OP != OP_COUNT) {
+                if (r.cnt) {
+                    __hip_atomic_fetch_max(L + 1, stored_value<T, OP>(r.v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    merged = true;
+                }
+                if constexpr (kRank) {
+                    if (r.zp != rid) __hip_atomic_fetch_max(L + 2, stored_rank<OP>(r.zp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (r.zn != rid) __hip_atomic_fetch_max(L + 3, stored_rank<OP>(r.zn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (r.nan) __hip_atomic_fetch_or(L + 4, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    merged = true;
+                }
+            }
+            if (merged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // performed before the arrival
+            __hip_atomic_fetch_add(L, ((uint64_t)r.cnt << kArriveBits) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        RDX_STAMP(2);
+        return;
+    }
+    // the folder (the chunk's last block): wave 0, lane s < 8 watches line s
+    if (threadIdx.x >= 64) return;
+    const uint32_t lane = threadIdx.x;
+    const bool mine = lane < kTicketShards;
+    uint64_t *L = acc_line(out, chunk, mine ? lane : 0);
+    const uint32_t want = bpc - 1;
+    uint32_t fault = 0;
+    for (uint32_t it = 0;; ++it) {
+        const uint64_t w = mine ? __hip_atomic_load(L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        uint32_t got = (uint32_t)(w & ((1u << kArriveBits) - 1));
+#pragma unroll
+        for (int m = 4; m >= 1; m >>= 1) got += __shfl_xor(got, m, 64);
+        if (__shfl(got, 0, 64) >= want) break;
+        if (it >= kSpinLimit) {
+            fault = 1;
+            break;
+        }
+        if (it < 2) __builtin_amdgcn_s_sleep(1);
+        else if (it < 6) __builtin_amdgcn_s_sleep(4);
+        else __builtin_amdgcn_s_sleep(16);
+    }
+    // take the totals (and zero the lines for the next launch)
+    uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+    if (mine) {
+        w0 = __hip_atomic_exchange(L, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (OP != OP_COUNT) w1 = __hip_atomic_exchange(L + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (kRank) {
+            w2 = __hip_atomic_exchange(L + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w3 = __hip_atomic_exchange(L + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w4 = __hip_atomic_exchange(L + 4, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    auto umax = [](uint64_t a, uint64_t c) { return a > c ? a : c; };
+#pragma unroll
+    for (int m = 4; m >= 1; m >>= 1) {
+        w0 += shfl_xor_u64(w0, m);
+        if constexpr (OP == OP_SUM) w1 += shfl_xor_u64(w1, m);
+        else if constexpr (OP != OP_COUNT) w1 = umax(w1, shfl_xor_u64(w1, m));
+        if constexpr (kRank) {
+            w2 = umax(w2, shfl_xor_u64(w2, m));
+            w3 = umax(w3, shfl_xor_u64(w3, m));
+            w4 |= shfl_xor_u64(w4, m);
+        }
+    }
+    if (lane != 0) return;
+    Red<T, OP> acc = r;   // the folder's own partial (thread 0 holds the block total)
+    Red<T, OP> o;
+    o.init();
+    o.cnt = (int64_t)(w0 >> kArriveBits);
+    if constexpr (OP == OP_SUM) o.si = w1;
+    else if constexpr (OP != OP_COUNT) {
+        if (w1) o.v = value_of_stored<T, OP>(w1);
+    }
+    if constexpr (kRank) {
+        o.zp = rank_of_stored<OP>(w2);
+        o.zn = rank_of_stored<OP>(w3);
+        o.nan = (uint32_t)(w4 & 1);
+    }
+    acc.merge(o);
+    write_folded<T, OP>(out, chunk, acc, fault != 0 || drop);
+    RDX_STAMP(3);
+}
+
 // Publish this workgroup's partial and let the LAST arriving workgroup of the chunk fold all
 // partials in workgroup order and write the response (one launch, no second kernel).
 template <typename T, int OP>
 __device__ void finalize_all(Red<T, OP> &r, const KOut &out, uint32_t chunk, uint32_t bpc, uint32_t b) {
     constexpr int kR = granules<T, OP>();
     block_reduce(r);
+    if constexpr (kAtomicFold<T, OP>) {
+        if (out.fold_last == 2) {
+            atomic_fold<T, OP>(r, out, chunk, bpc, b);
+            return;
+        }
+    }
     const uint64_t *P = out.partials + (uint64_t)chunk * bpc * kR;
 #if RDX_PROBES
     // fault injection (probe builds): grid block drop_block - 1 never publishes its record (it still

@@ -67,7 +67,8 @@ struct KOut {
                               // reduction), NaN ORed in; the caller clears it when a NaN can set it
     uint32_t epoch;           // this launch's hand-off tag (never 0): records carry it per granule
     uint32_t fold_last;       // 1: the chunk's LAST block (the last one dispatched) folds the records,
-                              // polling them; no arrival counters (rdx_device.hpp arrive_and_fold)
+                              // polling them; no arrival counters (rdx_device.hpp arrive_and_fold);
+                              // 2: the same, order-free folds through atomics (rdx_device.hpp atomic_fold)
     uint32_t host_slots;      // 1: `body` is a page-locked host slot of 3 tagged granules per chunk
                               // (value lo, value hi, count | status), written with system-scope stores
 #if RDX_PROBES
@@ -171,7 +172,7 @@ struct KMultiReq {
 };
 static_assert(sizeof(KMultiReq) == 152, "KMultiReq layout");
 
-enum : uint32_t { kMultiFoldLast = 1, kMultiHostSlots = 2 };   // KMultiArgs::flags -> KOut
+enum : uint32_t { kMultiFoldLast = 1, kMultiHostSlots = 2, kMultiAtomicFold = 4 };   // KMultiArgs::flags -> KOut
 struct KMultiArgs {
     uint64_t *partials;              // hand-off records: request k's block b at (block0 + b) * kRecordU64
     uint32_t *tickets;               // request k's arrival counters at k * kTicketWords

@@ -78,7 +78,7 @@ struct Tuning {
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
-    int fold_last = env_int("RDX_FOLD_LAST", 1);                       // A/B: 0 = arrival counters everywhere
+    int fold_last = env_int("RDX_FOLD_LAST", 2);                       // 2: + atomic folds, 1: records only, 0: arrival counters
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
     int direct_max = env_int("RDX_DIRECT_MAX", 1);                     // idle-queue fast path: callers launching at once
@@ -103,6 +103,10 @@ const Tuning &tuning() {
     static const Tuning t;
     return t;
 }
+
+// KOut::fold_last of a fold-last launch: 2 = order-free ops fold through atomics (rdx_device.hpp atomic_fold),
+// the rest through records; 1 = records for every op
+uint32_t fold_mode() { return tuning().fold_last >= 2 ? 2u : 1u; }
 
 template <class T>
 struct DevBuf {
@@ -426,7 +430,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
     out.body_stride = body_bytes;
     out.counts_stride = n_counts;
     // all-axes launches of few chunks: the last block of each chunk folds (no arrival counters)
-    out.fold_last = n_chunks <= kFoldLastChunks && tuning().fold_last ? 1u : 0u;
+    out.fold_last = n_chunks <= kFoldLastChunks && tuning().fold_last ? fold_mode() : 0u;
 #if RDX_PROBES
     out.drop_block = (uint32_t)tuning().drop_block;
 #endif
@@ -518,7 +522,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
                 c.out.body_stride = p.op == RDX_OP_COUNT ? 8 : p.esz;
                 c.out.counts_stride = 1;
                 c.out.status_any = 1;
-                c.out.fold_last = a.n_out <= kFoldLastChunks && tuning().fold_last ? 1u : 0u;
+                c.out.fold_last = a.n_out <= kFoldLastChunks && tuning().fold_last ? fold_mode() : 0u;
                 c.out.partials = ws->partials.p;
                 c.out.tickets = ws->tickets.p;
                 RDX_HIP(launch_all_contig(p.dtype, p.op, c, (uint32_t)a.n_out, s));
@@ -1047,6 +1051,19 @@ bool is_gfx950(int dev) {
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
+// The staged CBOR scratch (~9 B per count) is not kept at its high-water size above this: a workspace that
+// once encoded a very large count array would otherwise hold it (per workspace, per entry) and starve later,
+// unrelated requests of HBM.
+constexpr uint64_t kCborKeepStage = 512ull << 20;
+rdx_status trim_cbor_stage(rdx_workspace *ws, hipStream_t s, uint64_t keep = kCborKeepStage) {
+    if (ws->cbor_stage.cap <= keep) return RDX_OK;
+    RDX_HIP(hipStreamSynchronize(s));   // in-flight k_cbor_place may still read it
+    RDX_HIP(hipFree(ws->cbor_stage.p));
+    ws->cbor_stage.p = nullptr;
+    ws->cbor_stage.cap = 0;
+    return RDX_OK;
+}
+
 // Response serialisation on the device (rdx_cbor_encode_device, k_cbor.hip), asynchronous on `s`.
 rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const void *d_body, const int64_t *d_counts,
                        uint32_t flags, void *d_out, uint64_t out_cap, uint64_t *d_out_len, uint32_t *d_status,
@@ -1098,7 +1115,9 @@ rdx_status cbor_device(rdx_workspace *ws, const rdx_response_info *info, const v
     if (m.staged) {
         // tile lengths as tagged granules in the hand-off records, the sharded arrival counters
         m.tpg = cbor_pack_tpg(m.n_tiles);
-        if (!m.tpg || ensure(ws, ws->cbor_stage, cbor_stage_bytes(m.n_tiles), s) || ensure(ws, ws->partials, 2048, s, true) ||
+        const uint64_t need = cbor_stage_bytes(m.n_tiles);
+        if (need <= kCborKeepStage && (st = trim_cbor_stage(ws, s))) return st;   // an earlier huge one
+        if (!m.tpg || ensure(ws, ws->cbor_stage, need, s) || ensure(ws, ws->partials, 2048, s, true) ||
             ensure(ws, ws->tickets, kTicketWords, s, true)) {
             (void)hipGetLastError();
             m.staged = 0;
@@ -1669,7 +1688,8 @@ rdx_status launch_multi_group(rdx_workspace *ws, const KMultiReq *reqs, uint32_t
                               uint32_t flags = 0) {
     KMultiArgs args;
     args.n_items = n;
-    args.flags = flags | (tuning().fold_last ? kMultiFoldLast : 0u);   // <= 24 folders: always fold-last
+    args.flags = flags | (tuning().fold_last ? kMultiFoldLast : 0u) |   // <= 24 folders: always fold-last
+                 (fold_mode() == 2 ? kMultiAtomicFold : 0u);
     args.pad = 0;
     const uint64_t target = (uint64_t)ws->cus * tuning().multi_blocks_per_cu;
     uint64_t want = 0;
@@ -1869,7 +1889,7 @@ rdx_status launch_lane(Lane &L) {
         if ((st = next_epoch(ws, s, out.epoch))) return st;
         out.body = reinterpret_cast<uint8_t *>(L.h_res);
         out.host_slots = 1;
-        out.fold_last = L.n <= kFoldLastChunks && tuning().fold_last ? 1u : 0u;
+        out.fold_last = L.n <= kFoldLastChunks && tuning().fold_last ? fold_mode() : 0u;
         if (j0.mode == Mode::AllContig) {
             KAllContig a = j0.contig;
             a.src.table = 1;
@@ -2460,7 +2480,7 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
         }
         if ((r = ensure(ws, ws->body, std::max<uint64_t>(p.info.body_bytes, 16), s))) return r;
         if ((r = ensure(ws, ws->counts, std::max<uint64_t>(p.info.n_counts, 1), s))) return r;
-        if ((r = ensure(ws, ws->status, 1, s))) return r;
+        if ((r = ensure(ws, ws->status, 2, s))) return r;   // [0] the operation's, [1] the CBOR encoder's
         uint64_t len = chunk_len;
         if (compressed) {  // the chunk crossed PCIe compressed; inflate it in HBM, then plan on its size
             uint64_t hint = 0;
@@ -2492,23 +2512,29 @@ rdx_status execute_host(rdx_context *ctx, const rdx_request &req, const uint8_t 
             if ((r = ensure(ws, ws->cbor, bound, s))) return r;
             if ((r = ensure(ws, ws->cbor_len, 1, s))) return r;
             if ((r = pool_alloc(ctx, bound, &cb->host))) return r;
+            // the encoder's own status word (a hand-off fault in k_cbor_pack) next to the operation's: cbor_device
+            // clears the one it is given
             if ((r = cbor_device(ws, &p.info, ws->body.p, ws->counts.p, cb->flags, ws->cbor.p, bound, ws->cbor_len.p,
-                                 nullptr, s)))
+                                 ws->status.p + 1, s)))
                 return r;
             uint64_t &n = ws->h_back[1];
             n = 0;
+            uint32_t &enc_status = *(reinterpret_cast<uint32_t *>(ws->h_back) + 1);
+            enc_status = 0;
             RDX_HIP(hipMemcpyAsync(&n, ws->cbor_len.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-            RDX_HIP(hipMemcpyAsync(&status, ws->status.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            RDX_HIP(hipMemcpyAsync(&status, ws->status.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             if (bound <= kCborOneTrip) RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, bound, hipMemcpyDeviceToHost, s));
             if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, resident ? 0 : chunk_len, len))))
                 return r;
             if (status) return (rdx_status)status;
+            if (enc_status) return (rdx_status)enc_status;
+            if (n > bound) return RDX_E_DEVICE;   // a length the encoder cannot produce: never copy past the block
             if (bound > kCborOneTrip) {
                 RDX_HIP(hipMemcpyAsync(cb->host, ws->cbor.p, n, hipMemcpyDeviceToHost, s));
                 if ((r = wait_stream(ctx, entry, ws, spin_budget_us(entry, pl.weight, n, 0)))) return r;
             }
             cb->len = n;
-            return RDX_OK;
+            return trim_cbor_stage(ws, s);   // (the stream is idle here)
         }
         // a small response into pageable buffers goes through the page-locked block (then one host memcpy)
         const uint64_t bb = p.info.body_bytes, cbytes = p.info.n_counts * sizeof(int64_t);

@@ -23,32 +23,40 @@ sys.path[:0] = [sys.argv[1] + "/reductionist-rs_amd", sys.argv[1]]
 import numpy as np
 from reductionist_amd import Engine, _abi
 eng = Engine([0])
-v = np.arange(1 << 20, dtype=np.float32) % 7          # C1 shape: 4 MiB, 128 workgroups
+dt = sys.argv[2]                                      # float32 sum: records; int32 sum / float64 max: atomics
+v = (np.arange((4 << 20) // np.dtype(dt).itemsize) % 7).astype(dt)   # C1's 4 MiB: 128 workgroups
+op = sys.argv[3]
 t = time.time()
-st, info, body, counts = eng.execute_raw(_abi.CRequest("sum", "float32"), v.tobytes())
+st, info, body, counts = eng.execute_raw(_abi.CRequest(op, dt), v.tobytes())
 out = {"status": st, "seconds": time.time() - t}
 if st == 0:
-    out["sum"] = float(np.frombuffer(body, np.float32)[0])
-    out["expect"] = float(v.astype(np.float64).sum())
+    out["value"] = float(np.frombuffer(body, dt)[0])
+    out["expect"] = float(v.astype(np.float64).sum() if op == "sum" else v.max())
+    # the next request on the same engine sees clean accumulators (the folder zeroes them)
+    st2, _, body2, _ = eng.execute_raw(_abi.CRequest(op, dt), v.tobytes())
+    out["again"] = float(np.frombuffer(body2, dt)[0]) if st2 == 0 else None
 print(json.dumps(out))
 """
 
 
-def run(drop, fold_last):
+def run(drop, fold_last, dt="float32", op="sum"):
     env = dict(os.environ, RDX_LIB_PATH=str(PROBE), RDX_DROP_BLOCK=str(drop), RDX_FOLD_LAST=str(fold_last))
-    r = subprocess.run([sys.executable, "-c", SCRIPT, str(ROOT)], env=env, capture_output=True, text=True,
+    r = subprocess.run([sys.executable, "-c", SCRIPT, str(ROOT), dt, op], env=env, capture_output=True, text=True,
                        timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("fold_last", [1, 0])
-def test_missing_publisher_is_a_device_error(fold_last):
+@pytest.mark.parametrize("fold_last,dt,op", [(1, "float32", "sum"), (0, "float32", "sum"), (2, "int32", "sum"),
+                                             (2, "float64", "max")])
+def test_missing_publisher_is_a_device_error(fold_last, dt, op):
+    """fold_last 2 with an order-free op: the folder waits on the arrivals in the accumulator lines
+    (rdx_device.hpp atomic_fold), and a block that never arrives ends the same way."""
     if not PROBE.exists():
         pytest.fail(f"{PROBE} missing: make -C reductionist-rs_amd probe")
-    ok = run(0, fold_last)
-    assert ok["status"] == 0 and ok["sum"] == ok["expect"]
-    for drop in (6, 128):          # a middle block, and the chunk's last block (the folder in fold-last form)
-        bad = run(drop, fold_last)
+    ok = run(0, fold_last, dt, op)
+    assert ok["status"] == 0 and ok["value"] == ok["expect"] and ok["again"] == ok["expect"], ok
+    for drop in (6, 128):         # a middle block, and the chunk's last block (the folder in fold-last form)
+        bad = run(drop, fold_last, dt, op)
         assert bad["status"] == 9, bad      # RDX_E_DEVICE
         assert bad["seconds"] < 30, bad

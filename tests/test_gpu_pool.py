@@ -342,12 +342,19 @@ def test_pool_eight_entries_one_gpu(torch, n_threads):
     stats, pb = placed()
     reqs = [s["requests"] for s in stats]
     assert sum(reqs) == n_req and sum(pb) == sum(len(base[k][2]) for k, _ in work)
-    mean = sum(pb) / 8
-    print("mixed: requests per entry", reqs, "placed MiB", [round(b / 2**20) for b in pb])
-    # gross misplacement only (all work on a few entries): with eight entries on ONE GPU the entries' streams
-    # share its 4 hardware queues unevenly, so an entry whose requests finish faster is rightly given more
-    # (observed up to 2.7 x the mean, round 5); the strict bound is the uniform case's peak below
-    assert all(r > 0 for r in reqs) and all(0.1 * mean <= b <= 4.0 * mean for b in pb), (reqs, pb)
+    peaks = [s["peak_outstanding_bytes"] for s in stats]
+    wmax = max(len(c[2]) for c in base) + (64 << 10)      # the heaviest request's placement weight
+    bound = (-(-n_threads // 8) + 1) * wmax
+    print("mixed: requests per entry", reqs, "placed MiB", [round(b / 2**20) for b in pb],
+          "peak in flight / max weight", [round(p / wmax, 2) for p in peaks])
+    # What least-outstanding placement keeps is the work IN FLIGHT per entry, not cumulative bytes: each
+    # request goes to the entry holding the least, which is at most the mean of the other T - 1 callers'
+    # weights, so no entry ever holds more than ceil(T / 8) heaviest requests plus the one being placed
+    # (racing placements on the relaxed loads included).  Cumulative bytes are not balanced by design: with
+    # eight entries on one GPU an entry whose requests finish faster is rightly given more (round 5: entry 0,
+    # 2.69 x the mean).
+    assert all(r > 0 for r in reqs), reqs
+    assert all(p <= bound for p in peaks), (peaks, bound)
     assert all(s["device"] == 0 and s["workspaces_busy"] == 0 and s["outstanding_bytes"] == 0 for s in stats)
     assert all(s["workspaces"] <= s["max_workspaces"] for s in stats)
     assert sum(s["coalesced_requests"] + s["direct_requests"] for s in stats) > 0
