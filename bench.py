@@ -931,7 +931,8 @@ def leg_native_concurrent(cx):
     (app.rs:147-152): 1 thread and the worker-pool size (num_cpus - 1, capped at the box's CPU share).
       device:   each thread its own workspace + stream, rdx_execute_device + synchronize per request
                 (independent launches);
-      resident: rdx_execute_resident on the context's pool — concurrent small all-axes requests are
+      resident: rdx_execute_resident on the context's pool (c2: one 64 MiB chunk per request, the result seen
+                in a page-locked host slot instead of a stream synchronize) — concurrent small all-axes requests are
                 coalesced by the pool's dispatcher into shared launches (same-plan groups / k_multi), each
                 caller's result written to page-locked host memory by the fold; an idle entry runs the
                 request on the caller's own thread (the direct fast path, direct_requests);
@@ -952,7 +953,8 @@ def leg_native_concurrent(cx):
                                      ("c1", 4 * pool, 1000, "resident"),
                                      ("s1", 1, 2000, "owned"), ("s1", pool, 2000, "owned"),
                                      ("h4f32", 1, 1000, "owned"), ("h4f64", 1, 1000, "owned"),
-                                     ("c2", 1, 300, "device"), ("c2", 4, 300, "device")):
+                                     ("c2", 1, 300, "device"), ("c2", 4, 300, "device"),
+                                     ("c2", 1, 300, "resident"), ("c2", 4, 300, "resident")):
         out.append(conc_bench(cfg, threads, reqs, path))
     return out
 
