@@ -333,154 +333,106 @@ __global__ __launch_bounds__(kBlock) void k_all_contig(const KAllContig a) {
             consume<T, OP, MK>(r, load_elem<T, FUSED>(base, a.src.plane, bswap, e), a, e);
     }
     // vector body: full tiles split into contiguous per-workgroup ranges, UNR tiles in flight per
-    // lane; the one partial tile (if any) goes to workgroup 0 with the scalar head/tail.  With a dynamic
-    // tail (a.dyn_piece > 0) each workgroup's own range is shorter and the chunk's last tiles are handed out
-    // in pieces to the workgroups that finish first (below).  (Round 2's form, every tile claimed at run
-    // time from one shared counter, measured slower: profiles/r02_pool_ab.jsonl.)
+    // lane; the one partial tile (if any) goes to workgroup 0 with the scalar head/tail.  (A dynamic
+    // hand-out of the last tiles to the workgroups that finish first was measured slower: the claim
+    // round trips cost more than the imbalance, profiles/r02_pool_ab.jsonl.)
     const uint64_t te = tile_elems<T, FUSED>();
     const uint64_t nfull = (vb - va) / te;
-    const bool dyn = a.dyn_piece != 0;
-    const uint64_t per = dyn ? a.dyn_static : (nfull + bpc - 1) / bpc;
-    const uint64_t first_dyn = dyn ? (uint64_t)bpc * per : nfull;   // first tile of the handed-out tail
+#if RDX_TILE_STRIDE
+    // tiles b, b + bpc, b + 2 bpc, ...: the chunk's workgroups sweep it together, a window of bpc tiles
+    // wide (few DRAM pages / translations live at once) instead of bpc separate streams
+    const uint64_t kstride = bpc, k0 = b;
+    const uint64_t nk = b < nfull ? (nfull - b + bpc - 1) / bpc : 0;
+#else
+    const uint64_t per = (nfull + bpc - 1) / bpc;
     const uint64_t t_begin = (uint64_t)b * per;
-    const uint64_t t_lim = first_dyn < nfull ? first_dyn : nfull;
-    const uint64_t t_end = t_begin + per < t_lim ? t_begin + per : t_lim;
+    const uint64_t t_end = t_begin + per < nfull ? t_begin + per : nfull;
+    const uint64_t kstride = 1, k0 = t_begin;
     const uint64_t nk = t_end > t_begin ? t_end - t_begin : 0;
-
-    // tiles k0 .. k0 + n - 1 of the chunk into `acc`, UNR tiles in flight per lane
-    auto run_tiles = [&](Red<T, OP> &acc, uint64_t k0, uint64_t n) {
-        auto tile = [&](uint64_t k) { return va + (k0 + k) * te; };   // first element of the k-th tile
-        uint64_t k = 0;
-        // Float min/max (the heaviest per-element fold) are software pipelined: the next UNR tiles'
-        // loads are issued before the current UNR tiles are consumed (two register sets, alternating),
-        // so a lane's fold work overlaps its next round trip (f32 min over 8 x 64 MiB 86 -> 80 us).  Sums
-        // keep the plain loop: pipelined they measured 1-3 % slower (78.6 -> 80.7 us, tools/gpu_pipe.sh).
-        if constexpr (kPipelined<T, OP, FUSED>) {
-            if (k + UNR <= n) {
-                Tile<T, FUSED> x[UNR], y[UNR];
-                auto tiles_at = [&](uint64_t k0_, uint64_t (&t)[UNR]) {
-#pragma unroll
-                    for (int u = 0; u < UNR; ++u) t[u] = tile(k0_ + u);
-                };
-                {
-                    uint64_t t[UNR];
-                    tiles_at(k, t);
-                    load_tiles<T, FUSED, UNR>(x, base, a.src.plane, t, vb);
-                }
-                while (true) {
-                    const bool m1 = k + 2 * UNR <= n;
-                    if (m1) {
-                        uint64_t t[UNR];
-                        tiles_at(k + UNR, t);
-                        load_tiles<T, FUSED, UNR>(y, base, a.src.plane, t, vb);
-                    }
-#pragma unroll
-                    for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(acc, x[u], a, tile(k + u), vb, selA, selB);
-                    k += UNR;
-                    if (!m1) break;
-                    const bool m2 = k + 2 * UNR <= n;
-                    if (m2) {
-                        uint64_t t[UNR];
-                        tiles_at(k + UNR, t);
-                        load_tiles<T, FUSED, UNR>(x, base, a.src.plane, t, vb);
-                    }
-#pragma unroll
-                    for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(acc, y[u], a, tile(k + u), vb, selA, selB);
-                    k += UNR;
-                    if (!m2) break;
-                }
-            }
-        } else if constexpr (kSplit8<T, OP, FUSED>) {
-            for (; k + UNR <= n; k += UNR) {
-                Tile<T, FUSED> x[UNR];
-                uint64_t t[UNR];
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) t[u] = tile(k + u);
-                load_tiles_split<T, FUSED, UNR>(x, base, a.src.plane, t);
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(acc, x[u], a, t[u], vb, selA, selB);
-            }
-        } else {
-            for (; k + UNR <= n; k += UNR) {
-                Tile<T, FUSED> x[UNR];
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + u), vb);
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(acc, x[u], a, tile(k + u), vb, selA, selB);
-            }
-        }
-        for (; k < n; ++k) {
-            Tile<T, FUSED> x0;
-            load_tile<T, FUSED, true>(x0, base, a.src.plane, tile(k), vb);
-            consume_tile<T, OP, FUSED, MK, true>(acc, x0, a, tile(k), vb, selA, selB);
-        }
+#endif
+#if RDX_TILE_ROT
+    // each workgroup starts its range at a different point and wraps (decorrelates the DRAM channels the
+    // workgroups of a chunk stream from at one time)
+    const uint64_t rot = nk ? ((uint64_t)b * 0x9E3779B1u) % nk : 0;
+    auto tile = [&](uint64_t k) {
+        uint64_t kk = k + rot;
+        kk -= kk >= nk ? nk : 0;
+        return va + (k0 + kk * kstride) * te;
     };
-    run_tiles(r, t_begin, nk);
+#else
+    auto tile = [&](uint64_t k) { return va + (k0 + k * kstride) * te; };   // first element of the k-th tile
+#endif
+    uint64_t k = 0;
+    // Float min/max (the heaviest per-element fold) are software pipelined: the next UNR tiles'
+    // loads are issued before the current UNR tiles are consumed (two register sets, alternating),
+    // so a lane's fold work overlaps its next round trip (f32 min over 8 x 64 MiB 86 -> 80 us).  Sums
+    // keep the plain loop: pipelined they measured 1-3 % slower (78.6 -> 80.7 us, tools/gpu_pipe.sh).
+    if constexpr (kPipelined<T, OP, FUSED>) {
+    if (k + UNR <= nk) {
+        Tile<T, FUSED> x[UNR], y[UNR];
+        auto tiles_at = [&](uint64_t k0_, uint64_t (&t)[UNR]) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) t[u] = tile(k0_ + u);
+        };
+        {
+            uint64_t t[UNR];
+            tiles_at(k, t);
+            load_tiles<T, FUSED, UNR>(x, base, a.src.plane, t, vb);
+        }
+        while (true) {
+            const bool m1 = k + 2 * UNR <= nk;
+            if (m1) {
+                uint64_t t[UNR];
+                tiles_at(k + UNR, t);
+                load_tiles<T, FUSED, UNR>(y, base, a.src.plane, t, vb);
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
+            k += UNR;
+            if (!m1) break;
+            const bool m2 = k + 2 * UNR <= nk;
+            if (m2) {
+                uint64_t t[UNR];
+                tiles_at(k + UNR, t);
+                load_tiles<T, FUSED, UNR>(x, base, a.src.plane, t, vb);
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, y[u], a, tile(k + u), vb, selA, selB);
+            k += UNR;
+            if (!m2) break;
+        }
+    }
+    } else if constexpr (kSplit8<T, OP, FUSED>) {
+    for (; k + UNR <= nk; k += UNR) {
+        Tile<T, FUSED> x[UNR];
+        uint64_t t[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) t[u] = tile(k + u);
+        load_tiles_split<T, FUSED, UNR>(x, base, a.src.plane, t);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, t[u], vb, selA, selB);
+    }
+    } else {
+    for (; k + UNR <= nk; k += UNR) {
+        Tile<T, FUSED> x[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) load_tile<T, FUSED, true>(x[u], base, a.src.plane, tile(k + u), vb);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) consume_tile<T, OP, FUSED, MK, true>(r, x[u], a, tile(k + u), vb, selA, selB);
+    }
+    }
+    for (; k < nk; ++k) {
+        Tile<T, FUSED> x0;
+        load_tile<T, FUSED, true>(x0, base, a.src.plane, tile(k), vb);
+        consume_tile<T, OP, FUSED, MK, true>(r, x0, a, tile(k), vb, selA, selB);
+    }
     if (b == 0 && va + nfull * te < vb) {
         Tile<T, FUSED> x0;
         load_tile<T, FUSED, false>(x0, base, a.src.plane, va + nfull * te, vb);
         consume_tile<T, OP, FUSED, MK, false>(r, x0, a, va + nfull * te, vb, selA, selB);
     }
-    if (!dyn) {
-        RDX_STAMP(1);
-        finalize_all<T, OP>(r, a.out, chunk, bpc, b);
-        return;
-    }
-    // ---- the dynamic tail: pieces of P tiles from first_dyn on, one claim (a returning atomic add on the
-    // chunk's claim word) per piece, the next piece's claim issued before the current piece streams.  Every
-    // workgroup makes exactly one claim that finds the pieces gone, so the claims of a launch number
-    // pieces + bpc and the workgroup holding the last one resets the word for the next launch.  A piece's
-    // partial depends only on its tiles (positions, lanes, block order), not on which workgroup streamed it:
-    // float sums keep one record per piece and fold them in piece order (deterministic); order-free folds
-    // (fold_last 2) merge pieces into the workgroup's own partial.
-    __shared__ uint32_t s_claim;
-    const uint32_t P = a.dyn_piece;
-    const uint64_t npieces = nfull > first_dyn ? (nfull - first_dyn + P - 1) / P : 0;
-    const uint64_t rpc = a.rec_per_chunk;
-    uint32_t *claim = a.out.tickets + (uint64_t)chunk * kTicketWords + kClaimWord;
-    const bool merge_in = kAtomicFold<T, OP> && a.out.fold_last == 2;
-    constexpr int kR = granules<T, OP>();
-    uint64_t *const recs = a.out.partials + (uint64_t)chunk * rpc * kR;
-    uint32_t next = 0;
-    if (threadIdx.x == 0) next = __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!merge_in) {   // the workgroup's own range as record b (the claim above is in flight meanwhile)
-        block_reduce(r);
-        if (threadIdx.x == 0) publish<T, OP>(recs + (uint64_t)b * kR, r, a.out.epoch);
-        r.init();
-    }
-    for (;;) {
-        if (threadIdx.x == 0) s_claim = next;
-        __syncthreads();
-        const uint32_t piece = s_claim;
-        __syncthreads();   // (s_claim is written again next round)
-        if (piece >= npieces) {
-            if (threadIdx.x == 0 && (uint64_t)piece == npieces + bpc - 1)
-                __hip_atomic_store(claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-        if (threadIdx.x == 0) next = __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t k0 = first_dyn + (uint64_t)piece * P;
-        const uint64_t n = nfull - k0 < P ? nfull - k0 : P;
-        if (merge_in) {
-            run_tiles(r, k0, n);
-        } else {
-            Red<T, OP> q;
-            q.init();
-            run_tiles(q, k0, n);
-            block_reduce(q);
-            if (threadIdx.x == 0) publish<T, OP>(recs + ((uint64_t)bpc + piece) * kR, q, a.out.epoch);
-        }
-    }
     RDX_STAMP(1);
-    if (merge_in) {
-        finalize_all<T, OP>(r, a.out, chunk, bpc, b);   // (fold_last 2: atomic_fold)
-        return;
-    }
-    if (a.out.fold_last && b != bpc - 1) {   // only the folder goes on
-        RDX_STAMP(2);
-        return;
-    }
-    arrive_and_fold<T, OP>(a.out, recs, chunk, bpc, (uint32_t)(bpc + npieces), b);
+    finalize_all<T, OP>(r, a.out, chunk, bpc, b);
 }
 
 // ---- strided views ---------------------------------------------------------------------------------

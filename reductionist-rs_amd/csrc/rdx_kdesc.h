@@ -88,17 +88,8 @@ struct KAllContig {
     int64_t r0, rs;
     uint32_t filter_semantics;  // Count(All) uses missing_filter (operations.rs:25-33)
     uint32_t blocks_per_chunk;
-    // Dynamic tail (k_all.hip): dyn_piece > 0 gives every workgroup dyn_static full tiles of its own and
-    // hands the chunk's remaining tiles out in pieces of dyn_piece tiles to whichever workgroup asks first
-    // (a per-chunk claim counter); each piece is its own record (rec_per_chunk = bpc + pieces) unless the
-    // fold is order-free.  0: static split only.
-    uint32_t dyn_piece;
-    uint32_t dyn_static;
-    uint32_t rec_per_chunk;
-    uint32_t pad_dyn;
     KChunkTable tbl;            // src.table: chunk pointers (last: only this much is read)
 };
-constexpr uint32_t kClaimWord = 32;   // per-chunk claim counter: u32 word of the ticket area's top line (own 128 B)
 
 // A strided view: dims innermost-first.  offset(e) = base_off + sum idx_k * vstride_k,
 // rank(e) = r0 + sum idx_k * rstride_k.

@@ -78,9 +78,6 @@ struct Tuning {
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
-    int dyn_tail = env_int("RDX_DYN_TAIL", 0);          // per mille of a chunk's tiles handed out at run time (k_all_contig)
-    int dyn_piece = env_int("RDX_DYN_PIECE", 4);        // tiles per handed-out piece
-    int dyn_min_tiles = env_int("RDX_DYN_MIN_TILES", 32);  // per workgroup, below which the split stays static
     int fold_last = env_int("RDX_FOLD_LAST", 2);                       // 2: + atomic folds, 1: records only, 0: arrival counters
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
@@ -448,21 +445,7 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             const int per_cu = p.dtype == RDX_DTYPE_FLOAT64 && p.op == RDX_OP_SUM && !p.fused && p.miss.kind == 0 &&
                                tuning().blocks_per_cu == 1 ? 2 : 0;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus, per_cu);
-            // dynamic tail: the last RDX_DYN_TAIL per mille of each chunk's full tiles go out in pieces at run
-            // time (k_all.hip) when every workgroup has enough tiles of its own that a piece is a small part
-            uint64_t recs = a.blocks_per_chunk;
-            {
-                const uint64_t full = a.n / te, bpc = a.blocks_per_chunk;
-                const int f = tuning().dyn_tail, P = tuning().dyn_piece;
-                if (f > 0 && f < 1000 && P > 0 && bpc > 1 && full / bpc >= (uint64_t)std::max(1, tuning().dyn_min_tiles)) {
-                    const uint64_t stat = full * (uint64_t)(1000 - f) / 1000 / bpc;
-                    a.dyn_piece = (uint32_t)P;
-                    a.dyn_static = (uint32_t)stat;
-                    recs = bpc + (full - bpc * stat + P - 1) / P;
-                    a.rec_per_chunk = (uint32_t)recs;
-                }
-            }
-            if ((st = ensure(ws, ws->partials, n_chunks * recs * kRecordU64, s, true))) return st;
+            if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
             out.tickets = ws->tickets.p;
