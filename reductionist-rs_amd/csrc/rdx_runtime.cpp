@@ -78,7 +78,8 @@ struct Tuning {
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
-    int fold_last = env_int("RDX_FOLD_LAST", 2);                       // 2: + atomic folds, 1: records only, 0: arrival counters
+    int fold_last = env_int("RDX_FOLD_LAST", 2);
+    int fold_last_pairs = env_int("RDX_FOLD_LAST_PAIRS", 0);   // fold-last also above kFoldLastChunks when bpc <= 2                       // 2: + atomic folds, 1: records only, 0: arrival counters
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
     int direct_max = env_int("RDX_DIRECT_MAX", 1);                     // idle-queue fast path: callers launching at once
@@ -445,6 +446,10 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
             const int per_cu = p.dtype == RDX_DTYPE_FLOAT64 && p.op == RDX_OP_SUM && !p.fused && p.miss.kind == 0 &&
                                tuning().blocks_per_cu == 1 ? 2 : 0;
             a.blocks_per_chunk = pick_bpc((a.n + te - 1) / te, n_chunks, ws->cus, per_cu);
+            // many chunks of one or two blocks each: a folder waits at most for its partner, the block just
+            // below it in dispatch order, which never waits itself, so fold-last is safe at any chunk count
+            if (!out.fold_last && tuning().fold_last && tuning().fold_last_pairs && a.blocks_per_chunk <= 2)
+                out.fold_last = fold_mode();
             if ((st = ensure(ws, ws->partials, n_chunks * a.blocks_per_chunk * kRecordU64, s, true))) return st;
             if ((st = ensure(ws, ws->tickets, n_chunks * kTicketWords, s, true))) return st;
             out.partials = ws->partials.p;
