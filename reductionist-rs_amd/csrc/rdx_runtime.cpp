@@ -78,8 +78,8 @@ struct Tuning {
     // few long contiguous rows: reduce each row as a chunk of the batched all-axes kernel
     int axis_rowbatch_kib = env_int("RDX_AXIS_ROWBATCH_KIB", 64);      // min row bytes (0 = off)
     int multi_blocks_per_cu = env_int("RDX_MULTI_BLOCKS_PER_CU", 5);   // k_multi fill target (5 resident per CU)
-    int fold_last = env_int("RDX_FOLD_LAST", 2);
-    int fold_last_pairs = env_int("RDX_FOLD_LAST_PAIRS", 0);   // fold-last also above kFoldLastChunks when bpc <= 2                       // 2: + atomic folds, 1: records only, 0: arrival counters
+    int fold_last = env_int("RDX_FOLD_LAST", 2);                       // 2: + atomic folds, 1: records only, 0: arrival counters
+    int fold_last_pairs = env_int("RDX_FOLD_LAST_PAIRS", 1);           // fold-last above kFoldLastChunks when bpc <= 2 (r06_fold_pairs_ab)
     int wait_spin = env_int("RDX_WAIT_SPIN", 200);                     // coalesced callers: pause spins, then futex
     int coalesce_depth = env_int("RDX_COALESCE_DEPTH", 1);            // launches in flight per coalescer stream (1-2)
     int direct_max = env_int("RDX_DIRECT_MAX", 1);                     // idle-queue fast path: callers launching at once
