@@ -35,9 +35,20 @@
 namespace rdx {
 namespace {
 
+// (A/B builds: RDX_B2_RING / RDX_B2_IN set the per-wave LDS, which bounds the waves per CU of k_blosc2_decode;
+// RDX_B2_WPE > 0 asks the compiler for that many waves per SIMD)
+#ifndef RDX_B2_RING
+#define RDX_B2_RING 8192
+#endif
+#ifndef RDX_B2_IN
+#define RDX_B2_IN 2048
+#endif
+#ifndef RDX_B2_WPE
+#define RDX_B2_WPE 0
+#endif
 constexpr uint32_t kWaves = 4;
-constexpr uint32_t kRing = 8192;
-constexpr uint32_t kInBytes = 2048, kInWords = kInBytes / 4, kStage = 1024;
+constexpr uint32_t kRing = RDX_B2_RING;
+constexpr uint32_t kInBytes = RDX_B2_IN, kInWords = kInBytes / 4, kStage = kInBytes / 2;
 constexpr uint32_t kUnit = 4096;   // memcpy'ed / special chunks: bytes per work item
 
 template <uint32_t R>
@@ -1309,7 +1320,11 @@ struct ZDec {
 
 }  // namespace
 
+#if RDX_B2_WPE > 0
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(RDX_B2_WPE))) void k_blosc2_decode(const KBlosc2Args a) {
+#else
 __global__ __launch_bounds__(64 * kWaves) void k_blosc2_decode(const KBlosc2Args a) {
+#endif
     __shared__ WaveLds LW[kWaves];
     // the wave index made scalar: the compiler's uniformity analysis does not see threadIdx.x >> 6 as
     // wave-uniform, and everything below (items, stream positions, the token chain) derives from it
