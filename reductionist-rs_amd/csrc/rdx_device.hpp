@@ -962,6 +962,7 @@ __device__ __forceinline__ int64_t rank_of_stored(uint64_t s) {   // 0 (nothing 
 }
 
 constexpr uint32_t kArriveBits = 20;   // {count << 20 | arrivals}: arrivals per line < 2^20, count < 2^44
+constexpr uint32_t kDirtyWord = 48;    // u32 index in the chunk's ticket top line: set by a fold that timed out
 // accumulator line of shard s (0..7) of the chunk: u64 words [0] count | arrivals, [1] value / sum,
 // [2] +0 rank, [3] -0 rank, [4] NaN flag
 __device__ __forceinline__ uint64_t *acc_line(const KOut &out, uint32_t chunk, uint32_t s) {
@@ -1008,15 +1009,27 @@ __device__ void atomic_fold(const Red<T, OP> &r, const KOut &out, uint32_t chunk
     const bool mine = lane < kTicketShards;
     uint64_t *L = acc_line(out, chunk, mine ? lane : 0);
     const uint32_t want = bpc - 1;
+    // A fold that timed out (a publisher that never arrived: a device fault, or one held back for seconds)
+    // cannot know whether its late publishers will still add to the lines it zeroed, so it leaves the chunk's
+    // DIRTY word set, and every later order-free fold of that workspace slot reports RDX_E_DEVICE instead of
+    // folding over stale words (read with the first poll: no extra round trip).  Only a new workspace clears it.
+    uint64_t *const dirty = reinterpret_cast<uint64_t *>(out.tickets + (uint64_t)chunk * kTicketWords + kDirtyWord);
     uint32_t fault = 0;
     for (uint32_t it = 0;; ++it) {
         const uint64_t w = mine ? __hip_atomic_load(L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        if (it == 0 && lane == kTicketShards && __hip_atomic_load(dirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            fault = 1;
         uint32_t got = (uint32_t)(w & ((1u << kArriveBits) - 1));
 #pragma unroll
         for (int m = 4; m >= 1; m >>= 1) got += __shfl_xor(got, m, 64);
+        if (__builtin_amdgcn_ballot_w64(fault != 0)) {
+            fault = 1;
+            break;
+        }
         if (__shfl(got, 0, 64) >= want) break;
         if (it >= kSpinLimit) {
             fault = 1;
+            if (lane == 0) __hip_atomic_store(dirty, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
         if (it < 2) __builtin_amdgcn_s_sleep(1);
