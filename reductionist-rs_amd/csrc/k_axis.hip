@@ -114,23 +114,6 @@ __device__ __forceinline__ void fold_value(Red<T, OP> &r, const KMissing &miss, 
     }
 }
 
-// f32 sums without a missing predicate: a load's VW elements are added pairwise in f64 and the loads of a
-// pass go to two alternating partial sums, so a lane's dependent chain of f64 adds is kU / 2 long per pass
-// instead of kU x VW (the axis kernels spent 37-44 % of their wave cycles issue-stalled with the memory
-// pipeline never full: profiles/r06_pmc_issue_stalls.json).  Integer-valued data stays exact.
-#ifndef RDX_AXIS_PAIR
-#define RDX_AXIS_PAIR 1
-#endif
-template <typename T, int OP, int MK>
-constexpr bool kPairF32 = RDX_AXIS_PAIR && OP == OP_SUM && std::is_same_v<T, float> && MK == MK_NONE;
-
-template <int VW>
-__device__ __forceinline__ double pair_sum(const float (&x)[VW]) {
-    if constexpr (VW == 1) return (double)x[0];
-    else if constexpr (VW == 2) return (double)x[0] + (double)x[1];
-    else return ((double)x[0] + (double)x[1]) + ((double)x[2] + (double)x[3]);
-}
-
 template <typename T, int OP, bool FUSED, int VW, bool GEN, int MK, int KU>
 __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
     constexpr bool RANK = Red<T, OP>::kRank;
@@ -181,27 +164,14 @@ __global__ __launch_bounds__(kBlock) void k_axis_rows(const KAxis a) {
             for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) raw_pin(raw[u]);
-            if constexpr (kPairF32<T, OP, MK>) {
-                double acc[2] = {0.0, 0.0};
 #pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    if (r0 + (uint64_t)u * L >= r_hi) continue;
-                    T x[VW];
-                    raw_cvt(raw[u], a.src.bswap, x);
-                    acc[u & 1] += pair_sum<VW>(x);
-                    r.cnt += VW;
-                }
-                r.s += acc[0] + acc[1];
-            } else {
+            for (int u = 0; u < kU; ++u) {
+                if (r0 + (uint64_t)u * L >= r_hi) continue;
+                T x[VW];
+                raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    if (r0 + (uint64_t)u * L >= r_hi) continue;
-                    T x[VW];
-                    raw_cvt(raw[u], a.src.bswap, x);
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) fold_value<T, OP, MK>(r, a.miss, x[j], rk[u] + (int64_t)j * rg.s0);
-                    if constexpr (MK == MK_NONE) r.cnt += VW;
-                }
+                for (int j = 0; j < VW; ++j) fold_value<T, OP, MK>(r, a.miss, x[j], rk[u] + (int64_t)j * rg.s0);
+                if constexpr (MK == MK_NONE) r.cnt += VW;
             }
         }
         group_reduce(r, L);
@@ -323,29 +293,14 @@ __global__ __launch_bounds__(kBlock) void k_axis_cols(const KAxis a) {
             for (int u = 0; u < kU; ++u) raw_load(raw[u], a.src.base, a.src.plane, (uint64_t)off[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) raw_pin(raw[u]);
-            if constexpr (kPairF32<T, OP, MK>) {
-                double acc[VW][2] = {};
 #pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    if (r0 + (uint64_t)u * step >= r_hi) continue;
-                    T x[VW];
-                    raw_cvt(raw[u], a.src.bswap, x);
+            for (int u = 0; u < kU; ++u) {
+                if (r0 + (uint64_t)u * step >= r_hi) continue;
+                T x[VW];
+                raw_cvt(raw[u], a.src.bswap, x);
 #pragma unroll
-                    for (int j = 0; j < VW; ++j) acc[j][u & 1] += (double)x[j];
-                    ++rows;
-                }
-#pragma unroll
-                for (int j = 0; j < VW; ++j) r[j].s += acc[j][0] + acc[j][1];
-            } else {
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    if (r0 + (uint64_t)u * step >= r_hi) continue;
-                    T x[VW];
-                    raw_cvt(raw[u], a.src.bswap, x);
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) fold_value<T, OP, MK>(r[j], a.miss, x[j], rk[u]);
-                    if constexpr (MK == MK_NONE) ++rows;
-                }
+                for (int j = 0; j < VW; ++j) fold_value<T, OP, MK>(r[j], a.miss, x[j], rk[u]);
+                if constexpr (MK == MK_NONE) ++rows;
             }
         }
     }
