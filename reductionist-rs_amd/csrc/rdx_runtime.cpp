@@ -72,6 +72,7 @@ struct Tuning {
 #if RDX_PROBES
     int axis_probe = env_int("RDX_AXIS_PROBE", 0);                     // phase probe (wrong results)
     int drop_block = env_int("RDX_DROP_BLOCK", 0);                     // fault injection: 1 + grid block
+    int drop_launches = env_int("RDX_DROP_LAUNCHES", 0);               // ... in this many launches only (0: all)
 #else
     int axis_probe = 0;   // product builds: the phase probe is compiled out (make EXTRA=-DRDX_PROBES=1)
 #endif
@@ -433,7 +434,11 @@ rdx_status run_device(rdx_workspace *ws, ExecPlan &p, const uint8_t *d_chunk, co
     // all-axes launches of few chunks: the last block of each chunk folds (no arrival counters)
     out.fold_last = n_chunks <= kFoldLastChunks && tuning().fold_last ? fold_mode() : 0u;
 #if RDX_PROBES
-    out.drop_block = (uint32_t)tuning().drop_block;
+    {
+        static std::atomic<int> launches{0};
+        const int k = launches.fetch_add(1, std::memory_order_relaxed);
+        out.drop_block = tuning().drop_launches <= 0 || k < tuning().drop_launches ? (uint32_t)tuning().drop_block : 0u;
+    }
 #endif
 
     switch (p.mode) {

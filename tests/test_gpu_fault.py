@@ -60,3 +60,34 @@ def test_missing_publisher_is_a_device_error(fold_last, dt, op):
         bad = run(drop, fold_last, dt, op)
         assert bad["status"] == 9, bad      # RDX_E_DEVICE
         assert bad["seconds"] < 30, bad
+
+
+SCRIPT_DIRTY = r"""
+import json, sys
+sys.path[:0] = [sys.argv[1] + "/reductionist-rs_amd", sys.argv[1]]
+import numpy as np
+from reductionist_amd import Engine, _abi
+eng = Engine([0])
+v = (np.arange(1 << 20) % 7).astype(np.int32)        # 4 MiB: 128 workgroups, an order-free fold (fold_last 2)
+req = _abi.CRequest("max", "int32")
+out = []
+for _ in range(3):
+    st, info, body, counts = eng.execute_raw(req, v.tobytes())
+    out.append(st)
+print(json.dumps({"statuses": out}))
+"""
+
+
+def test_timed_out_atomic_fold_poisons_its_slot():
+    """A fold that timed out (RDX_DROP_LAUNCHES=1: only the first launch loses a publisher) zeroes its lines but
+    cannot know whether the missing publisher will still add to them, so it sets the chunk slot's dirty word:
+    every later order-free fold on that workspace reports RDX_E_DEVICE instead of folding over stale words
+    (rdx_device.hpp atomic_fold)."""
+    if not PROBE.exists():
+        pytest.fail(f"{PROBE} missing: make -C reductionist-rs_amd probe")
+    env = dict(os.environ, RDX_LIB_PATH=str(PROBE), RDX_DROP_BLOCK="6", RDX_DROP_LAUNCHES="1", RDX_FOLD_LAST="2")
+    r = subprocess.run([sys.executable, "-c", SCRIPT_DIRTY, str(ROOT)], env=env, capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    st = json.loads(r.stdout.strip().splitlines()[-1])["statuses"]
+    assert st == [9, 9, 9], st   # RDX_E_DEVICE: the timed-out launch, then the poisoned slot
