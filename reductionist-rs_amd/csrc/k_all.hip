@@ -492,10 +492,7 @@ __device__ __forceinline__ void decompose(const KView &v, const DimRegs<ND> &d, 
 template <typename T, int OP, bool FUSED, int VW, int ND, int MK>
 __global__ __launch_bounds__(kBlock) void k_all_strided(const KAllStrided a) {
     RDX_STAMP(0);
-#ifndef RDX_STRIDED_KU
-#define RDX_STRIDED_KU 4   // (A/B builds) vectors in flight per lane for VW > 1; the host sizes the grid for 4
-#endif
-    constexpr int kU = VW > 1 ? RDX_STRIDED_KU : 8;
+    constexpr int kU = VW > 1 ? 4 : 8;
     const uint32_t bpc = a.blocks_per_chunk;
     const uint32_t chunk = blockIdx.x / bpc, b = blockIdx.x - chunk * bpc;
     const uint8_t *base = chunk_ptr(a, chunk);
