@@ -71,6 +71,19 @@ __constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65
 __constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 
 typedef const __attribute__((address_space(3))) uint32_t *lds_u32p;   // an LDS pointer: ds_read, not flat
+typedef __attribute__((address_space(3))) uint64_t *lds_u64p;
+// k_pinf_emit: a lane's short matches are recorded (position | (length | distance << 16) << 32) in its LDS
+// slots, kEmitRecs of them interleaved with the other lanes' (slot k of thread t at k * kEmitThreads + t),
+// and expanded after its decode loop ends: the loop itself writes no match bytes, so a wavefront's symbol
+// step no longer runs as long as the longest match any of its 64 lanes copies (an inner loop of up to 31
+// per-byte steps per symbol); a lane with more matches than slots writes the rest in the loop
+#ifndef RDX_PINF_EMIT_RECS
+#define RDX_PINF_EMIT_RECS 24
+#endif
+constexpr uint32_t kEmitRecs = RDX_PINF_EMIT_RECS;
+constexpr uint32_t kEmitThreads = kLanes / kPinfEmitSplit;   // k_pinf_emit's workgroup
+// its window of the stream: 16 KiB, a quarter of a 1024-lane block's lanes up to 512 K bits (past it, L2)
+constexpr uint32_t kEmitWin = kWinDwords * kPinfEmitSplit / 8;
 
 // ---- the stream as dwords from its 4-byte aligned base (bit positions in those coordinates) ------------
 struct Stream {
@@ -331,7 +344,10 @@ constexpr uint32_t kLongMatch = kPinfLongMatch;   // matches at least this long 
 template <bool EMIT>
 __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t stop, uint64_t end_bits,
                              uint64_t *exit, uint64_t *bytes, uint32_t *src, uint64_t o0, const PinfArgs *pa = nullptr,
-                             uint64_t limit = 0) {
+                             uint64_t limit = 0, uint32_t *stat = nullptr, lds_u64p rec = nullptr,
+                             uint32_t *n_rec = nullptr) {
+    // stat (EMIT, RDX_PINF_PROF): symbols, decodes past the root table, refills from L2 instead of LDS
+    uint32_t n_sym = 0, n_slow = 0, n_glob = 0;
     SrcOut out;
     if (EMIT) {
         out.p = src;
@@ -340,15 +356,25 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
     }
     uint64_t nb = 0;
     uint32_t r = 0;
+    // `stop` is used before the loop, as a distance: a value still in flight from a global load at the loop
+    // header made the compiler wait for every outstanding memory operation there — with EMIT, for the
+    // lane's source stores of the previous symbols, a round trip to memory per symbol
+    const uint64_t p0 = br.pos();
+    const uint64_t run = stop > p0 ? stop - p0 : 0;
     for (;;) {
         const uint64_t p = br.pos();
         if (p > end_bits) {
             r = 2;
             break;
         }
-        if (p >= stop) break;
+        if (p - p0 >= run) break;
+        if (EMIT && stat) {
+            ++n_sym;
+            n_glob += br.bc <= 32 && br.nxt - S.l0 >= S.ln ? 1u : 0u;
+        }
         br.refill(S);
         uint32_t e = T.lit[(uint32_t)br.bb & ((1u << kRoot) - 1)];
+        if (EMIT && stat) n_slow += ((e >> 16) & 15) == 0 ? 1u : 0u;
         if (((e >> 16) & 15) == 0) e = slow_decode(br.bb, T.lcount, T.lfirst, T.loffs, T.lsym, true, kRoot);
         br.drop((e >> 16) & 15);
         const uint32_t ty = e & (3u << 24);
@@ -376,6 +402,7 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
         br.drop(lx);
         br.refill(S);
         uint32_t d = T.dist[(uint32_t)br.bb & ((1u << kDRoot) - 1)];
+        if (EMIT && stat) n_slow += ((d >> 16) & 15) == 0 ? 1u : 0u;
         if (((d >> 16) & 15) == 0) d = slow_decode(br.bb, T.dcount, T.dfirst, T.doffs, T.dsym, false, kDRoot);
         if ((d & (3u << 24)) == kTyBad) {
             r = 2;
@@ -399,6 +426,10 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
             }
             if (slot < pa->mcap) {
                 out.skip(len);
+            } else if (rec && *n_rec < kEmitRecs) {
+                rec[*n_rec * kEmitThreads] = q | (uint64_t)(len | dist << 16) << 32;
+                ++*n_rec;
+                out.skip(len);
             } else if (dist >= len) {
                 for (uint32_t j = 0; j < len; ++j) out.put(base + j);
             } else {   // overlapping: byte j repeats byte (j mod dist) of the dist bytes before the match
@@ -412,6 +443,11 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
         nb += len;
     }
     if (EMIT) out.finish();
+    if (EMIT && stat) {
+        stat[0] = n_sym;
+        stat[1] = n_slow;
+        stat[2] = n_glob;
+    }
     *exit = br.pos();
     *bytes = nb;
     return r;
@@ -1370,20 +1406,26 @@ __global__ __launch_bounds__(kChainThreads) void k_pinf_chain(PinfArgs a) {
 }
 
 // ---- 4. sources of every output byte ----------------------------------------------------------------------
+// kPinfEmitSplit workgroups per chain block (consecutive blockIdx), workgroup g with lanes
+// [g * kEmitThreads, (g + 1) * kEmitThreads): its own window of the stream and its own tables
 __device__ void emit_body(const PinfArgs &a) {
     __shared__ Tabs T;
-    __shared__ uint64_t s_off[kLanes];
-    __shared__ uint32_t win[kWinDwords];
+    __shared__ uint64_t s_off[kEmitThreads];
+    __shared__ uint64_t s_red[kEmitThreads / 64];
+    __shared__ uint32_t win[kEmitWin];
+    __shared__ uint64_t s_rec[(kEmitRecs ? kEmitRecs : 1) * kEmitThreads];
     const uint32_t t = threadIdx.x;
-    const uint32_t c = a.chain[blockIdx.x];
-    const uint64_t o = a.coff[blockIdx.x];
+    const uint32_t bi = blockIdx.x / kPinfEmitSplit, g = blockIdx.x % kPinfEmitSplit;
+    const uint32_t lane = g * kEmitThreads + t;
+    const uint32_t c = a.chain[bi];
+    const uint64_t o = a.coff[bi];
     const PinfBlk B = a.blk[c];
     Stream S = make_stream(a);
     uint32_t *src = a.src;
     const uint32_t type = (uint32_t)(a.cand[c] & 3);
     if (type == 0) {   // stored: four bytes per thread and step, 16-byte stores where the quad is aligned
         const uint64_t q0 = B.body / 8;
-        for (uint64_t j = 4 * (uint64_t)t; j < B.bytes; j += 4 * kLanes) {
+        for (uint64_t j = 4 * (uint64_t)lane; j < B.bytes; j += 4 * kLanes) {
             const uint32_t w = S.at(8 * (q0 + j));
             const uint64_t d = o + j;
             const uint32_t k = (uint32_t)min<uint64_t>(4, B.bytes - j);
@@ -1397,38 +1439,82 @@ __device__ void emit_body(const PinfArgs &a) {
         return;
     }
     const uint32_t L = B.nlanes;
-    const uint64_t l0 = a.lst[(uint64_t)c * kLanes];
-    S.stage(win, kWinDwords, l0 >> 5, (B.end >> 5) + 2);
-    for (uint32_t i = t; i < 320; i += kLanes) T.lens[i] = a.lens[(uint64_t)c * 320 + i];
+    const uint32_t g0 = g * kEmitThreads;
+    if (g0 >= L) return;   // (the whole workgroup)
+    const uint64_t *const lst = a.lst + (uint64_t)c * kLanes;
+    const uint32_t *const lnb = a.lnb + (uint64_t)c * kLanes;
+    const uint32_t g1 = min(L, g0 + kEmitThreads);
+    S.stage(win, kEmitWin, lst[g0] >> 5, ((g1 < L ? lst[g1] : B.end) >> 5) + 2);
+    for (uint32_t i = t; i < 320; i += kEmitThreads) T.lens[i] = a.lens[(uint64_t)c * 320 + i];
+    // the output bytes of the block's lanes before this workgroup's (a block's bytes fit 32 bits)
+    uint32_t before = 0;
+    for (uint32_t k = t; k < g0; k += kEmitThreads) before += lnb[k];
+#pragma unroll
+    for (int d = 32; d; d >>= 1) before += (uint32_t)__shfl_xor((int)before, d, 64);
+    if ((t & 63) == 0) s_red[t >> 6] = before;
     __syncthreads();
+    before = 0;
+    for (uint32_t w = 0; w < kEmitThreads / 64; ++w) before += (uint32_t)s_red[w];
     build_tabs(T, B.nlen, B.ndist);
-    uint64_t *const prof = a.prof ? a.prof + 8ull * (kPinfMaxCand + blockIdx.x) : nullptr;
-    const uint32_t nb = t < L ? a.lnb[(uint64_t)c * kLanes + t] : 0;
+    uint64_t *const prof = a.prof && blockIdx.x < kPinfMaxCand ? a.prof + 8ull * (kPinfMaxCand + blockIdx.x) : nullptr;
+    const uint32_t nb = lane < L ? lnb[lane] : 0;
     // exclusive prefix of the lanes' bytes
     s_off[t] = nb;
     __syncthreads();
-    for (uint32_t d = 1; d < kLanes; d <<= 1) {
+    for (uint32_t d = 1; d < kEmitThreads; d <<= 1) {
         const uint64_t v = t >= d ? s_off[t - d] : 0;
         __syncthreads();
         s_off[t] += v;
         __syncthreads();
     }
     PINF_STAMP(1, wall_clock64());
-    if (t >= L) return;
-    const uint64_t my = o + s_off[t] - nb;
+    if (lane >= L) return;
+    const uint64_t my = o + before + s_off[t] - nb;
     Bits br;
-    br.seek(S, a.lst[(uint64_t)c * kLanes + t]);
-    const uint64_t stop = t + 1 < L ? a.lst[(uint64_t)c * kLanes + t + 1] : ~0ull;
+    br.seek(S, lst[lane]);
+    const uint64_t stop = lane + 1 < L ? lst[lane + 1] : ~0ull;
     uint64_t x, got;
-    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + nb);
-    const uint32_t want = t + 1 < L ? 0u : 1u;
+#ifndef RDX_PINF_LANESTAT
+#define RDX_PINF_LANESTAT 0   // tuning builds: RDX_PINF_PROF also reports emit's slowest lane (costs scratch)
+#endif
+#if RDX_PINF_LANESTAT
+    uint32_t stat[3] = {0, 0, 0};
+    const uint64_t tl = prof ? wall_clock64() : 0;
+    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + nb, prof ? stat : nullptr);
+#else
+    uint32_t n_rec = 0;
+    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + nb, nullptr,
+                                      (lds_u64p)s_rec + t, &n_rec);
+    // the recorded matches (checked against the output bounds when they were decoded)
+    for (uint32_t k = 0; k < n_rec; ++k) {
+        const uint64_t m = s_rec[k * kEmitThreads + t];
+        const uint32_t q = (uint32_t)m, len = (uint32_t)(m >> 32) & 0xffff, dist = (uint32_t)(m >> 48), base = q - dist;
+        if (dist >= len) {
+            for (uint32_t j = 0; j < len; ++j) src[q + j] = base + j;
+        } else {
+            uint32_t mm = 0;
+            for (uint32_t j = 0; j < len; ++j) {
+                src[q + j] = base + mm;
+                mm = mm + 1 == dist ? 0 : mm + 1;
+            }
+        }
+    }
+#endif
+    const uint32_t want = lane + 1 < L ? 0u : 1u;
     if (r != want || got != nb) atomicOr(&a.state->emit_err, 1u);
+#if RDX_PINF_LANESTAT
+    if (prof) {   // the slowest lane: [2] its decode time (ticks), [5] symbols, [6] past the root, [7] L2 refills
+        const uint64_t dt = wall_clock64() - tl;
+        const uint64_t mine = dt << 32 | (uint64_t)stat[0] << 16 | min(stat[1], 255u) << 8 | min(stat[2], 255u);
+        atomicMax((unsigned long long *)&prof[2], (unsigned long long)mine);
+    }
+#endif
 }
 
-__global__ __launch_bounds__(kLanes) void k_pinf_emit(PinfArgs a) {
+__global__ __launch_bounds__(kEmitThreads) void k_pinf_emit(PinfArgs a) {
     const uint64_t t0 = a.prof ? wall_clock64() : 0;
     emit_body(a);
-    if (a.prof) {
+    if (a.prof && blockIdx.x < kPinfMaxCand) {
         __syncthreads();
         if (threadIdx.x == 0) {
             a.prof[8 * (kPinfMaxCand + blockIdx.x)] = t0;
@@ -1797,7 +1883,7 @@ hipError_t launch_pinf_chain(const PinfArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_pinf_rest(const PinfArgs &a, uint32_t n_chain, uint64_t total, int cus, hipStream_t s) {
-    if (n_chain) hipLaunchKernelGGL(k_pinf_emit, dim3(n_chain), dim3(kLanes), 0, s, a);
+    if (n_chain) hipLaunchKernelGGL(k_pinf_emit, dim3(n_chain * kPinfEmitSplit), dim3(kEmitThreads), 0, s, a);
     if (a.mcap)
         hipLaunchKernelGGL(k_pinf_expand, dim3(std::min<uint32_t>(kExpandMaxBlocks, (a.mcap + 3) / 4)), dim3(256), 0, s, a);
     if (total) {

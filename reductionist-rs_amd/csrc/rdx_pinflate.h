@@ -10,6 +10,13 @@ constexpr uint32_t kPinfMaxCand = 4096;   // block-start candidates per stream (
 #define RDX_PINF_LANES 1024
 #endif
 constexpr uint32_t kPinfLanes = RDX_PINF_LANES;   // decode lanes per block (k_pinf_block / k_pinf_emit)
+#ifndef RDX_PINF_EMIT_SPLIT
+#define RDX_PINF_EMIT_SPLIT 4
+#endif
+// k_pinf_emit workgroups per chain block: each re-decodes kPinfLanes / kPinfEmitSplit of its lanes on a CU
+// of its own (a block's lanes on one CU share its four SIMDs' issue slots)
+constexpr uint32_t kPinfEmitSplit = RDX_PINF_EMIT_SPLIT;
+static_assert(kPinfLanes % (64 * kPinfEmitSplit) == 0, "whole waves per emit workgroup");
 constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
 #ifndef RDX_PINF_LONG_MATCH
 #define RDX_PINF_LONG_MATCH 32

@@ -766,7 +766,8 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
         RDX_HIP(hipMemcpy(blks.data(), a.blk, blks.size() * sizeof(PinfBlk), hipMemcpyDeviceToHost));
         RDX_HIP(hipMemcpy(chain.data(), a.chain, chain.size() * 4, hipMemcpyDeviceToHost));
         for (int k = 0; k < 2; ++k) {
-            const uint32_t n = k == 0 ? std::min(h.n_cand, kPinfMaxCand) : h.n_chain;
+            // (k_pinf_emit: kPinfEmitSplit workgroups per chain block)
+            const uint32_t n = k == 0 ? std::min(h.n_cand, kPinfMaxCand) : std::min(h.n_chain * kPinfEmitSplit, kPinfMaxCand);
             uint64_t lo = ~0ull, hi = 0, worst = 0;
             uint32_t wi = 0;
             std::vector<uint64_t> d;
@@ -779,7 +780,7 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
                 if (w[4] - w[0] > worst) { worst = w[4] - w[0]; wi = i; }
             }
             std::sort(d.begin(), d.end());
-            const uint32_t c = k == 0 ? wi : chain[wi];
+            const uint32_t c = k == 0 ? wi : chain[wi / kPinfEmitSplit];
             const uint64_t *w = &pr[8 * (k * kPinfMaxCand + wi)];
             auto us = [&](uint64_t x) { return x > w[0] ? (x - w[0]) / 100.0 : -1.0; };
             std::fprintf(stderr, "{\"pinf_prof\": \"%s\", \"wgs\": %zu, \"span_us\": %.1f, \"median_us\": %.1f, "
@@ -789,8 +790,11 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
                          (hi - lo) / 100.0, d.empty() ? 0.0 : d[d.size() / 2] / 100.0, worst / 100.0, c,
                          (unsigned)(keys[c] & 3), (unsigned long long)blks[c].bytes,
                          (unsigned long long)(blks[c].end - (keys[c] >> 2)), blks[c].nlanes, blks[c].status, us(w[1]),
-                         us(w[2]), us(w[3]), (unsigned long long)(k ? 0 : w[5]), k ? -1.0 : us(w[6]),
-                         (unsigned long long)(k ? 0 : w[7] & 0xffffffffu), (unsigned long long)(k ? 0 : w[7] >> 32));
+                         // (emit: t_pass0 = its slowest lane's decode, rounds / exts / walks = that lane's symbols,
+                         // decodes past the root table, refills from L2)
+                         k ? (w[2] >> 32) / 100.0 : us(w[2]), us(w[3]), (unsigned long long)(k ? (w[2] >> 16) & 0xffff : w[5]),
+                         k ? -1.0 : us(w[6]), (unsigned long long)(k ? (w[2] >> 8) & 0xff : w[7] & 0xffffffffu),
+                         (unsigned long long)(k ? w[2] & 0xff : w[7] >> 32));
         }
     }
     if (a.prof) {   // k_pinf_find: the slowest workgroup's phases

@@ -3,7 +3,7 @@ whose host zlib then decodes it — the plugin's route, integration/app_gpu.rs) 
 for the bench's chunk kinds, Z_FIXED streams (a fixed-Huffman block per 16 K symbols: declined), corrupt
 streams (declined) and a GNU gzip member.  For a declined stream also the old route: the device's
 sequential k_inflate (a context with inflate_fallback).  One JSON line per case.
-Usage: python tools/probe_pinflate.py [reps]"""
+Usage: python tools/probe_pinflate.py [reps] [filter: substrings of "<chunk>_<format><level>", comma-separated]"""
 import json
 import shutil
 import subprocess
@@ -56,12 +56,15 @@ def host(fmt, s):
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    keep = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     eng = Engine([0])
     ws = eng.workspace(0)
     eng_serial = Engine([0])
     eng_serial.configure(inflate_fallback=True)
     ws_serial = eng_serial.workspace(0)
     for name, fmt, level, raw, s in cases():
+        if keep and not any(k in f"{name}_{fmt}{level}" for k in keep):
+            continue
         d_in = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
         d_out = torch.empty(len(raw) + 16, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
