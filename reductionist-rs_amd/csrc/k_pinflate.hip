@@ -467,6 +467,27 @@ __device__ bool dyn_candidate(const SRC &S, uint64_t p, uint64_t end_bits) {
     return dyn_candidate_rest(S, p, end_bits, h, cb);
 }
 
+// The finder only (never the block parse, which accepts whatever oracle_inflate accepts): code-length
+// sequences that zlib's encoder (scan_tree / send_tree in trees.c, and GNU gzip's and miniz's, which run-length
+// code the same way) never writes.  A run of equal lengths is coded as few symbols as its rules allow, so a
+// run of zeros is 17 (3-10) or 18 (11-138) and only a remainder below 3 (at most 2 zeros, after an 18 or
+// alone) is written out; 16 repeats only a nonzero length; after a 17 the run has ended, so a nonzero length
+// follows.  A false survivor in random bits breaks one of these within a few symbols, where its Kraft sums
+// could only reject it after ~300 (the finder's slowest workgroup decoded one of those per lane).  A real
+// block whose encoder codes runs otherwise is not listed: the chain then reaches it as a miss, which the host
+// decodes (k_pinf_chain, pinflate_stream).
+#ifndef RDX_PINF_FIND_RLE
+#define RDX_PINF_FIND_RLE 1
+#endif
+constexpr bool kFindRle = RDX_PINF_FIND_RLE != 0;
+__device__ __forceinline__ bool rle_impossible(uint32_t sym, uint32_t psym, uint32_t z0, uint32_t prev) {
+    const bool zero_after_zero = sym == 0 && psym == 0 && z0 >= 2;    // a third explicit zero
+    const bool after17 = psym == 17 && (sym == 0 || sym >= 16);       // a zero run continued after a 17
+    const bool after0 = psym == 0 && sym >= 17;                       // 17 / 18 after explicit zeros
+    const bool rep_zero = sym == 16 && prev == 0;                     // 16 repeating a zero length
+    return zero_after_zero || after17 || after0 || rep_zero;
+}
+
 // A dynamic header's code lengths (STORE: into lens[]) with oracle_inflate's rules — a complete
 // code-length code, no repeat (16) first, no run past HLIT + HDIST, no over-subscribed literal / length or
 // distance code — and their Kraft sums (kl, kd: x 2^15), the distance codes used, whether the end-of-block
@@ -513,7 +534,7 @@ __device__ __forceinline__ bool header_lengths(const SRC &S, uint64_t &pos, uint
     uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
     uint32_t bc = 64 - (uint32_t)(pos & 31);
     nxt += 2;
-    uint32_t idx = 0, prev = 0;
+    uint32_t idx = 0, prev = 0, psym = 19, z0 = 0;
     kl = kd = used_d = 0;
     eob = false;
     bool bad = false, live = true;
@@ -538,6 +559,11 @@ __device__ __forceinline__ bool header_lengths(const SRC &S, uint64_t &pos, uint
             const uint32_t used = len + (s16 ? 2 : s17 ? 3 : s18 ? 7 : 0);
             const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
             bad |= (s16 && idx == 0) || idx + rep > total;
+            if (!STORE && kFindRle) {
+                bad |= rle_impossible(sym, psym, z0, prev);
+                z0 = sym == 0 ? z0 + 1 : 0;
+                psym = sym;
+            }
             if (STORE && !bad && val)   // (lens[] is zeroed by the caller: runs of zeros write nothing)
                 for (uint32_t r = 0; r < rep; ++r) lens[idx + r] = (uint8_t)val;
             const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
@@ -559,13 +585,16 @@ __device__ __forceinline__ bool header_lengths(const SRC &S, uint64_t &pos, uint
     return !bad;
 }
 
-// The same for k_pinf_block's parse, by the 64 lanes of one wave together (the wave is alone on the block's
-// critical path: one lane decoding ~300 symbols took 70-90 us, every step waiting on the previous one's
-// latency).  Lane k decodes the symbol that would start at bit base + k (all 64 candidates at once); the
-// chain of actual symbols is then followed with uniform lane reads (scalar work, ~14 symbols per 64-bit
-// window), and a nonzero run is stored by its lanes in parallel.  Same rules and results as
-// header_lengths<true>; every lane returns the same values.
-__device__ bool header_lengths_wave(const Stream &S, uint64_t &pos_io, uint64_t end_bits, uint64_t cb, uint32_t nl,
+// The same by the 64 lanes of one wave together (k_pinf_block's parse, k_pinf_find's open survivors: one
+// lane decoding ~300 symbols took 70-120 us, every step waiting on the previous one's latency).  Per 64-bit
+// window: lane k decodes the symbol that would start at bit pos + k (all 64 candidates at once); the chain
+// of actual symbols is followed with uniform lane reads, a few instructions a symbol; then every symbol's
+// effect at once on its lane — its table index by a prefix of the repeat counts, the value a 16 repeats,
+// the stores of its run, the Kraft sums by reductions (they only grow, so a sum past 1 at the window's end
+// is one past 1 at some symbol).  Same rules and results as header_lengths<true>; every lane returns the
+// same values.
+template <class SRC>
+__device__ bool header_lengths_wave(const SRC &S, uint64_t &pos_io, uint64_t end_bits, uint64_t cb, uint32_t nl,
                                     uint32_t nd, uint8_t *lens, uint32_t &kl_o, uint32_t &kd_o, uint32_t &used_d_o,
                                     bool &eob_o) {
     constexpr int kField[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
@@ -597,52 +626,69 @@ __device__ bool header_lengths_wave(const Stream &S, uint64_t &pos_io, uint64_t 
     }
     const uint64_t E = Sp >> 16;
     const uint32_t total = nl + nd;
-    uint64_t base = pos_io, pos = pos_io;
-    uint32_t off = 64;   // (forces the first window)
-    uint32_t symv = 0, usedv = 0, repv = 0;
+    const uint64_t below = (1ull << lane) - 1;
+    uint64_t pos = pos_io;
     uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0;
     bool eob = false, bad = false;
     while (!bad && idx < total) {
-        if (off >= 64) {   // this window: lane k decodes the symbol at bit base + k
-            base = pos;
-            off = 0;
-            const uint32_t v = S.at(base + lane);
-            const uint32_t j = __builtin_bitreverse32(v) >> 25;
-            uint32_t len = 1;
+        // this window: lane k decodes the symbol that would start at bit pos + k
+        const uint32_t v = S.at(pos + lane);
+        const uint32_t j = __builtin_bitreverse32(v) >> 25;
+        uint32_t len = 1;
 #pragma unroll
-            for (int l = 0; l < 6; ++l) len += ((uint32_t)(E >> (8 * l)) & 0xff) <= j ? 1u : 0u;
-            const uint32_t Sl = (uint32_t)(Sp >> (8 * len)) & 0xff, Ol = (uint32_t)(Op >> (8 * len)) & 0xff;
-            const uint32_t si = Ol + ((j - Sl) >> (7 - len));
-            symv = (uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31;
-            const uint32_t x = v >> len;
-            repv = symv == 16 ? 3 + (x & 3) : symv == 17 ? 3 + (x & 7) : symv == 18 ? 11 + (x & 127) : 1;
-            usedv = len + (symv == 16 ? 2 : symv == 17 ? 3 : symv == 18 ? 7 : 0);
+        for (int l = 0; l < 6; ++l) len += ((uint32_t)(E >> (8 * l)) & 0xff) <= j ? 1u : 0u;
+        const uint32_t Sl = (uint32_t)(Sp >> (8 * len)) & 0xff, Ol = (uint32_t)(Op >> (8 * len)) & 0xff;
+        const uint32_t si = Ol + ((j - Sl) >> (7 - len));
+        const uint32_t sym = (uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31;
+        const uint32_t x = v >> len;
+        const uint32_t rep = sym == 16 ? 3 + (x & 3) : sym == 17 ? 3 + (x & 7) : sym == 18 ? 11 + (x & 127) : 1;
+        const uint32_t used = len + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
+        // the actual symbols: the chain from lane 0 (uniform lane reads, a few instructions a symbol)
+        uint64_t M = 0;
+        uint32_t c = 0;
+        while (c < 64) {
+            M |= 1ull << c;
+            c += (uint32_t)__builtin_amdgcn_readlane((int)used, (int)c);
         }
-        const uint32_t sym = (uint32_t)__builtin_amdgcn_readlane((int)symv, (int)off);
-        const uint32_t rep = (uint32_t)__builtin_amdgcn_readlane((int)repv, (int)off);
-        const uint32_t used = (uint32_t)__builtin_amdgcn_readlane((int)usedv, (int)off);
-        const uint32_t val = sym == 16 ? prev : sym >= 17 ? 0 : sym;
-        if ((sym == 16 && idx == 0) || idx + rep > total) {
-            bad = true;
-            break;
+        const bool member = (M >> lane) & 1;
+        // their table indices: an exclusive prefix of the repeat counts over the chain
+        uint32_t incl = member ? rep : 0u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= (uint32_t)d) incl += o;
         }
-        if (val && lane < rep) lens[idx + lane] = (uint8_t)val;   // (zeroed by the caller)
-        const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
-        if (idx <= 256 && 256 < idx + nlit) eob = val != 0;
-        if (val) {
-            kl += nlit << (15 - val);
-            kd += ndst << (15 - val);
-            used_d += ndst;
-            if (kl > (1u << 15) || kd > (1u << 15)) {
-                bad = true;
-                break;
-            }
+        const uint32_t at = idx + incl - (member ? rep : 0u);
+        const bool valid = member && at < total;   // (chain symbols past the header are body bits)
+        // 16 repeats the value of the last symbol before it that is not a 16 (or the previous window's)
+        const uint32_t own = sym < 16 ? sym : 0u;
+        const uint64_t src = __ballot(member && sym != 16) & below;
+        const int sl = src ? 63 - __builtin_clzll(src) : 0;
+        const uint32_t from = (uint32_t)__shfl((int)own, sl, 64);
+        const uint32_t val = sym == 16 ? (src ? from : prev) : own;
+        const uint32_t nlit = at < nl ? min(rep, nl - at) : 0u, ndst = rep - nlit;
+        const bool fault = valid && ((sym == 16 && at == 0) || at + rep > total || pos + lane + used > end_bits);
+        if (valid && val && at + rep <= total)   // (lens[] is zeroed by the caller)
+            for (uint32_t r = 0; r < rep; ++r) lens[at + r] = (uint8_t)val;
+        uint32_t skl = valid && val ? nlit << (15 - val) : 0u, skd = valid && val ? ndst << (15 - val) : 0u;
+        uint32_t sud = valid && val ? ndst : 0u;
+#pragma unroll
+        for (int d = 32; d; d >>= 1) {
+            skl += (uint32_t)__shfl_xor((int)skl, d, 64);
+            skd += (uint32_t)__shfl_xor((int)skd, d, 64);
+            sud += (uint32_t)__shfl_xor((int)sud, d, 64);
         }
-        pos += used;
-        off += used;
-        idx += rep;
-        prev = val;
-        if (pos > end_bits) bad = true;
+        kl += skl;
+        kd += skd;
+        used_d += sud;
+        eob |= __ballot(valid && at <= 256 && 256 < at + nlit && val != 0) != 0;
+        bad = __ballot(fault) != 0 || kl > (1u << 15) || kd > (1u << 15);
+        // on past the last valid symbol
+        const uint64_t vm = __ballot(valid);
+        const int last = 63 - __builtin_clzll(vm);
+        pos += (uint32_t)__builtin_amdgcn_readlane((int)(lane + used), last);
+        idx = (uint32_t)__builtin_amdgcn_readlane((int)(at + rep), last);
+        prev = (uint32_t)__builtin_amdgcn_readlane((int)val, last);
     }
     pos_io = pos;
     kl_o = kl;
@@ -705,6 +751,10 @@ __device__ bool dyn_candidate_rest(const SRC &S, uint64_t p, uint64_t end_bits, 
 constexpr uint32_t kFindBytes = 8192, kFindLook = 640;
 constexpr uint32_t kFindWin = (kFindBytes + kFindLook) / 4 + 4;
 constexpr uint32_t kFindList = 8192 + 256;   // a round adds at most 8192; decoded once it holds 256
+#ifndef RDX_PINF_FIND_LANESYMS
+#define RDX_PINF_FIND_LANESYMS 32   // code-length symbols a lane decodes before a wave takes over (0: all)
+#endif
+constexpr uint32_t kFindLaneSyms = RDX_PINF_FIND_LANESYMS;
 
 struct WinStream {   // bit reads from the staged window only (positions inside it by construction)
     lds_u32p lds;
@@ -729,7 +779,13 @@ typedef __attribute__((address_space(3))) uint8_t *lds_u8p;
 constexpr uint32_t kFindLutStride = 132;   // bytes per lane's table: 33 dwords, lanes in different banks
 static_assert(kFindList * 4 >= 256 * kFindLutStride, "the survivor list's memory holds 256 tables");
 
-__device__ bool dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb, lds_u8p lut) {
+// Returns kCandNo / kCandYes, or kCandOpen when the header is still consistent after `cap` code-length symbols
+// (a real header, almost always, once the run-length rules have thrown out false ones: a whole wave then
+// decides it, header_lengths_wave — one lane walking a real header's ~300 symbols was the finder's slowest
+// step).
+enum : uint32_t { kCandNo = 0, kCandYes = 1, kCandOpen = 2 };
+__device__ uint32_t dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_bits, uint32_t h, uint64_t cb,
+                                      lds_u8p lut, uint32_t cap) {
     constexpr int kField[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};   // symbol -> field
     const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
     uint64_t pos = p + 17 + 3 * nc;
@@ -748,7 +804,7 @@ __device__ bool dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_b
         st += c << (7 - l);
         of += c;
     }
-    if (left != 0) return false;
+    if (left != 0) return kCandNo;
     uint64_t pk0 = 0, pk1 = 0, run = 0;
 #pragma unroll
     for (int sy = 0; sy < 19; ++sy) {
@@ -773,10 +829,10 @@ __device__ bool dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_b
     uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
     uint32_t bc = 64 - (uint32_t)(pos & 31);
     nxt += 2;
-    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0;
+    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0, psym = 19, z0 = 0, nsym = 0;
     bool eob = false, bad = false;
     uint32_t w = S.ld(nxt);
-    while (!bad && idx < total) {
+    while (!bad && idx < total && nsym++ < cap) {
         const bool need = bc < 32;
         bb |= need ? (uint64_t)w << (bc & 63) : 0;
         bc += need ? 32 : 0;
@@ -790,6 +846,11 @@ __device__ bool dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_b
         const uint32_t used = len + (s16 ? 2 : s17 ? 3 : s18 ? 7 : 0);
         const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
         bad |= (s16 && idx == 0) || idx + rep > total;
+        if (kFindRle) {
+            bad |= rle_impossible(sym, psym, z0, prev);
+            z0 = sym == 0 ? z0 + 1 : 0;
+            psym = sym;
+        }
         const uint32_t nlit = idx < nl ? min(rep, nl - idx) : 0u, ndst = rep - nlit;
         eob |= idx <= 256 && 256 < idx + nlit && val != 0;
         const uint32_t sh = 15 - val;
@@ -804,7 +865,9 @@ __device__ bool dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t end_b
         prev = val;
         bad |= pos > end_bits;
     }
-    return !bad && eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
+    if (bad) return kCandNo;
+    if (idx < total) return kCandOpen;
+    return eob && kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1) ? kCandYes : kCandNo;
 }
 
 __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
@@ -812,6 +875,9 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     __shared__ uint32_t list[kFindList];   // survivors: bit offsets from 8 * q0
     __shared__ uint32_t n_list;
     __shared__ uint16_t kraft4[4096];      // Kraft sum (x128) of four 3-bit code-length fields
+    __shared__ uint32_t open[256];         // survivors still consistent after kFindLaneSyms symbols
+    __shared__ uint32_t n_open;
+    __shared__ uint8_t wlens[4 * 320];     // a wave's code lengths while it decides one of them
     const uint32_t t = threadIdx.x, lane = t & 63;
     // RDX_PINF_PROF: (start, staged, last header pass, end, survivors) per workgroup, after k_pinf_emit's
     uint64_t *const prof = a.prof && blockIdx.x < kPinfMaxCand ? a.prof + 16ull * kPinfMaxCand + 8ull * blockIdx.x : nullptr;
@@ -835,10 +901,11 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     S.lds = (lds_u32p)win;
     S.l0 = l0;
     PinfState *st = a.state;
-    auto push = [&](uint64_t key) {
+    auto push = [&](uint64_t key) -> uint32_t {
         const uint32_t i = atomicAdd(&st->n_cand, 1u);
         if (i < kPinfMaxCand) a.cand[i] = key;
         else atomicOr(&st->overflow, 1u);
+        return i;
     };
     const uint64_t ts1 = prof ? wall_clock64() : 0;
     uint64_t ts2 = 0;
@@ -910,13 +977,46 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
                 // one survivor per thread; the list's memory becomes the threads' tables once each has its
                 // position
                 const uint32_t mine = t < n ? list[t] : 0u;
+                if (t == 0) n_open = 0;
                 __syncthreads();
                 if (t < n) {
                     const uint64_t p = 8 * q0 + mine;
                     const uint32_t h = S.at(p);
                     const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) &
                                         ((1ull << (3 * (((h >> 13) & 15) + 4))) - 1);
-                    if (dyn_candidate_lut(S, p, a.end_bits, h, cb, (lds_u8p)list + t * kFindLutStride)) push(p << 2 | 2);
+                    const uint32_t v = dyn_candidate_lut(S, p, a.end_bits, h, cb, (lds_u8p)list + t * kFindLutStride,
+                                                         kFindLaneSyms ? kFindLaneSyms : ~0u);
+                    if (v == kCandYes) push(p << 2 | 2);
+                    if (v == kCandOpen) open[atomicAdd(&n_open, 1u)] = mine;
+                }
+                __syncthreads();
+                // the still-open headers, one per wave at a time, all 64 lanes on it
+                for (uint32_t i = t >> 6; i < n_open; i += 4) {
+                    const uint64_t p = 8 * q0 + open[i];
+                    const uint32_t h = S.at(p);
+                    const uint32_t nl = ((h >> 3) & 31) + 257, nd = ((h >> 8) & 31) + 1, nc = ((h >> 13) & 15) + 4;
+                    const uint64_t cb = ((uint64_t)S.at(p + 17) | (uint64_t)S.at(p + 49) << 32) & ((1ull << (3 * nc)) - 1);
+                    uint8_t *const lens = wlens + 320 * (t >> 6);
+                    for (uint32_t k = lane; k < 320; k += 64) lens[k] = 0;
+                    uint64_t pos = p + 17 + 3 * nc;
+                    uint32_t kl, kd, used_d;
+                    bool eob;
+                    const bool ok = header_lengths_wave(S, pos, a.end_bits, cb, nl, nd, lens, kl, kd, used_d, eob) && eob &&
+                                    kl == (1u << 15) && (kd == (1u << 15) || used_d <= 1);
+                    if (ok) {
+                        // listed as parsed (type 3): its code lengths and body start for k_pinf_block, which
+                        // then skips the header parse
+                        uint32_t ci = lane == 0 ? push(p << 2 | 3) : 0u;
+                        ci = (uint32_t)__shfl((int)ci, 0, 64);
+                        if (ci < kPinfMaxCand) {
+                            for (uint32_t k = lane; k < 320; k += 64) a.lens[(uint64_t)ci * 320 + k] = lens[k];
+                            if (lane == 0) {
+                                a.blk[ci].body = pos;
+                                a.blk[ci].nlen = nl;
+                                a.blk[ci].ndist = nd;
+                            }
+                        }
+                    }
                 }
             } else
             for (uint32_t i0 = t; RDX_PINF_FIND_HDR && i0 < n + 255; i0 += 256) {
@@ -1021,7 +1121,15 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
     if (t < 64) {
         uint64_t body = 0;
         uint32_t nl = 0, nd = 0;
-        const bool ok = parse_header_wave(S, bit, type, a.end_bits, T, &body, &nl, &nd);
+        bool ok = true;
+        if (type == 3) {   // parsed by k_pinf_find (the same rules): its code lengths and body start
+            for (uint32_t i = t; i < 320; i += 64) T.lens[i] = a.lens[(uint64_t)ci * 320 + i];
+            body = B.body;
+            nl = B.nlen;
+            nd = B.ndist;
+        } else {
+            ok = parse_header_wave(S, bit, type, a.end_bits, T, &body, &nl, &nd);
+        }
         if (t == 0) {
             s_ok = ok ? 1 : 0;
             s_body = body;
@@ -1313,7 +1421,8 @@ __global__ __launch_bounds__(kChainThreads) void k_pinf_chain(PinfArgs a) {
             if ((sk[mid] >> 12) < k) lo = mid + 1;
             else hi = mid;
         }
-        if (lo < n && (sk[lo] >> 12) == k) return (int32_t)lo;
+        // (a dynamic block's candidate is type 2, or 3 when k_pinf_find parsed its header: the next key)
+        if (lo < n && ((sk[lo] >> 12) == k || (ty == 2 && (sk[lo] >> 12) == (k | 1)))) return (int32_t)lo;
         return -1;
     };
     for (uint32_t i = t; i < n; i += kChainThreads) {

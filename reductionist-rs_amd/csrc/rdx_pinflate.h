@@ -55,7 +55,8 @@ struct PinfArgs {
     uint64_t first_byte;    // the stream's first byte in aligned coordinates (its base's skew)
     uint64_t end_byte;      // first byte past it
     uint64_t end_bits;      // 8 * end_byte
-    uint64_t *cand;         // [kPinfMaxCand] bit << 2 | type (0 stored: bit of LEN; 1 fixed; 2 dynamic)
+    uint64_t *cand;         // [kPinfMaxCand] bit << 2 | type (0 stored: bit of LEN; 1 fixed; 2 dynamic;
+                            //  3 dynamic, its header parsed by k_pinf_find: lens, blk body / nlen / ndist set)
     PinfBlk *blk;           // [kPinfMaxCand]
     uint64_t *lst;          // [kPinfMaxCand][kPinfLanes] lane starts
     uint32_t *lnb;          // [kPinfMaxCand][kPinfLanes] lane output bytes

@@ -2,7 +2,8 @@
 (tuning aid, not product code): every bit offset screened as the finder does (BTYPE 2, HLIT / HDIST, a complete
 code-length code), then each survivor's code lengths decoded until rejected, printing the survivors' longest
 decodes (iterations = code-length symbols).  Usage: python tools/pinf_finder_sim.py [workgroup]"""
-import zlib, numpy as np, sys
+import os, zlib, numpy as np, sys
+RLE = os.environ.get("RLE", "0") == "1"   # the finder's run-length rules (k_pinflate.hip rle_impossible)
 rng = np.random.default_rng(0x5EED2000)
 v = rng.standard_normal(1 << 20).astype(np.float32)
 sh = v.view(np.uint8).reshape(-1, 4).T.copy().tobytes()
@@ -46,7 +47,7 @@ def decode_header(p, end_bits):
         if l:
             codes[(l, next_code[l])] = sym; next_code[l] += 1
     pos = p + 17 + 3 * nc
-    total = nl + nd; idx = 0; prev = 0; kl = kd = 0; it = 0
+    total = nl + nd; idx = 0; prev = 0; kl = kd = 0; it = 0; psym = 19; z0 = 0
     while idx < total:
         it += 1
         # decode one symbol msb-first
@@ -56,6 +57,11 @@ def decode_header(p, end_bits):
             if (l, cv) in codes: sym = codes[(l, cv)]; used = l; break
         if sym is None: return ('nosym', it)
         pos += used
+        if RLE and ((sym == 0 and psym == 0 and z0 >= 2) or (psym == 17 and (sym == 0 or sym >= 16))
+                    or (psym == 0 and sym >= 17) or (sym == 16 and prev == 0)):
+            return ('rle', it)
+        z0 = z0 + 1 if sym == 0 else 0
+        psym = sym
         if sym == 16:
             if idx == 0: return ('rep0', it)
             rep = 3 + getbits(pos, 2); pos += 2; val = prev
@@ -78,4 +84,5 @@ for byte in range(q0, min(q0 + 8192, len(s))):
         r = decode_header(8 * byte + b, 8 * len(s))
         if r is not None and r[0] not in ('over', 'incomplete'): res.append((8 * byte + b, r))
 its = sorted((r[1], r[0], p) for p, r in res)
-print("stream", len(s), "wg", wg, "survivors", len(res), "max iterations", its[-5:])
+print("stream", len(s), "wg", wg, "rle", RLE, "survivors", len(res), "max iterations", its[-5:],
+      "alive past 16/32/64/96:", [sum(1 for r in res if r[1][1] > k) for k in (16, 32, 64, 96)])
