@@ -53,7 +53,7 @@ constexpr uint32_t kRoot = 11, kDRoot = 9; // LDS root tables: literal/length, d
 constexpr uint32_t kFlag = 0x80000000u;    // a source that is a literal byte
 constexpr uint32_t kRounds = 6;            // resync rounds before a sequential walk
 #ifndef RDX_PINF_WARMBITS
-#define RDX_PINF_WARMBITS 128
+#define RDX_PINF_WARMBITS 256
 #endif
 constexpr uint64_t kWarmBits = RDX_PINF_WARMBITS;   // bits a lane decodes before its range in pass 0
 constexpr uint64_t kMaxSpan = 1ull << 21;  // bits a candidate may decode (a zlib block is < 1.6 M bits)
@@ -910,17 +910,18 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
     const uint64_t ts1 = prof ? wall_clock64() : 0;
     uint64_t ts2 = 0;
     uint32_t survivors = 0;   // (thread 0: this workgroup's, for the tuning counter)
+    uint64_t ts_open = 0;     // (RDX_PINF_PROF) the last pass's lane phase ended
+    uint32_t opens = 0;       // survivors handed to whole waves
     for (uint32_t r = 0; r < kFindBytes / 1024; ++r) {
         // this thread's 4 bytes: consecutive, so their 32 offsets' bits come from one 64-bit window
         const uint64_t qt = q0 + 1024 * r + 4 * t;
         const uint64_t w64 = (uint64_t)S.at(8 * qt) | (uint64_t)S.at(8 * qt + 32) << 32;
-        uint32_t cheap = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < 32; ++b) {
-            const uint32_t h = (uint32_t)(w64 >> b);
-            const bool pass = ((h >> 1) & 3) == 2 && ((h >> 3) & 31) <= 29 && ((h >> 8) & 31) <= 29 && qt + b / 8 < a.end_byte;
-            cheap |= pass ? 1u << b : 0u;
-        }
+        // all 32 offsets at once, bit b for offset b: BTYPE = 2 (bit b+1 clear, b+2 set), HLIT <= 29 (not bits
+        // b+4..b+7 all set), HDIST <= 29 (not bits b+9..b+12 all set), inside the stream
+        const uint64_t hl = (w64 >> 4) & (w64 >> 5) & (w64 >> 6) & (w64 >> 7);
+        const uint64_t hd = (w64 >> 9) & (w64 >> 10) & (w64 >> 11) & (w64 >> 12);
+        const uint64_t in = qt >= a.end_byte ? 0u : qt + 4 <= a.end_byte ? 0xffffffffu : (1u << (8 * (a.end_byte - qt))) - 1;
+        uint32_t cheap = (uint32_t)(~(w64 >> 1) & (w64 >> 2) & ~hl & ~hd & in);
         // the code-length code's Kraft sum (about a fifth of the offsets get here)
         uint32_t mask = 0;
         while (cheap) {
@@ -990,6 +991,8 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
                     if (v == kCandOpen) open[atomicAdd(&n_open, 1u)] = mine;
                 }
                 __syncthreads();
+                if (prof) ts_open = wall_clock64();
+                opens += n_open;
                 // the still-open headers, one per wave at a time, all 64 lanes on it
                 for (uint32_t i = t >> 6; i < n_open; i += 4) {
                     const uint64_t p = 8 * q0 + open[i];
@@ -1043,6 +1046,8 @@ __global__ __launch_bounds__(256) void k_pinf_find(PinfArgs a) {
             prof[2] = ts2;
             prof[3] = wall_clock64();
             prof[4] = survivors;
+            prof[5] = ts_open;
+            prof[6] = opens;
         }
     }
 }

@@ -815,8 +815,9 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
         auto us = [&](uint64_t x) { return x > w[0] ? (x - w[0]) / 100.0 : -1.0; };
         std::fprintf(stderr, "{\"pinf_prof\": \"find\", \"wgs\": %u, \"span_us\": %.1f, \"max_us\": %.1f, "
                      "\"survivors\": %llu, \"max_wg\": %u, \"t_staged\": %.1f, \"t_headers\": %.1f, "
-                     "\"wg_survivors\": %llu}\n", n, (hi - lo) / 100.0, worst / 100.0, (unsigned long long)surv, wi,
-                     us(w[1]), us(w[2]), (unsigned long long)w[4]);
+                     "\"wg_survivors\": %llu, \"t_lanes_done\": %.1f, \"wg_opens\": %llu}\n", n, (hi - lo) / 100.0,
+                     worst / 100.0, (unsigned long long)surv, wi, us(w[1]), us(w[2]), (unsigned long long)w[4], us(w[5]),
+                     (unsigned long long)w[6]);
     }
     // the sources of an unusually large stream are not kept at their high-water size
     if (ws->psrc.cap > kPinfKeepSources) {
