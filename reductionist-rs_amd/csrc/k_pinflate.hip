@@ -1516,6 +1516,15 @@ __global__ __launch_bounds__(kChainThreads) void k_pinf_chain(PinfArgs a) {
         st->n_chain = nc;
         st->total = total;
         st->status = status;
+        if (a.hslot) {   // the host's copy, polled (system-scope vector stores into page-locked memory)
+            const uint64_t T = (uint64_t)a.tag << 48;
+            const uint64_t mb = status == kPinfMiss ? s_miss : 0;
+            const uint64_t mt = status == kPinfMiss ? (S.at(mb) >> 1) & 3 : 0;
+            const uint64_t g0 = status | mt << 2 | (uint64_t)nc << 4 | (uint64_t)min(st->n_cand, 8191u) << 17;
+            __hip_atomic_store(a.hslot + 1, (total & kPinfPayload) | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.hslot + 2, (mb & kPinfPayload) | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.hslot + 0, g0 | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1978,6 +1987,9 @@ __global__ __launch_bounds__(64) void k_pinf_check(PinfArgs a, uint32_t parts) {
         ok = ok && want == crc && isz == (uint32_t)N;
     }
     st->final_ok = ok ? 1 : 0;
+    if (a.hslot)
+        __hip_atomic_store(a.hslot + 3, (ok ? 1u : 0u) | (uint64_t)min(st->emit_err, 255u) << 8 | (uint64_t)a.tag << 48,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace

@@ -71,7 +71,14 @@ struct PinfArgs {
     uint32_t mcap;
     uint32_t *tflag;        // [ceil(total / 32 KiB)] k_pinf_tile: the tile is literals only
     uint64_t *prof;         // RDX_PINF_PROF: per-workgroup (start, end) of k_pinf_block, then k_pinf_emit; else null
+    // page-locked coherent host memory, or null: tagged granules (payload | tag << 48) the host polls instead
+    // of copying the state back after a stream synchronise — [0..2] k_pinf_chain's verdict, [3] k_pinf_check's
+    uint64_t *hslot;
+    uint32_t tag;           // this launch's tag (1..65535)
 };
+// k_pinf_chain's granules: [0] status | miss_type << 2 | n_chain << 4 | min(n_cand, 8191) << 17, [1] total,
+// [2] miss_bit; k_pinf_check's: [3] final_ok | min(emit_err, 255) << 8
+constexpr uint64_t kPinfPayload = (1ull << 48) - 1;
 
 hipError_t launch_pinf_find(const PinfArgs &a, hipStream_t s);
 hipError_t launch_pinf_block(const PinfArgs &a, uint32_t first, uint32_t count, hipStream_t s);

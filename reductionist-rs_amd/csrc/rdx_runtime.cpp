@@ -173,6 +173,8 @@ struct rdx_workspace {
     DevBuf<uint64_t> cbor_rec;   // k_cbor_agg / k_cbor_scan: per-tile lengths, then offsets
     DevBuf<uint8_t> cbor_stage;  // k_cbor_pack: the tiles' encoded bytes (the staged form)
     PinfState *pinf_back = nullptr;
+    uint64_t *pinf_slot = nullptr;   // k_pinflate's tagged granules (PinfArgs::hslot), coherent page-locked
+    uint32_t pinf_tag = 0;
     // pipelined host path (map_pipelined): a second stream and one event per piece
     hipStream_t aux_stream = nullptr;
     hipEvent_t piece_ev[8] = {};
@@ -670,6 +672,28 @@ thread_local uint32_t g_inflate_path = RDX_INFLATE_PATH_NONE;
 // Returns RDX_OK with the stream's bytes in ws->raw (*raw_len of them), kNotDecoded when the sequential
 // decoder must run (an error anywhere, a chain it could not follow), or a device / memory error.
 const rdx_status kNotDecoded = static_cast<rdx_status>(254);
+
+// Wait for granules [i0, i1) of the pinflate slot to carry `tag` (a spin with pauses; the stream is asked
+// every 256 turns whether it has ended): false when it ended or failed without them — the caller then reads
+// the state back through the stream, which reports any device error.
+bool pinf_wait(const uint64_t *slot, uint32_t i0, uint32_t i1, uint32_t tag, hipStream_t s) {
+    auto fresh = [&] {
+        bool f = true;
+        for (uint32_t i = i0; i < i1; ++i) f &= (__atomic_load_n(slot + i, __ATOMIC_ACQUIRE) >> 48) == tag;
+        return f;
+    };
+    for (uint32_t it = 1;; ++it) {
+        if (fresh()) return true;
+        if ((it & 255) == 0) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) {
+                (void)hipGetLastError();
+                return e == hipSuccess && fresh();
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
 constexpr uint64_t kPinfKeepSources = 256ull << 20;   // source entries kept between streams (1 GiB)
 
 rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_t *d_src, uint64_t len, hipStream_t s,
@@ -708,14 +732,40 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
         RDX_HIP(hipMemsetAsync(ws->pprof.p, 0, 192ull * kPinfMaxCand, s));
         a.prof = ws->pprof.p;
     }
+    // the two points where the host needs the device's answer (the chain's verdict and size; the final check)
+    // are read from tagged granules the kernels write into page-locked memory, not by copying the state back
+    // after a stream synchronise (~20-40 us of idle device each, profiles/r06_pinflate_kernel_stats_final.csv)
+    if (!tuning().pinflate_prof) {
+        if (!ws->pinf_slot) {
+            RDX_HIP(hipHostMalloc((void **)&ws->pinf_slot, 4 * sizeof(uint64_t), hipHostMallocCoherent));
+            std::memset(ws->pinf_slot, 0, 4 * sizeof(uint64_t));
+        }
+        a.hslot = ws->pinf_slot;
+    }
+    auto next_tag = [&] {
+        ws->pinf_tag = ws->pinf_tag % 65535 + 1;
+        return ws->pinf_tag;
+    };
     RDX_HIP(hipMemsetAsync(a.state, 0, sizeof(PinfState), s));
     RDX_HIP(launch_pinf_find(a, s));
     RDX_HIP(launch_pinf_block(a, 0, kPinfMaxCand, s));
     PinfState &h = *ws->pinf_back;
     for (uint32_t forced = 0;; ++forced) {
+        a.tag = next_tag();
         RDX_HIP(launch_pinf_chain(a, s));
-        RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
-        RDX_HIP(hipStreamSynchronize(s));
+        if (a.hslot && pinf_wait(a.hslot, 0, 3, a.tag, s)) {
+            const uint64_t g0 = a.hslot[0], g1 = a.hslot[1], g2 = a.hslot[2];
+            h.status = (uint32_t)(g0 & 3);
+            h.miss_type = (uint32_t)(g0 >> 2) & 3;
+            h.n_chain = (uint32_t)(g0 >> 4) & 8191;
+            h.n_cand = (uint32_t)(g0 >> 17) & 8191;
+            h.total = g1 & kPinfPayload;
+            h.miss_bit = g2 & kPinfPayload;
+            h.overflow = 0;
+        } else {
+            RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
+            RDX_HIP(hipStreamSynchronize(s));
+        }
         if (h.status != kPinfMiss) break;
         // a block start no candidate covers (a fixed-Huffman block, or a header the finder's zlib-encoder
         // rules reject): decode that one block and follow the chain again
@@ -753,9 +803,16 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
     a.mcap = (uint32_t)mcap;
     a.tflag = ws->psrc.p + msta + 4 * mcap;
     a.out = ws->raw.p;
+    a.tag = next_tag();
     RDX_HIP(launch_pinf_rest(a, h.n_chain, total, ws->cus, s));
-    RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
-    RDX_HIP(hipStreamSynchronize(s));
+    if (a.hslot && pinf_wait(a.hslot, 3, 4, a.tag, s)) {
+        const uint64_t g3 = a.hslot[3];
+        h.final_ok = (uint32_t)(g3 & 1);
+        h.emit_err = (uint32_t)(g3 >> 8) & 0xff;
+    } else {
+        RDX_HIP(hipMemcpyAsync(&h, a.state, sizeof(PinfState), hipMemcpyDeviceToHost, s));
+        RDX_HIP(hipStreamSynchronize(s));
+    }
     if (a.prof) {   // tuning: the slowest workgroups of k_pinf_block / k_pinf_emit, phase by phase
         std::vector<uint64_t> pr(24ull * kPinfMaxCand);
         std::vector<uint64_t> keys(kPinfMaxCand);
@@ -1045,6 +1102,7 @@ void destroy_workspace(rdx_workspace *ws) {
     if (ws->h_back) (void)hipHostFree(ws->h_back);
     if (ws->h_slot) (void)hipHostFree(ws->h_slot);
     if (ws->pinf_back) (void)hipHostFree(ws->pinf_back);
+    if (ws->pinf_slot) (void)hipHostFree(ws->pinf_slot);
     fr(ws->pinf.p);
     fr(ws->psrc.p);
     fr(ws->pprof.p);
