@@ -164,13 +164,14 @@ struct Bits {
 // Per code: count[len] (count[0] = unused symbols), first[len] = the first canonical code of that length
 // and offs[len] = its first symbol's index in sym[] (puff's running `first` / `index`), the symbols in
 // canonical order, and a root table of 2^root entries (codes up to `root` bits in one lookup).
-struct Tabs {
+struct alignas(16) Tabs {
     uint32_t lit[1u << kRoot];
     uint32_t dist[1u << kDRoot];
     uint16_t lcount[16], dcount[16], lfirst[16], dfirst[16], loffs[16], doffs[16];
     uint16_t lsym[288], dsym[32];
     uint8_t lens[320];
 };
+static_assert(sizeof(Tabs) % 16 == 0 && sizeof(Tabs) <= kPinfTabBytes, "PinfArgs::tabs slot");
 
 __device__ __forceinline__ uint32_t entry_of(uint32_t s, bool litlen) {
     if (litlen) {
@@ -1151,8 +1152,12 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
         return;
     }
     PINF_STAMP(1, wall_clock64());
-    // keep the code lengths: k_pinf_emit rebuilds the tables from them
-    for (uint32_t i = t; i < 320; i += kLanes) a.lens[(uint64_t)ci * 320 + i] = T.lens[i];
+    // keep the built tables: k_pinf_emit's workgroups copy them instead of building them again
+    {
+        const uint4 *from = reinterpret_cast<const uint4 *>(&T);
+        uint4 *to = reinterpret_cast<uint4 *>(a.tabs + (uint64_t)ci * sizeof(Tabs));
+        for (uint32_t i = t; i < sizeof(Tabs) / 16; i += kLanes) to[i] = from[i];
+    }
     const uint64_t body = s_body;
     uint64_t E = next_cand(a, n, bit, s_red);
     for (uint32_t ext = 0; ext < 8; ++ext) {
@@ -1568,7 +1573,11 @@ __device__ void emit_body(const PinfArgs &a) {
     const uint32_t *const lnb = a.lnb + (uint64_t)c * kLanes;
     const uint32_t g1 = min(L, g0 + kEmitThreads);
     S.stage(win, kEmitWin, lst[g0] >> 5, ((g1 < L ? lst[g1] : B.end) >> 5) + 2);
-    for (uint32_t i = t; i < 320; i += kEmitThreads) T.lens[i] = a.lens[(uint64_t)c * 320 + i];
+    {   // the block's tables, as k_pinf_block built them
+        const uint4 *from = reinterpret_cast<const uint4 *>(a.tabs + (uint64_t)c * sizeof(Tabs));
+        uint4 *to = reinterpret_cast<uint4 *>(&T);
+        for (uint32_t i = t; i < sizeof(Tabs) / 16; i += kEmitThreads) to[i] = from[i];
+    }
     // the output bytes of the block's lanes before this workgroup's (a block's bytes fit 32 bits)
     uint32_t before = 0;
     for (uint32_t k = t; k < g0; k += kEmitThreads) before += lnb[k];
@@ -1578,7 +1587,6 @@ __device__ void emit_body(const PinfArgs &a) {
     __syncthreads();
     before = 0;
     for (uint32_t w = 0; w < kEmitThreads / 64; ++w) before += (uint32_t)s_red[w];
-    build_tabs(T, B.nlen, B.ndist);
     uint64_t *const prof = a.prof && blockIdx.x < kPinfMaxCand ? a.prof + 8ull * (kPinfMaxCand + blockIdx.x) : nullptr;
     const uint32_t nb = lane < L ? lnb[lane] : 0;
     // exclusive prefix of the lanes' bytes

@@ -18,6 +18,7 @@ constexpr uint32_t kPinfLanes = RDX_PINF_LANES;   // decode lanes per block (k_p
 constexpr uint32_t kPinfEmitSplit = RDX_PINF_EMIT_SPLIT;
 static_assert(kPinfLanes % (64 * kPinfEmitSplit) == 0, "whole waves per emit workgroup");
 constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
+constexpr uint64_t kPinfTabBytes = 11392;  // one block's decode tables (k_pinflate.hip Tabs)
 #ifndef RDX_PINF_LONG_MATCH
 #define RDX_PINF_LONG_MATCH 32
 #endif
@@ -60,7 +61,8 @@ struct PinfArgs {
     PinfBlk *blk;           // [kPinfMaxCand]
     uint64_t *lst;          // [kPinfMaxCand][kPinfLanes] lane starts
     uint32_t *lnb;          // [kPinfMaxCand][kPinfLanes] lane output bytes
-    uint8_t *lens;          // [kPinfMaxCand][320] code lengths
+    uint8_t *lens;          // [kPinfMaxCand][320] code lengths (k_pinf_find -> k_pinf_block)
+    uint8_t *tabs;          // [kPinfMaxCand][kPinfTabBytes] decode tables (k_pinf_block -> k_pinf_emit)
     uint32_t *chain;        // [kPinfMaxCand] candidate of each chain block
     uint64_t *coff;         // [kPinfMaxCand] its output offset
     PinfState *state;
