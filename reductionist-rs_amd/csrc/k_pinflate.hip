@@ -473,7 +473,7 @@ __device__ bool dyn_candidate(const SRC &S, uint64_t p, uint64_t end_bits) {
 // code the same way) never writes.  A run of equal lengths is coded as few symbols as its rules allow, so a
 // run of zeros is 17 (3-10) or 18 (11-138) and only a remainder below 3 (at most 2 zeros, after an 18 or
 // alone) is written out; 16 repeats only a nonzero length; after a 17 the run has ended, so a nonzero length
-// follows.  A false survivor in random bits breaks one of these within a few symbols, where its Kraft sums
+// follows; a run of a nonzero length is written out only up to three times (longer ones become 16s).  A false survivor in random bits breaks one of these within a few symbols, where its Kraft sums
 // could only reject it after ~300 (the finder's slowest workgroup decoded one of those per lane).  A real
 // block whose encoder codes runs otherwise is not listed: the chain then reaches it as a miss, which the host
 // decodes (k_pinf_chain, pinflate_stream).
@@ -481,12 +481,20 @@ __device__ bool dyn_candidate(const SRC &S, uint64_t p, uint64_t end_bits) {
 #define RDX_PINF_FIND_RLE 1
 #endif
 constexpr bool kFindRle = RDX_PINF_FIND_RLE != 0;
-__device__ __forceinline__ bool rle_impossible(uint32_t sym, uint32_t psym, uint32_t z0, uint32_t prev) {
+// `same`: explicit repeats of the previous nonzero length so far (counted within one code: zlib sends the
+// literal / length and distance lengths as two sequences, so three explicit L may end one and a fourth
+// start the other); `first_dist`: this symbol starts the distance lengths.
+__device__ __forceinline__ bool rle_impossible(uint32_t sym, uint32_t psym, uint32_t z0, uint32_t prev, uint32_t same,
+                                               bool first_dist) {
     const bool zero_after_zero = sym == 0 && psym == 0 && z0 >= 2;    // a third explicit zero
     const bool after17 = psym == 17 && (sym == 0 || sym >= 16);       // a zero run continued after a 17
     const bool after0 = psym == 0 && sym >= 17;                       // 17 / 18 after explicit zeros
     const bool rep_zero = sym == 16 && prev == 0;                     // 16 repeating a zero length
-    return zero_after_zero || after17 || after0 || rep_zero;
+    const bool fourth = sym - 1u < 15u && sym == psym && same >= 2 && !first_dist;   // a fourth explicit L
+    return zero_after_zero || after17 || after0 || rep_zero || fourth;
+}
+__device__ __forceinline__ uint32_t rle_same(uint32_t sym, uint32_t psym, uint32_t same, bool first_dist) {
+    return sym - 1u < 15u && sym == psym && !first_dist ? same + 1 : 0u;
 }
 
 // A dynamic header's code lengths (STORE: into lens[]) with oracle_inflate's rules — a complete
@@ -535,7 +543,7 @@ __device__ __forceinline__ bool header_lengths(const SRC &S, uint64_t &pos, uint
     uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
     uint32_t bc = 64 - (uint32_t)(pos & 31);
     nxt += 2;
-    uint32_t idx = 0, prev = 0, psym = 19, z0 = 0;
+    uint32_t idx = 0, prev = 0, psym = 19, z0 = 0, same = 0;
     kl = kd = used_d = 0;
     eob = false;
     bool bad = false, live = true;
@@ -561,7 +569,8 @@ __device__ __forceinline__ bool header_lengths(const SRC &S, uint64_t &pos, uint
             const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
             bad |= (s16 && idx == 0) || idx + rep > total;
             if (!STORE && kFindRle) {
-                bad |= rle_impossible(sym, psym, z0, prev);
+                bad |= rle_impossible(sym, psym, z0, prev, same, idx == nl);
+                same = rle_same(sym, psym, same, idx == nl);
                 z0 = sym == 0 ? z0 + 1 : 0;
                 psym = sym;
             }
@@ -830,7 +839,7 @@ __device__ uint32_t dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t e
     uint64_t bb = ((uint64_t)S.ld(nxt) | (uint64_t)S.ld(nxt + 1) << 32) >> (pos & 31);
     uint32_t bc = 64 - (uint32_t)(pos & 31);
     nxt += 2;
-    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0, psym = 19, z0 = 0, nsym = 0;
+    uint32_t idx = 0, prev = 0, kl = 0, kd = 0, used_d = 0, psym = 19, z0 = 0, nsym = 0, same = 0;
     bool eob = false, bad = false;
     uint32_t w = S.ld(nxt);
     while (!bad && idx < total && nsym++ < cap) {
@@ -848,7 +857,8 @@ __device__ uint32_t dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t e
         const uint32_t val = s16 ? prev : (s17 || s18) ? 0 : sym;
         bad |= (s16 && idx == 0) || idx + rep > total;
         if (kFindRle) {
-            bad |= rle_impossible(sym, psym, z0, prev);
+            bad |= rle_impossible(sym, psym, z0, prev, same, idx == nl);
+            same = rle_same(sym, psym, same, idx == nl);
             z0 = sym == 0 ? z0 + 1 : 0;
             psym = sym;
         }

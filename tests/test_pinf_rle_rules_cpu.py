@@ -1,6 +1,6 @@
 """k_pinf_find lists a dynamic-block header only when its code-length symbols follow the run-length coding of
 zlib's encoder (k_pinflate.hip `rle_impossible`: no third explicit zero, no zero run continued after a 17, no
-17 / 18 after an explicit zero, no 16 repeating a zero).  Real zlib / GNU gzip streams must never break those
+17 / 18 after an explicit zero, no 16 repeating a zero, no fourth explicit repeat of a length within one code).  Real zlib / GNU gzip streams must never break those
 rules, or their blocks would reach the chain as misses (correct, but decoded by the host).  This parses every
 dynamic header of real streams — CPython's zlib (the C library) at every level, strategy and memLevel over
 several data kinds, and GNU gzip when installed — and checks the rules on each.  (The rules are the encoder's
@@ -17,9 +17,14 @@ LEXT = [0] * 8 + [1] * 4 + [2] * 4 + [3] * 4 + [4] * 4 + [5] * 4 + [0]
 DEXT = [0, 0, 0, 0] + [i // 2 for i in range(2, 28)]
 
 
-def rle_impossible(sym, psym, z0, prev):   # the device rule, restated
+def rle_impossible(sym, psym, z0, prev, same, first_dist):   # the device rule, restated
     return ((sym == 0 and psym == 0 and z0 >= 2) or (psym == 17 and (sym == 0 or sym >= 16))
-            or (psym == 0 and sym >= 17) or (sym == 16 and prev == 0))
+            or (psym == 0 and sym >= 17) or (sym == 16 and prev == 0)
+            or (1 <= sym <= 15 and sym == psym and same >= 2 and not first_dist))
+
+
+def rle_same(sym, psym, same, first_dist):
+    return same + 1 if 1 <= sym <= 15 and sym == psym and not first_dist else 0
 
 
 class Reader:
@@ -80,7 +85,7 @@ def header_symbol_runs(raw):
                 while len(lens) < nl + nd:
                     sym, ln = dec(r, p, ct)
                     p += ln
-                    syms.append((sym, lens[-1] if lens else 0))
+                    syms.append((sym, lens[-1] if lens else 0, len(lens) == nl))
                     if sym < 16:
                         lens.append(sym)
                     elif sym == 16:
@@ -111,9 +116,10 @@ def header_symbol_runs(raw):
 def check(raw):
     runs = header_symbol_runs(raw)
     for syms in runs:
-        psym, z0 = 19, 0
-        for sym, prev in syms:
-            assert not rle_impossible(sym, psym, z0, prev), (sym, psym, z0, prev)
+        psym, z0, same = 19, 0, 0
+        for sym, prev, first_dist in syms:
+            assert not rle_impossible(sym, psym, z0, prev, same, first_dist), (sym, psym, z0, prev, same)
+            same = rle_same(sym, psym, same, first_dist)
             z0 = z0 + 1 if sym == 0 else 0
             psym = sym
     return len(runs)
@@ -151,9 +157,13 @@ def test_gnu_gzip_headers_follow_the_finders_rules():
 
 
 def test_rules_reject_what_they_should():
-    # a third explicit zero, a 17 continued by a zero, 18 after an explicit zero, 16 repeating a zero
-    assert rle_impossible(0, 0, 2, 0)
-    assert rle_impossible(0, 17, 0, 0) and rle_impossible(18, 17, 0, 0)
-    assert rle_impossible(17, 0, 1, 0)
-    assert rle_impossible(16, 18, 0, 0)
-    assert not rle_impossible(0, 18, 0, 0) and not rle_impossible(17, 18, 0, 0) and not rle_impossible(5, 17, 0, 0)
+    # a third explicit zero, a 17 continued by a zero, 18 after an explicit zero, 16 repeating a zero, a fourth
+    # explicit repeat of a length (but not across the literal / distance boundary)
+    assert rle_impossible(0, 0, 2, 0, 0, False)
+    assert rle_impossible(0, 17, 0, 0, 0, False) and rle_impossible(18, 17, 0, 0, 0, False)
+    assert rle_impossible(17, 0, 1, 0, 0, False)
+    assert rle_impossible(16, 18, 0, 0, 0, False)
+    assert rle_impossible(7, 7, 0, 7, 2, False) and not rle_impossible(7, 7, 0, 7, 2, True)
+    assert not rle_impossible(7, 7, 0, 7, 1, False)
+    assert not rle_impossible(0, 18, 0, 0, 0, False) and not rle_impossible(17, 18, 0, 0, 0, False)
+    assert not rle_impossible(5, 17, 0, 0, 0, False)

@@ -3,7 +3,8 @@
 code-length code), then each survivor's code lengths decoded until rejected, printing the survivors' longest
 decodes (iterations = code-length symbols).  Usage: python tools/pinf_finder_sim.py [workgroup]"""
 import os, zlib, numpy as np, sys
-RLE = os.environ.get("RLE", "0") == "1"   # the finder's run-length rules (k_pinflate.hip rle_impossible)
+RLE = os.environ.get("RLE", "0") == "1"
+RLE4 = os.environ.get("RLE4", "0") == "1"   # also: no fourth explicit repeat of a nonzero length   # the finder's run-length rules (k_pinflate.hip rle_impossible)
 rng = np.random.default_rng(0x5EED2000)
 v = rng.standard_normal(1 << 20).astype(np.float32)
 sh = v.view(np.uint8).reshape(-1, 4).T.copy().tobytes()
@@ -47,7 +48,7 @@ def decode_header(p, end_bits):
         if l:
             codes[(l, next_code[l])] = sym; next_code[l] += 1
     pos = p + 17 + 3 * nc
-    total = nl + nd; idx = 0; prev = 0; kl = kd = 0; it = 0; psym = 19; z0 = 0
+    total = nl + nd; idx = 0; prev = 0; kl = kd = 0; it = 0; psym = 19; z0 = 0; same = 0
     while idx < total:
         it += 1
         # decode one symbol msb-first
@@ -60,6 +61,9 @@ def decode_header(p, end_bits):
         if RLE and ((sym == 0 and psym == 0 and z0 >= 2) or (psym == 17 and (sym == 0 or sym >= 16))
                     or (psym == 0 and sym >= 17) or (sym == 16 and prev == 0)):
             return ('rle', it)
+        if RLE4 and 1 <= sym <= 15 and sym == psym and same >= 2:
+            return ('rle4', it)
+        same = same + 1 if (1 <= sym <= 15 and sym == psym) else 0
         z0 = z0 + 1 if sym == 0 else 0
         psym = sym
         if sym == 16:
