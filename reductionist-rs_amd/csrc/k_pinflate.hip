@@ -786,6 +786,7 @@ struct WinStream {   // bit reads from the staged window only (positions inside 
 #define RDX_PINF_FIND_LUT 1
 #endif
 typedef __attribute__((address_space(3))) uint8_t *lds_u8p;
+typedef __attribute__((address_space(3))) uint32_t *lds_u32w;
 constexpr uint32_t kFindLutStride = 132;   // bytes per lane's table: 33 dwords, lanes in different banks
 static_assert(kFindList * 4 >= 256 * kFindLutStride, "the survivor list's memory holds 256 tables");
 
@@ -824,15 +825,24 @@ __device__ uint32_t dyn_candidate_lut(const WinStream &S, uint64_t p, uint64_t e
         pk0 |= l && r < 12 ? (uint64_t)sy << (5 * r) : 0;
         pk1 |= l && r >= 12 ? (uint64_t)sy << (5 * (r - 12)) : 0;
     }
-    const uint64_t E = Sp >> 16;
-    for (uint32_t j = 0; j < 128; ++j) {
-        uint32_t len = 1;
+    // the table by runs: a code of length l is one run of 2^(7-l) entries of the 7-bit space, the codes of one
+    // length consecutive from S_l (a complete code fills all 128), runs of 4 or more as dword stores
 #pragma unroll
-        for (int l = 0; l < 6; ++l) len += ((uint32_t)(E >> (8 * l)) & 0xff) <= j ? 1u : 0u;
-        const uint32_t Sl = (uint32_t)(Sp >> (8 * len)) & 0xff, Ol = (uint32_t)(Op >> (8 * len)) & 0xff;
-        const uint32_t si = Ol + ((j - Sl) >> (7 - len));
-        const uint32_t sym = (uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31;
-        lut[j] = (uint8_t)(sym | len << 5);
+    for (uint32_t l = 1; l < 8; ++l) {
+        const uint32_t c = (uint32_t)(cnt >> (8 * l)) & 0xff;
+        const uint32_t S0 = (uint32_t)(Sp >> (8 * l)) & 0xff, O0 = (uint32_t)(Op >> (8 * l)) & 0xff;
+        constexpr uint32_t kSpan[8] = {0, 64, 32, 16, 8, 4, 2, 1};
+        const uint32_t span = kSpan[l];
+        for (uint32_t k = 0; k < c; ++k) {
+            const uint32_t si = O0 + k;
+            const uint32_t v = ((uint32_t)(si < 12 ? pk0 >> (5 * si) : pk1 >> (5 * (si - 12))) & 31) | l << 5;
+            const uint32_t st = S0 + k * span;
+            if (span >= 4) {
+                for (uint32_t q = 0; q < span; q += 4) ((lds_u32w)lut)[(st + q) >> 2] = v * 0x01010101u;
+            } else {
+                for (uint32_t q = 0; q < span; ++q) lut[st + q] = (uint8_t)v;
+            }
+        }
     }
     const uint32_t total = nl + nd;
     uint64_t nxt = pos >> 5;
@@ -1702,7 +1712,7 @@ __global__ __launch_bounds__(256) void k_pinf_expand(PinfArgs a) {
 // also writes its bytes.  k_pinf_xhop / k_pinf_xout (below) resolve the links between tiles.  Links always
 // point back (a copy source precedes its byte); one that does not, or a link further back than the window,
 // is an inconsistency (stale sources after a failed emit): the check rejects the stream.
-constexpr uint32_t kTile = 32768, kTileThreads = 1024;
+constexpr uint32_t kTile = kPinfTile, kTileThreads = 1024, kWindow = 32768;
 #ifndef RDX_PINF_TILE_HOPS
 #define RDX_PINF_TILE_HOPS 4
 #endif
@@ -1769,7 +1779,7 @@ __global__ __launch_bounds__(kTileThreads) void k_pinf_tile(PinfArgs a) {
             }
         }
     } else {         // the entries themselves, back over the tile's sources: literals, or links into the previous tile
-        const uint64_t base = T0 - kTile;   // (T0 > 0 here: tile 0 has no links out)
+        const uint64_t base = T0 >= kWindow ? T0 - kWindow : 0;   // (T0 > 0 here: tile 0 has no links out)
         auto chk = [&](uint32_t v) -> uint32_t {
             if (!(v & kFlag) && (T0 == 0 || v < base || v >= T0)) {
                 err = true;

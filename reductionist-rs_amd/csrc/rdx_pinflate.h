@@ -19,6 +19,11 @@ constexpr uint32_t kPinfEmitSplit = RDX_PINF_EMIT_SPLIT;
 static_assert(kPinfLanes % (64 * kPinfEmitSplit) == 0, "whole waves per emit workgroup");
 constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
 constexpr uint64_t kPinfTabBytes = 11392;  // one block's decode tables (k_pinflate.hip Tabs)
+#ifndef RDX_PINF_TILE
+#define RDX_PINF_TILE 32768
+#endif
+constexpr uint32_t kPinfTile = RDX_PINF_TILE;   // k_pinf_tile's tile of output entries (<= the 32 KiB window)
+static_assert(kPinfTile <= 32768 && (kPinfTile & (kPinfTile - 1)) == 0, "tile size");
 #ifndef RDX_PINF_LONG_MATCH
 #define RDX_PINF_LONG_MATCH 32
 #endif

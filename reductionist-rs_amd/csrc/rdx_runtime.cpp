@@ -793,7 +793,7 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
     // the output, the sources, the long-match records (at most total / kPinfLongMatch of them), the tiles'
     // flags: about 5.5 bytes of HBM per output byte.  An allocation that fails here declines the stream (the
     // sequential decoder needs only the output) instead of failing the request.
-    const uint64_t mcap = total / kPinfLongMatch, msta = (total + 3) / 4 * 4, tiles = (total + 32767) / 32768;
+    const uint64_t mcap = total / kPinfLongMatch, msta = (total + 3) / 4 * 4, tiles = (total + kPinfTile - 1) / kPinfTile;
     if ((st = ensure(ws, ws->raw, std::max<uint64_t>((total + 15) / 16 * 16, 16), s)) ||
         (st = ensure(ws, ws->psrc, std::max<uint64_t>(msta + 4 * mcap + tiles, 1), s))) {
         (void)hipGetLastError();
