@@ -63,12 +63,6 @@ constexpr uint32_t kWinDwords = 8192;      // LDS window of the stream per block
 // type 24-25 (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol)
 constexpr uint32_t kTyLen = 1u << 24, kTyEob = 2u << 24, kTyBad = 3u << 24;
 
-__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
-                                     193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 
 typedef const __attribute__((address_space(3))) uint32_t *lds_u32p;   // an LDS pointer: ds_read, not flat
 typedef __attribute__((address_space(3))) uint64_t *lds_u64p;
@@ -177,10 +171,17 @@ __device__ __forceinline__ uint32_t entry_of(uint32_t s, bool litlen) {
     if (litlen) {
         if (s < 256) return s;
         if (s == 256) return kTyEob;
-        if (s < 286) return c_lbase[s - 257] | (uint32_t)c_lext[s - 257] << 20 | kTyLen;
+        if (s < 286) {   // RFC 1951 3.2.5's length table in closed form (no constant-memory load)
+            const uint32_t k = s - 257, x = k < 8 || k == 28 ? 0u : (k - 8) / 4 + 1;
+            const uint32_t base = k == 28 ? 258u : k < 8 ? 3 + k : ((4 + (k & 3)) << x) + 3;
+            return base | x << 20 | kTyLen;
+        }
         return kTyBad;
     }
-    if (s < 30) return c_dbase[s] | (uint32_t)c_dext[s] << 20;
+    if (s < 30) {   // and its distance table
+        const uint32_t x = s < 4 ? 0u : s / 2 - 1, base = s < 4 ? 1 + s : ((2 + (s & 1)) << x) + 1;
+        return base | x << 20;
+    }
     return kTyBad;
 }
 
