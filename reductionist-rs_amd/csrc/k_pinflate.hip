@@ -57,7 +57,12 @@ constexpr uint32_t kRounds = 6;            // resync rounds before a sequential 
 #endif
 constexpr uint64_t kWarmBits = RDX_PINF_WARMBITS;   // bits a lane decodes before its range in pass 0
 constexpr uint64_t kMaxSpan = 1ull << 21;  // bits a candidate may decode (a zlib block is < 1.6 M bits)
-constexpr uint32_t kWinDwords = 8192;      // LDS window of the stream per block workgroup (32 KiB)
+#ifndef RDX_PINF_WIN
+#define RDX_PINF_WIN 8192
+#endif
+// LDS window of the stream per block workgroup: 32 KiB, 256 K bits from the header (past it a lane's refills
+// are L2 round trips; an 80 KiB window measured the same on 306 K-bit blocks, r06_pinflate_ab_window.jsonl)
+constexpr uint32_t kWinDwords = RDX_PINF_WIN;
 
 // decode-table entry: value in bits 0-15, code length 16-19 (0: longer than the root), extra bits 20-23,
 // type 24-25 (0 literal or distance, 1 length, 2 end of block, 3 invalid symbol)
@@ -77,7 +82,7 @@ typedef __attribute__((address_space(3))) uint64_t *lds_u64p;
 constexpr uint32_t kEmitRecs = RDX_PINF_EMIT_RECS;
 constexpr uint32_t kEmitThreads = kLanes / kPinfEmitSplit;   // k_pinf_emit's workgroup
 // its window of the stream: 16 KiB, a quarter of a 1024-lane block's lanes up to 512 K bits (past it, L2)
-constexpr uint32_t kEmitWin = kWinDwords * kPinfEmitSplit / 8;
+constexpr uint32_t kEmitWin = 8192 * kPinfEmitSplit / 8;
 
 // ---- the stream as dwords from its 4-byte aligned base (bit positions in those coordinates) ------------
 struct Stream {
