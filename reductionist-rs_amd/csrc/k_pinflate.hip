@@ -1423,9 +1423,23 @@ __global__ __launch_bounds__(kChainThreads) void k_pinf_chain(PinfArgs a) {
         s_p0 = 8 * q;
     }
     __syncthreads();
-    // bitonic sort of the candidate keys (only as many as there are, rounded up to a power of two)
+    // sort the candidate keys (unique: the index is in the low bits).  Up to one per thread: each key's rank
+    // by counting the smaller ones (uniform LDS reads, no barrier per stage); more: a bitonic sort of as many
+    // as there are, rounded up to a power of two
     uint32_t m = 2;
     while (m < n) m <<= 1;
+    if (n <= kChainThreads) {
+        uint64_t key = 0;
+        uint32_t rank = 0;
+        if (t < n) {
+            key = sk[t];
+            for (uint32_t j = 0; j < n; ++j) rank += sk[j] < key ? 1u : 0u;
+        }
+        __syncthreads();
+        if (t < n) sk[rank] = key;
+        __syncthreads();
+        m = 0;   // (no bitonic stages)
+    }
     for (uint32_t k = 2; k <= m; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t i = t; i < m; i += kChainThreads) {
