@@ -80,9 +80,14 @@ typedef __attribute__((address_space(3))) uint64_t *lds_u64p;
 #define RDX_PINF_EMIT_RECS 24
 #endif
 constexpr uint32_t kEmitRecs = RDX_PINF_EMIT_RECS;
-constexpr uint32_t kEmitThreads = kLanes / kPinfEmitSplit;   // k_pinf_emit's workgroup
-// its window of the stream: 16 KiB, a quarter of a 1024-lane block's lanes up to 512 K bits (past it, L2)
-constexpr uint32_t kEmitWin = 8192 * kPinfEmitSplit / 8;
+#ifndef RDX_PINF_EMIT_HALVES
+#define RDX_PINF_EMIT_HALVES 1
+#endif
+constexpr bool kEmitHalves = RDX_PINF_EMIT_HALVES != 0;        // two threads a lane (PinfArgs::lmid)
+constexpr uint32_t kEmitLanes = kLanes / kPinfEmitSplit;      // lanes per k_pinf_emit workgroup
+constexpr uint32_t kEmitThreads = kEmitHalves ? 2 * kEmitLanes : kEmitLanes;   // k_pinf_emit's workgroup
+// its window of the stream: 16 KiB, its lanes of a 1024-lane block up to 1 M bits (past it, L2)
+constexpr uint32_t kEmitWin = 8192 * 4 / kPinfEmitSplit;
 
 // ---- the stream as dwords from its 4-byte aligned base (bit positions in those coordinates) ------------
 struct Stream {
@@ -352,7 +357,7 @@ template <bool EMIT>
 __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t stop, uint64_t end_bits,
                              uint64_t *exit, uint64_t *bytes, uint32_t *src, uint64_t o0, const PinfArgs *pa = nullptr,
                              uint64_t limit = 0, uint32_t *stat = nullptr, lds_u64p rec = nullptr,
-                             uint32_t *n_rec = nullptr) {
+                             uint32_t *n_rec = nullptr, uint64_t mid_at = ~0ull, uint64_t *mid = nullptr) {
     // stat (EMIT, RDX_PINF_PROF): symbols, decodes past the root table, refills from L2 instead of LDS
     uint32_t n_sym = 0, n_slow = 0, n_glob = 0;
     SrcOut out;
@@ -375,6 +380,7 @@ __device__ uint32_t run_lane(const Tabs &T, const Stream &S, Bits &br, uint64_t 
             break;
         }
         if (p - p0 >= run) break;
+        if (!EMIT && mid && p >= mid_at && *mid == ~0ull) *mid = p | nb << 40;   // (k_pinf_block: the lane's middle)
         if (EMIT && stat) {
             ++n_sym;
             n_glob += br.bc <= 32 && br.nxt - S.l0 >= S.ln ? 1u : 0u;
@@ -1116,6 +1122,7 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
     __shared__ uint64_t s_st[kLanes], s_x[kLanes], s_red[kLanes / 64];
     static_assert(kLanes % 64 == 0 && kLanes <= 1024, "lanes per block");
     __shared__ uint32_t s_nb[kLanes];
+    __shared__ uint64_t s_mid[kLanes];   // the lane's first boundary at or past its middle | bytes before it << 40
     __shared__ uint8_t s_ed[kLanes];
     __shared__ uint32_t s_wm[kLanes / 64];
     __shared__ uint64_t s_body;
@@ -1195,12 +1202,15 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
         auto run = [&](uint32_t k, uint64_t from) {
             Bits br;
             br.seek(S, from);
-            uint64_t x, nb;
-            const uint32_t r = run_lane<false>(T, S, br, lo(k + 1), a.end_bits, &x, &nb, nullptr, 0);
+            uint64_t x, nb, md = ~0ull;
+            const uint64_t m = lo(k) + (lo(k + 1) - lo(k)) / 2;
+            const uint32_t r = run_lane<false>(T, S, br, lo(k + 1), a.end_bits, &x, &nb, nullptr, 0, nullptr, 0, nullptr,
+                                               nullptr, nullptr, kEmitHalves && from < m ? m : ~0ull, &md);
             s_st[k] = from;
             s_x[k] = x;
             s_nb[k] = (uint32_t)nb;
             s_ed[k] = (uint8_t)r;
+            s_mid[k] = md;
         };
         // pass 0: lane k > 0 first decodes kWarmBits before its range and starts at its first symbol
         // boundary at or past lo(k) — by then its parse has almost always resynchronised with the true one,
@@ -1299,6 +1309,7 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
                             s_st[j] = st;
                             s_x[j] = s_tx[q];
                             s_nb[j] = s_tnb[q];
+                            s_mid[j] = ~0ull;   // (not recorded by the tabulation)
                             s_ed[j] = s_ted[q];
                         } else {
                             run(j, st);   // (a symbol longer than kOff bits cannot occur)
@@ -1350,6 +1361,7 @@ __device__ void block_body(const PinfArgs &a, uint32_t first, uint32_t count) {
         if (t <= j) {
             a.lst[(uint64_t)ci * kLanes + t] = s_st[t];
             a.lnb[(uint64_t)ci * kLanes + t] = s_nb[t];
+            a.lmid[(uint64_t)ci * kLanes + t] = s_mid[t];
         }
         return;
     }
@@ -1584,7 +1596,7 @@ __device__ void emit_body(const PinfArgs &a) {
     __shared__ uint64_t s_rec[(kEmitRecs ? kEmitRecs : 1) * kEmitThreads];
     const uint32_t t = threadIdx.x;
     const uint32_t bi = blockIdx.x / kPinfEmitSplit, g = blockIdx.x % kPinfEmitSplit;
-    const uint32_t lane = g * kEmitThreads + t;
+    const uint32_t lane = g * kEmitLanes + (kEmitHalves ? t / 2 : t), half = kEmitHalves ? t & 1 : 0u;
     const uint32_t c = a.chain[bi];
     const uint64_t o = a.coff[bi];
     const PinfBlk B = a.blk[c];
@@ -1593,7 +1605,7 @@ __device__ void emit_body(const PinfArgs &a) {
     const uint32_t type = (uint32_t)(a.cand[c] & 3);
     if (type == 0) {   // stored: four bytes per thread and step, 16-byte stores where the quad is aligned
         const uint64_t q0 = B.body / 8;
-        for (uint64_t j = 4 * (uint64_t)lane; j < B.bytes; j += 4 * kLanes) {
+        for (uint64_t j = 4 * ((uint64_t)g * kEmitThreads + t); j < B.bytes; j += 4ull * kEmitThreads * kPinfEmitSplit) {
             const uint32_t w = S.at(8 * (q0 + j));
             const uint64_t d = o + j;
             const uint32_t k = (uint32_t)min<uint64_t>(4, B.bytes - j);
@@ -1607,11 +1619,11 @@ __device__ void emit_body(const PinfArgs &a) {
         return;
     }
     const uint32_t L = B.nlanes;
-    const uint32_t g0 = g * kEmitThreads;
+    const uint32_t g0 = g * kEmitLanes;
     if (g0 >= L) return;   // (the whole workgroup)
     const uint64_t *const lst = a.lst + (uint64_t)c * kLanes;
     const uint32_t *const lnb = a.lnb + (uint64_t)c * kLanes;
-    const uint32_t g1 = min(L, g0 + kEmitThreads);
+    const uint32_t g1 = min(L, g0 + kEmitLanes);
     S.stage(win, kEmitWin, lst[g0] >> 5, ((g1 < L ? lst[g1] : B.end) >> 5) + 2);
     {   // the block's tables, as k_pinf_block built them
         const uint4 *from = reinterpret_cast<const uint4 *>(a.tabs + (uint64_t)c * sizeof(Tabs));
@@ -1629,8 +1641,9 @@ __device__ void emit_body(const PinfArgs &a) {
     for (uint32_t w = 0; w < kEmitThreads / 64; ++w) before += (uint32_t)s_red[w];
     uint64_t *const prof = a.prof && blockIdx.x < kPinfMaxCand ? a.prof + 8ull * (kPinfMaxCand + blockIdx.x) : nullptr;
     const uint32_t nb = lane < L ? lnb[lane] : 0;
-    // exclusive prefix of the lanes' bytes
-    s_off[t] = nb;
+    const uint64_t mid = kEmitHalves && lane < L ? a.lmid[(uint64_t)c * kLanes + lane] : ~0ull;
+    // exclusive prefix of the lanes' bytes (a lane's bytes counted once, on its first half)
+    s_off[t] = half ? 0u : nb;
     __syncthreads();
     for (uint32_t d = 1; d < kEmitThreads; d <<= 1) {
         const uint64_t v = t >= d ? s_off[t - d] : 0;
@@ -1640,10 +1653,15 @@ __device__ void emit_body(const PinfArgs &a) {
     }
     PINF_STAMP(1, wall_clock64());
     if (lane >= L) return;
-    const uint64_t my = o + before + s_off[t] - nb;
+    // this thread's part of the lane: all of it, or the half before / from its recorded middle boundary
+    const bool split = mid != ~0ull;
+    if (half && !split) return;
+    const uint64_t mpos = mid & ((1ull << 40) - 1), mnb = mid >> 40;
+    const uint64_t my = o + before + s_off[t] - nb + (half ? mnb : 0);
+    const uint64_t want_nb = split ? (half ? nb - mnb : mnb) : nb;
     Bits br;
-    br.seek(S, lst[lane]);
-    const uint64_t stop = lane + 1 < L ? lst[lane + 1] : ~0ull;
+    br.seek(S, half ? mpos : lst[lane]);
+    const uint64_t stop = split && !half ? mpos : lane + 1 < L ? lst[lane + 1] : ~0ull;
     uint64_t x, got;
 #ifndef RDX_PINF_LANESTAT
 #define RDX_PINF_LANESTAT 0   // tuning builds: RDX_PINF_PROF also reports emit's slowest lane (costs scratch)
@@ -1651,10 +1669,10 @@ __device__ void emit_body(const PinfArgs &a) {
 #if RDX_PINF_LANESTAT
     uint32_t stat[3] = {0, 0, 0};
     const uint64_t tl = prof ? wall_clock64() : 0;
-    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + nb, prof ? stat : nullptr);
+    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + want_nb, prof ? stat : nullptr);
 #else
     uint32_t n_rec = 0;
-    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + nb, nullptr,
+    const uint32_t r = run_lane<true>(T, S, br, stop, a.end_bits, &x, &got, src, my, &a, my + want_nb, nullptr,
                                       (lds_u64p)s_rec + t, &n_rec);
     // the recorded matches (checked against the output bounds when they were decoded)
     for (uint32_t k = 0; k < n_rec; ++k) {
@@ -1671,8 +1689,8 @@ __device__ void emit_body(const PinfArgs &a) {
         }
     }
 #endif
-    const uint32_t want = lane + 1 < L ? 0u : 1u;
-    if (r != want || got != nb) atomicOr(&a.state->emit_err, 1u);
+    const uint32_t want = lane + 1 < L || (split && !half) ? 0u : 1u;
+    if (r != want || got != want_nb) atomicOr(&a.state->emit_err, 1u);
 #if RDX_PINF_LANESTAT
     if (prof) {   // the slowest lane: [2] its decode time (ticks), [5] symbols, [6] past the root, [7] L2 refills
         const uint64_t dt = wall_clock64() - tl;

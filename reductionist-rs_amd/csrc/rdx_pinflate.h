@@ -11,12 +11,13 @@ constexpr uint32_t kPinfMaxCand = 4096;   // block-start candidates per stream (
 #endif
 constexpr uint32_t kPinfLanes = RDX_PINF_LANES;   // decode lanes per block (k_pinf_block / k_pinf_emit)
 #ifndef RDX_PINF_EMIT_SPLIT
-#define RDX_PINF_EMIT_SPLIT 4
+#define RDX_PINF_EMIT_SPLIT 8
 #endif
 // k_pinf_emit workgroups per chain block: each re-decodes kPinfLanes / kPinfEmitSplit of its lanes on a CU
-// of its own (a block's lanes on one CU share its four SIMDs' issue slots)
+// of its own (a block's lanes on one CU share its four SIMDs' issue slots), two threads a lane — each half
+// from the symbol boundary k_pinf_block recorded at the lane's middle (PinfArgs::lmid)
 constexpr uint32_t kPinfEmitSplit = RDX_PINF_EMIT_SPLIT;
-static_assert(kPinfLanes % (64 * kPinfEmitSplit) == 0, "whole waves per emit workgroup");
+static_assert(kPinfLanes % (32 * kPinfEmitSplit) == 0, "whole waves per emit workgroup");
 constexpr uint32_t kPinfMaxParts = 1024;  // checksum segments
 constexpr uint64_t kPinfTabBytes = 11392;  // one block's decode tables (k_pinflate.hip Tabs)
 #ifndef RDX_PINF_TILE
@@ -66,6 +67,8 @@ struct PinfArgs {
     PinfBlk *blk;           // [kPinfMaxCand]
     uint64_t *lst;          // [kPinfMaxCand][kPinfLanes] lane starts
     uint32_t *lnb;          // [kPinfMaxCand][kPinfLanes] lane output bytes
+    uint64_t *lmid;         // [kPinfMaxCand][kPinfLanes] a lane's first symbol boundary at or past its middle
+                            //  (bit) | output bytes before it << 40; ~0: none recorded
     uint8_t *lens;          // [kPinfMaxCand][320] code lengths (k_pinf_find -> k_pinf_block)
     uint8_t *tabs;          // [kPinfMaxCand][kPinfTabBytes] decode tables (k_pinf_block -> k_pinf_emit)
     uint32_t *chain;        // [kPinfMaxCand] candidate of each chain block

@@ -699,12 +699,13 @@ constexpr uint64_t kPinfKeepSources = 256ull << 20;   // source entries kept bet
 rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_t *d_src, uint64_t len, hipStream_t s,
                            uint64_t *raw_len) {
     rdx_status st;
-    // arena: state | cand | blk | chain | coff | partial | lens | lnb | lst | tabs
+    // arena: state | cand | blk | chain | coff | partial | lens | lnb | lst | tabs | lmid
     constexpr uint64_t oState = 0, oCand = 256, oBlk = oCand + 8ull * kPinfMaxCand,
                        oChain = oBlk + sizeof(PinfBlk) * kPinfMaxCand, oCoff = oChain + 4ull * kPinfMaxCand,
                        oPart = oCoff + 8ull * kPinfMaxCand, oLens = oPart + 24ull * kPinfMaxParts,
                        oLnb = oLens + 320ull * kPinfMaxCand, oLst = oLnb + 4ull * kPinfMaxCand * kPinfLanes,
-                       oTabs = oLst + 8ull * kPinfMaxCand * kPinfLanes, oEnd = oTabs + kPinfTabBytes * kPinfMaxCand;
+                       oTabs = oLst + 8ull * kPinfMaxCand * kPinfLanes, oMid = oTabs + kPinfTabBytes * kPinfMaxCand,
+                       oEnd = oMid + 8ull * kPinfMaxCand * kPinfLanes;
     static_assert(sizeof(PinfState) <= 256, "state slot");
     if ((st = ensure(ws, ws->pinf, oEnd, s))) return st;
     if (!ws->pinf_back) RDX_HIP(hipHostMalloc((void **)&ws->pinf_back, sizeof(PinfState), hipHostMallocDefault));
@@ -728,6 +729,7 @@ rdx_status pinflate_stream(rdx_workspace *ws, uint32_t compression, const uint8_
     a.lnb = reinterpret_cast<uint32_t *>(ar + oLnb);
     a.lst = reinterpret_cast<uint64_t *>(ar + oLst);
     a.tabs = ar + oTabs;
+    a.lmid = reinterpret_cast<uint64_t *>(ar + oMid);
     if (tuning().pinflate_prof) {
         if ((st = ensure(ws, ws->pprof, 24ull * kPinfMaxCand, s))) return st;
         RDX_HIP(hipMemsetAsync(ws->pprof.p, 0, 192ull * kPinfMaxCand, s));
